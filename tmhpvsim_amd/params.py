@@ -1,0 +1,137 @@
+"""Model parameters for the batched simulator (plain data, no compute).
+
+Shape table
+    The six hourly cloud-cover step distributions of
+    tmhpvsim/data/mc_dist_shapes.csv as the reference LOADS them
+    (tmhpvsim/cloud_cover_hourly.py:278-288, pandas default float parser), bit
+    for bit (pinned by tests/test_oracle_golden.py against
+    tests/golden/functions.npz).  Bins are right-closed with right edges
+    EDGES; the draw uses the bin `searchsorted(EDGES, state)` (side='left',
+    cloud_cover_hourly.py:309,314).
+
+Site / PV system (tmhpvsim/pvmodel.py:12-30)
+    Munich: latitude 48.12, longitude 11.60, altitude 34 m, tilt = latitude,
+    surface azimuth 180, tz Europe/Berlin; pvlib's PVSystem default albedo
+    0.25; sapm_celltemp with wind 0, air 20 C (pvmodel.py:69-70).
+
+Module / inverter
+    pvmodel.py:13-17 names the SAM entries "Hanwha_HSL60P6_PA_4_250T__2013_"
+    (Sandia module DB) and "ABB__MICRO_0_25_I_OUTD_US_208_208V__CEC_2014_"
+    (CEC inverter DB).  Those databases ship with pvlib, which is absent from
+    this image (and unfetchable), so the numbers below are STAND-INS of the
+    right class (a 60-cell 250 W mc-Si module, a 250 W micro-inverter) and are
+    explicit, overridable inputs.  PV parity against pvlib is unpinned
+    (DESIGN.md); parity of the kernels against the C oracle is exact to 1e-12.
+
+Linke turbidity
+    pvlib's LinkeTurbidities.h5 lookup (clearsky.lookup_linke_turbidity) is
+    replaced by 12 monthly values (a central-European climatology stand-in),
+    interpolated by day of year exactly as pvlib 0.6.3 interpolates them.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+EDGES = (0.1, 0.3, 0.7, 0.9, 0.99, 1.0)
+# (loc, scale, kappa, df) per bin; kappa NaN for the Student-t bin, df NaN otherwise
+SHAPES = (
+    (-float.fromhex("0x1.e798442f368e5p-14"), float.fromhex("0x1.19aae076866b8p-5"),
+     float.fromhex("0x1.351825923f16fp-1"), math.nan),
+    (-float.fromhex("0x1.7743f483ff9e8p-5"), float.fromhex("0x1.bb2006b5fca1cp-4"),
+     float.fromhex("0x1.497ea156fd1cep-1"), math.nan),
+    (float.fromhex("0x1.fafdc82eeb650p-7"), float.fromhex("0x1.678f64b7b949dp-3"),
+     math.nan, float.fromhex("0x1.64d0cc399bf28p+3")),
+    (float.fromhex("0x1.3e4d683c0b176p-4"), float.fromhex("0x1.b16dba5381b9cp-4"),
+     float.fromhex("0x1.ae7e9badb2252p+0"), math.nan),
+    (float.fromhex("0x1.793a94312d8eap-6"), float.fromhex("0x1.55f53b6448c1bp-5"),
+     float.fromhex("0x1.ef7b16a3870c2p+0"), math.nan),
+    (float.fromhex("0x1.8e16c284b4885p-20"), float.fromhex("0x1.9d9a05656754dp-8"),
+     float.fromhex("0x1.1e66761d9c6e4p+1"), math.nan),
+)
+SHAPE_IS_T = (0, 0, 1, 0, 0, 0)
+
+# SAPM module parameter order used by the C-ABI (include/tmhpvsim.h, TMH_MOD_*)
+MODULE_KEYS = ("A0", "A1", "A2", "A3", "A4", "B0", "B1", "B2", "B3", "B4", "B5", "FD",
+               "Impo", "Vmpo", "Aimp", "C0", "C1", "C2", "C3", "Bvmpo", "Mbvmp", "N",
+               "Cells_in_Series", "temp_a", "temp_b", "temp_deltaT")
+MODULE_DEFAULT = dict(
+    A0=0.9381, A1=0.05402, A2=-0.009848, A3=0.0008356, A4=-2.712e-05,
+    B0=1.0, B1=-0.002438, B2=0.0003103, B3=-1.246e-05, B4=2.112e-07, B5=-1.359e-09,
+    FD=1.0, Impo=8.1, Vmpo=30.6, Aimp=-0.0002, C0=1.0118, C1=-0.0118, C2=0.1, C3=-8.0,
+    Bvmpo=-0.14, Mbvmp=0.0, N=1.1, Cells_in_Series=60.0,
+    # sapm_celltemp 'open_rack_cell_glassback' (pvlib 0.6.3)
+    temp_a=-3.47, temp_b=-0.0594, temp_deltaT=3.0,
+)
+INVERTER_KEYS = ("Paco", "Pdco", "Vdco", "Pso", "C0", "C1", "C2", "C3", "Pnt")
+INVERTER_DEFAULT = dict(Paco=250.0, Pdco=259.522, Vdco=40.2426, Pso=1.7716, C0=-4.1e-05,
+                        C1=-9.1e-05, C2=0.000494, C3=-0.013171, Pnt=0.075)
+LINKE_DEFAULT = (3.2, 3.4, 3.9, 4.3, 4.6, 4.9, 5.0, 4.8, 4.3, 3.8, 3.4, 3.2)
+
+CC_FAITHFUL = 0   # reference behaviour: fresh get_cloud_cover generator per hourly draw
+CC_MARKOV = 1     # the hourly Markov chain get_cloud_cover describes (persistent state)
+RNG_KEYED = 0     # counter-based Philox keyed by (chain, step, draw family)
+RNG_INJECTED = 1  # per-chain uniform stream consumed in reference order
+
+
+@dataclass
+class Site:
+    latitude: float = 48.12
+    longitude: float = 11.60
+    altitude: float = 34.0
+    tilt: float = 48.12
+    surface_azimuth: float = 180.0
+    albedo: float = 0.25
+    temp_air: float = 20.0
+    wind_speed: float = 0.0
+    tz: str = "Europe/Berlin"
+
+    def as_array(self):
+        return np.array([self.latitude, self.longitude, self.altitude, self.tilt,
+                         self.surface_azimuth, self.albedo, self.temp_air, self.wind_speed])
+
+
+@dataclass
+class ModelParams:
+    cc_mode: int = CC_FAITHFUL
+    rng_mode: int = RNG_KEYED
+    seed: int = 0x5EED
+    with_pv: bool = True
+    shapes: np.ndarray = field(default_factory=lambda: np.array(SHAPES, dtype=np.float64))
+    shape_is_t: tuple = SHAPE_IS_T
+    edges: tuple = EDGES
+    site: Site = field(default_factory=Site)
+    linke: tuple = LINKE_DEFAULT
+    module: dict = field(default_factory=lambda: dict(MODULE_DEFAULT))
+    inverter: dict = field(default_factory=lambda: dict(INVERTER_DEFAULT))
+
+    def module_array(self):
+        return np.array([self.module[k] for k in MODULE_KEYS], dtype=np.float64)
+
+    def inverter_array(self):
+        return np.array([self.inverter[k] for k in INVERTER_KEYS], dtype=np.float64)
+
+
+def load_shapes_csv(path):
+    """Load a shape table in the reference's mc_dist_shapes.csv format.
+
+    Uses pandas' default parser exactly like cloud_cover_hourly.py:282-288 so
+    the loaded bits equal the reference's.  Returns (shapes[6,4], is_t[6], edges[6]).
+    """
+    import pandas as pd
+    df = pd.read_csv(path, index_col=[0, 1])
+    shapes = np.full((len(df), 4), np.nan)
+    is_t = np.zeros(len(df), dtype=np.int32)
+    edges = np.array([iv[1] for iv in df.index], dtype=np.float64)
+    for i, (_, row) in enumerate(df.iterrows()):
+        shapes[i, 0], shapes[i, 1] = row["loc"], row["scale"]
+        if row["dist"] == "t":
+            is_t[i] = 1
+            shapes[i, 3] = row["df"]
+        elif row["dist"] == "al":
+            shapes[i, 2] = row["kappa"]
+        else:
+            raise NotImplementedError(f"distribution {row['dist']!r} is not implemented")
+    return shapes, is_t, edges
