@@ -1,0 +1,162 @@
+#!/usr/bin/env python3
+"""Benchmark: simulated chain-seconds/sec (BASELINE.json metric) on the C2 workload.
+
+Workload (BASELINE.json configs[1]): 4,096 independent chains
+(Munich site, Europe/Berlin clock) x one day (86,400 s) at 1 s, fp32 per-second
+arithmetic (fp64 Markov state), keyed Philox uniforms, trace mode: every
+chain-second's meter, pv and residual streamed to HBM (12 B / chain-second).
+One bench "step" = one batch: build the day's clock/geometry table, construct
+4,096 fresh chains (new global chain ids every step) and advance them 86,400 s.
+
+Multi-GPU (torchrun, one rank per GPU): weak scaling, every rank runs its own
+4,096 chains with distinct global ids; no data-path collective (chains are
+independent).  value = chain-seconds of all ranks / max rank time.
+
+Roofline: the dominant kernel (chain_kernel) is timed alone with HIP events on
+the stream it runs on; achieved = 12 B x chains x seconds per launch / mean
+launch time, against 8 TB/s.  cpu_baseline: the C oracle (oracle/tmh_oracle.c,
+"port") on a bounded sample of the same workload on this host, rank 0, N = 1.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+TRACE_BYTES = 12               # meter + pv + residual, fp32
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--chains", type=int, default=4096, help="chains per GPU")
+    ap.add_argument("--seconds", type=int, default=86400)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64"])
+    ap.add_argument("--mode", default="trace", choices=["trace", "stats"])
+    ap.add_argument("--start", default="2019-09-05 00:00:00")
+    ap.add_argument("--cpu-sample-chains", type=int, default=1024)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """The C oracle on a bounded sample of the same workload (same site/day/modes, fp64)."""
+    from oracle import oracle as O
+    from tmhpvsim_amd.params import ModelParams
+    threads = max(1, min(16, os.cpu_count() or 1))
+    n = args.cpu_sample_chains
+    O.run(ModelParams(), 0, 2, 600, args.start, tz="Europe/Berlin", n_threads=1)   # load + warm
+    t = time.perf_counter()
+    O.run(ModelParams(), 10 ** 9, n, args.seconds, args.start, tz="Europe/Berlin", n_threads=threads,
+          outputs=("residual",))
+    dt = time.perf_counter() - t
+    return {"value": n * args.seconds / dt, "unit": "chain-seconds/s", "cores": threads, "kind": "port",
+            "sample": f"{n} chains x {args.seconds} s (C2 site/day, fp64 C oracle, {threads} OpenMP threads, "
+                      f"{dt:.1f} s wall)"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from tmhpvsim_amd import _lib
+    from tmhpvsim_amd.engine import BatchedSim
+    from tmhpvsim_amd.params import ModelParams
+
+    L = _lib.load()
+    n, secs = args.chains, args.seconds
+    sim = BatchedSim(n, args.start, tz="Europe/Berlin", params=ModelParams(), precision=args.precision,
+                     chain0=rank * n, device=dev, horizon=secs)
+    real = sim.real
+    trace = {f: torch.empty(secs, n, dtype=real, device=dev) for f in ("pv", "meter", "residual")}
+    if args.mode == "stats":
+        sim.enable_stats()
+    st = sim._stats_struct()
+    tr = _lib.Trace(None, None, *(trace[f].data_ptr() if args.mode == "trace" else None
+                                  for f in ("pv", "meter", "residual")), n)
+    ws = sim.workspace(secs)
+    stream = torch.cuda.current_stream(dev)
+    sptr = C.c_void_p(stream.cuda_stream)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.warmup + args.steps)]
+
+    def one_step(k):
+        chain0 = (rank + k * world) * n                    # fresh global chains every batch
+        _lib.check(L.tmh_geometry(sim._eng, 0, secs, C.c_void_p(ws.data_ptr()), sptr))
+        _lib.check(L.tmh_init(sim._eng, C.c_void_p(sim.state.data_ptr()), chain0, n, None, sptr))
+        ev[k][0].record(stream)
+        _lib.check(L.tmh_step(sim._eng, C.c_void_p(sim.state.data_ptr()), chain0, n, 0, secs, None,
+                              C.byref(tr), C.byref(st) if st is not None else None,
+                              C.c_void_p(ws.data_ptr()), sptr))
+        ev[k][1].record(stream)
+
+    for k in range(args.warmup):
+        one_step(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.warmup, args.warmup + args.steps):
+        one_step(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [ev[k][0].elapsed_time(ev[k][1]) for k in range(args.warmup, args.warmup + args.steps)]
+    bad = int((sim.status() != 0).sum())
+    if world > 1:
+        t = torch.tensor([elapsed, sum(kern_ms) / len(kern_ms)], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kmean = float(t[0]), float(t[1])
+    else:
+        kmean = sum(kern_ms) / len(kern_ms)
+    chain_seconds = world * n * secs * args.steps
+    value = chain_seconds / elapsed
+    achieved = TRACE_BYTES * n * secs / (kmean / 1e3) / 1e9
+    line = {
+        "metric": "simulated chain-seconds/sec (node) at 1/2/4/8 GPUs + % HBM roofline",
+        "value": value, "unit": "chain-seconds/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic (keyed Philox)",
+        "config": {"workload": f"C2: {n} chains/GPU x {secs} s at 1 s, Munich, Europe/Berlin, "
+                               f"{args.start[:10]}, {args.mode} mode ({'meter+pv+residual fp32 trace' if args.mode == 'trace' else 'on-GPU stats'})",
+                   "chains_per_gpu": n, "seconds": secs, "parallelism": f"chains sharded over {world} GPU(s)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "chain_kernel", "kernel_ms": kmean,
+                     "bytes_per_launch": TRACE_BYTES * n * secs},
+        "faulted_chains": bad,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,180 @@
+/*
+ * tmhpvsim.h — C-ABI of the MI355X batched simulator for tmhpvsim's
+ * clear-sky-index chain + PV model (libtmhpvsim.so, gfx950).
+ *
+ * The reference (coroa/tmhpvsim) is pure Python; its per-step operator API is
+ *   ClearskyindexModel(time).next(time) -> float   tmhpvsim/clearskyindexmodel.py:57,128
+ *   PVModel(time).next(time) -> float              tmhpvsim/pvmodel.py:12,82
+ *   get_meter_value() -> float                     tmhpvsim/metersim.py:49
+ *   residual = meter - pv                          tmhpvsim/pvsim.py:83
+ * The Python package tmhpvsim_amd keeps those classes and signatures and binds
+ * this library with ctypes (tmhpvsim_amd/_lib.py); INTEGRATION.md shows the
+ * ctypes stub a reference maintainer would add.  Every entry point below
+ * replaces a batch of those per-step calls: one call advances N chains
+ * (chain = site x scenario) over a window of consecutive seconds.
+ *
+ * Conventions
+ *  - plain pointers and sizes only; every device buffer is allocated by the
+ *    caller (PyTorch-ROCm in tmhpvsim_amd) and passed as a raw device pointer.
+ *    The library allocates nothing persistent on the device.
+ *  - return 0 on success or a negative TMH_E_* code; never aborts; the last
+ *    error message of the calling thread is available from tmh_last_error().
+ *  - model faults that the reference raises as Python exceptions are reported
+ *    per chain in the state's status word (TMH_CHAIN_*); a faulted chain is
+ *    frozen and emits NaN (covered = 255) from the faulting step on.
+ *  - `stream` is a hipStream_t (NULL = default stream); all work is enqueued
+ *    asynchronously on it.  One engine per device; not re-entrant per engine.
+ */
+#ifndef TMHPVSIM_H
+#define TMHPVSIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TMH_ABI_VERSION 1
+
+/* ---- error codes ---- */
+#define TMH_OK 0
+#define TMH_E_INVAL (-1)
+#define TMH_E_HIP (-2)
+#define TMH_E_NOMEM (-3)
+#define TMH_E_STATE (-4)
+
+/* ---- per-chain status (the reference's exceptions) ---- */
+#define TMH_CHAIN_OK 0
+#define TMH_CHAIN_NAMEERROR_INIT 1  /* clearskyindexmodel.py:72-80 (undefined x, cc in [0.75,0.875)) */
+#define TMH_CHAIN_ASSERT_BINARY 2   /* cloud_cover_binary.py:90-98 (assert not recurse) */
+#define TMH_CHAIN_SIGMA_OVERFLOW 3  /* sigma arrays exceed TMH_SIGMA_CAP (no reference analogue) */
+#define TMH_CHAIN_U_EXHAUSTED 4     /* injected uniform stream ran out */
+
+/* ---- modes ---- */
+#define TMH_CC_FAITHFUL 0  /* reference: a fresh get_cloud_cover generator per hourly draw */
+#define TMH_CC_MARKOV 1    /* persistent 6-bin hourly Markov chain (cloud_cover_hourly.py:290-316) */
+#define TMH_RNG_KEYED 0    /* counter-based Philox4x32-10 keyed by (chain, step, draw family) */
+#define TMH_RNG_INJECTED 1 /* per-chain uniform stream, consumed in reference order */
+#define TMH_FP32 0         /* per-second CSI/PV/meter arithmetic in fp32 (Markov state stays fp64) */
+#define TMH_FP64 1         /* everything in fp64 */
+
+#define TMH_SIGMA_CAP 64   /* capacity of sigma_cloud / sigma_clear per chain */
+#define TMH_GEOM_FIELDS 20 /* doubles per step in the clock/geometry table */
+
+/* ---- SAPM module parameter order (tmh_params.module) ---- */
+enum {
+    TMH_MOD_A0 = 0, TMH_MOD_A4 = 4, TMH_MOD_B0 = 5, TMH_MOD_B5 = 10, TMH_MOD_FD = 11,
+    TMH_MOD_IMPO = 12, TMH_MOD_VMPO = 13, TMH_MOD_AIMP = 14, TMH_MOD_C0 = 15, TMH_MOD_C1 = 16,
+    TMH_MOD_C2 = 17, TMH_MOD_C3 = 18, TMH_MOD_BVMPO = 19, TMH_MOD_MBVMP = 20, TMH_MOD_N = 21,
+    TMH_MOD_NS = 22, TMH_MOD_TEMP_A = 23, TMH_MOD_TEMP_B = 24, TMH_MOD_TEMP_DT = 25,
+    TMH_MOD_COUNT = 26
+};
+/* ---- Sandia inverter order (tmh_params.inverter): Paco Pdco Vdco Pso C0 C1 C2 C3 Pnt ---- */
+#define TMH_INV_COUNT 9
+
+typedef struct tmh_params {
+    int32_t cc_mode;          /* TMH_CC_* */
+    int32_t rng_mode;         /* TMH_RNG_* */
+    int32_t precision;        /* TMH_FP32 / TMH_FP64 */
+    int32_t with_pv;          /* 0: pv = 0 (CSI-only runs, as ClearskyindexModel) */
+    uint64_t seed;            /* keyed Philox seed (the meter always draws keyed) */
+    double shapes[6][4];      /* loc, scale, kappa, df per cloud-cover bin (mc_dist_shapes.csv) */
+    int32_t shape_is_t[6];    /* 1: Student-t bin, 0: asymmetric Laplace */
+    double edges[6];          /* right edges of the bins */
+    double site[8];           /* lat, lon, altitude, tilt, surface azimuth, albedo, temp_air, wind */
+    double linke[12];         /* monthly Linke turbidity */
+    double module[TMH_MOD_COUNT];
+    double inverter[TMH_INV_COUNT];
+} tmh_params;
+
+/* Wall clock of a run.  Step s is the (s+1)-th call of ClearskyindexModel.next;
+ * the engine is constructed at the time of step 0 (clearskyindexmodel.py:57). */
+typedef struct tmh_clock {
+    int64_t utc0;            /* unix seconds of step 0 (solar geometry) */
+    int64_t local0;          /* local wall-clock seconds of step 0, counted from 1970-01-01 00:00 local */
+    int32_t n_shifts;        /* DST changes within the horizon (<= 8) */
+    int32_t reserved;
+    int64_t shift_step[8];   /* from this step on ... */
+    int32_t shift_delta[8];  /* ... local time is shifted by this many seconds (e.g. -3600) */
+} tmh_clock;
+
+/* Injected uniform streams: chain i (0-based within the call) reads
+ * u[i * stride + k] for its k-th draw, k < len.  Device pointer. */
+typedef struct tmh_ustream {
+    const double* u;
+    uint64_t stride;
+    uint64_t len;
+} tmh_ustream;
+
+/* Per-second traces, time-major: element (step j of the call, chain i) lives at
+ * [j * ld + i].  Real = float (TMH_FP32) or double (TMH_FP64).  Any may be NULL. */
+typedef struct tmh_trace {
+    void* csi;          /* clear-sky index (ClearskyindexModel.next) */
+    uint8_t* covered;   /* CloudCoverBinary bit (1 = the "covered" branch), 255 on fault */
+    void* pv;           /* AC power, W (PVModel.next) */
+    void* meter;        /* 9000 * U, W (get_meter_value) */
+    void* residual;     /* meter - pv, W (pvsim.py:83) */
+    uint64_t ld;        /* >= n_chains */
+} tmh_trace;
+
+/* On-GPU statistics, accumulated over calls (caller zero-initialises).  Device pointers. */
+typedef struct tmh_stats {
+    uint64_t* hist;     /* [n_bins] residual histogram, edge bins absorb out-of-range; NULL = off */
+    uint32_t n_bins;
+    uint32_t reserved;
+    double lo, hi;      /* histogram range, W */
+    double* chain_acc;  /* [4][n_chains] sum pv, sum meter, sum residual (W*s), max residual */
+} tmh_stats;
+
+int tmh_abi_version(void);
+const char* tmh_last_error(void);
+
+/* Chain state (structure of arrays, one element per chain per field). */
+size_t tmh_state_bytes(uint32_t n_chains);
+/* byte offsets of the TMH_STATE_NFIELDS fields (order documented in DESIGN.md) */
+#define TMH_STATE_NFIELDS 24
+int tmh_state_offsets(uint32_t n_chains, uint64_t* offsets);
+
+/* Workspace for tmh_run (clock/geometry table of the window) */
+size_t tmh_workspace_bytes(uint32_t n_steps);
+
+int tmh_engine_create(const tmh_params* params, const tmh_clock* clock, int device,
+                      struct tmh_engine** out);
+int tmh_engine_destroy(struct tmh_engine* eng);
+
+/* ClearskyindexModel.__init__ for chains [chain0, chain0 + n_chains): the 14+
+ * constructor draws and CloudCoverBinary's first cloud.  `inj` may be NULL
+ * (keyed mode). */
+int tmh_init(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains,
+             const tmh_ustream* inj, void* stream);
+
+/* Advance the chains over steps [step0, step0 + n_steps): per second the
+ * hourly/daily/minute resampling, the cloud-cover binary, the clear-sky index,
+ * the PV chain, the meter draw and the residual, fused.  Writes traces and/or
+ * accumulates statistics.  `workspace` holds tmh_workspace_bytes(n_steps). */
+int tmh_run(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains,
+            int64_t step0, uint32_t n_steps, const tmh_ustream* inj, const tmh_trace* trace,
+            const tmh_stats* stats, void* workspace, size_t workspace_bytes, void* stream);
+
+/* tmh_run without the table build: advance the chains over the window whose
+ * clock/geometry table `table` was built by tmh_geometry(step0, n_steps).  One
+ * table serves every chain batch of the same site and window. */
+int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains,
+             int64_t step0, uint32_t n_steps, const tmh_ustream* inj, const tmh_trace* trace,
+             const tmh_stats* stats, const void* table, void* stream);
+
+/* Build the clock/geometry table for steps [step0, step0 + n_steps) into
+ * `table` (tmh_workspace_bytes(n_steps) bytes: n_steps * TMH_GEOM_FIELDS
+ * doubles, then the fp32 copy). */
+int tmh_geometry(struct tmh_engine* eng, int64_t step0, uint32_t n_steps, double* table,
+                 void* stream);
+
+/* Device math probes for parity tests: out[i] = f(a, x[i]) with
+ * f = 0 ndtri, 1 gammaincinv, 2 stdtrit, 3 al_ppf, 4 ndtri (fp32 path). */
+int tmh_probe(int fn, double a, const double* x, double* out, uint32_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TMHPVSIM_H */

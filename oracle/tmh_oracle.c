@@ -683,6 +683,7 @@ int orc_run(const orc_params* P, uint64_t chain0, uint32_t n_chains, uint32_t n_
     if (P->with_pv) {
         G = (geom_t*)malloc(sizeof(geom_t) * (size_t)n_steps);
         if (!G) return -3;
+#pragma omp parallel for schedule(static) num_threads(P->n_threads > 0 ? P->n_threads : 1)
         for (uint32_t s = 0; s < n_steps; ++s)
             geometry(P, utc[s], cal[6 * s + 4], cal[6 * s + 5], &G[s]);
     }

@@ -1,0 +1,79 @@
+"""The C-ABI library without a GPU: it loads, exports every entry point that
+include/tmhpvsim.h declares, and its host-side logic (layout, validation)
+behaves.  No compute calls."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from tmhpvsim_amd import _lib
+from tmhpvsim_amd.params import ModelParams
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "tmhpvsim.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:[\w\s\*]+?)\b(tmh_\w+)\s*\(", src, re.M)))
+
+
+def test_exports_every_declared_symbol():
+    L = _lib.load()
+    syms = declared_symbols()
+    assert len(syms) >= 11, syms
+    for s in syms:
+        assert hasattr(L, s), f"{s} declared in include/tmhpvsim.h but not exported"
+    assert set(syms) == set(_lib.EXPORTS)
+
+
+def test_abi_version_and_layout():
+    L = _lib.load()
+    assert L.tmh_abi_version() == 1
+    for n in (1, 63, 64, 4096, 1 << 20):
+        off = _lib.state_offsets(n)
+        total = L.tmh_state_bytes(n)
+        assert (np.diff(off.astype(np.int64)) >= 0).all()
+        assert all(int(o) % 256 == 0 for o in off)
+        # sigma arrays hold CAP doubles per chain
+        assert int(off[21]) - int(off[20]) >= 8 * n * _lib.TMH_SIGMA_CAP
+        assert total >= int(off[21]) + 8 * n * _lib.TMH_SIGMA_CAP
+    assert L.tmh_workspace_bytes(86400) >= 86400 * 20 * 12
+
+
+def test_engine_create_validates_before_touching_device():
+    L = _lib.load()
+    ck = _lib.Clock()
+    eng = C.c_void_p()
+    for field, bad in (("cc_mode", 7), ("rng_mode", 9), ("precision", 3)):
+        P = _lib.make_params(ModelParams(), 0)
+        setattr(P, field, bad)
+        rc = L.tmh_engine_create(C.byref(P), C.byref(ck), 0, C.byref(eng))
+        assert rc == -1
+        assert field.split("_")[0] in L.tmh_last_error().decode()
+    ck.n_shifts = 99
+    P = _lib.make_params(ModelParams(), 0)
+    assert L.tmh_engine_create(C.byref(P), C.byref(ck), 0, C.byref(eng)) == -1
+    assert L.tmh_engine_create(None, C.byref(ck), 0, C.byref(eng)) == -1
+
+
+def test_null_arguments_rejected():
+    L = _lib.load()
+    assert L.tmh_init(None, None, 0, 1, None, None) == -1
+    assert L.tmh_run(None, None, 0, 1, 0, 1, None, None, None, None, 0, None) == -1
+    assert L.tmh_geometry(None, 0, 1, None, None) == -1
+    assert L.tmh_probe(0, 0.0, None, None, 1, None) == -1
+    assert L.tmh_state_offsets(4, None) == -1
+
+
+def test_params_struct_matches_header():
+    # tmh_params: 4 int32 + u64 + 24 + 6 int32 + 6 + 8 + 12 + 26 + 9 doubles
+    assert C.sizeof(_lib.Params) == 16 + 8 + 24 * 8 + 6 * 4 + 6 * 8 + 8 * 8 + 12 * 8 + 26 * 8 + 9 * 8
+    assert C.sizeof(_lib.Clock) == 8 + 8 + 4 + 4 + 64 + 32
+
+
+def test_no_cpu_fallback():
+    from tmhpvsim_amd.engine import BatchedSim
+    with pytest.raises(Exception):
+        BatchedSim(4, "2019-09-05 00:00:00", device="cpu")

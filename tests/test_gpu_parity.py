@@ -1,0 +1,187 @@
+"""GPU parity: the HIP kernels (through the C-ABI) against the C oracle and the
+reference's golden fixtures.
+
+Bars (DESIGN.md "Parity"):
+  * discrete Markov state (covered bit, uniforms consumed, fault status): bit-exact;
+  * fp64 kernel: every continuous output within 1e-12 relative (PV / residual
+    relative to max(|ref|, 1 W));
+  * fp32 kernel: within 1e-5 relative (same floor);
+  * reference fixtures (injected uniforms): CSI within 1e-12 relative.
+"""
+import numpy as np
+import pytest
+
+from golden_util import CHAIN_CASES, load, streams
+from oracle import oracle as O
+from tmhpvsim_amd.params import CC_MARKOV, RNG_INJECTED, SHAPES, ModelParams
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _sim(n, start, tz=None, mp=None, prec="fp64", chain0=0, inj=None, horizon=None):
+    from tmhpvsim_amd.engine import BatchedSim
+    return BatchedSim(n, start, tz=tz, params=mp or ModelParams(), precision=prec, chain0=chain0,
+                      device="cuda:0", injected=inj, horizon=horizon or 400 * 86400)
+
+
+def _np(t):
+    return t.double().cpu().numpy() if t.dtype != torch.uint8 else t.cpu().numpy()
+
+
+def _rel(got, ref, floor=1.0):
+    return np.abs(got - ref) / np.maximum(np.abs(ref), floor)
+
+
+# ------------------------------------------------------------------ device math
+def test_probe_math():
+    from tmhpvsim_amd.engine import probe
+    F = load("functions")
+    u = F["u"][(F["u"] >= 2.0 ** -53)]
+    np.testing.assert_allclose(probe(0, 0, u), O.ndtri(u), rtol=1e-14)
+    np.testing.assert_allclose(probe(1, 2.69, u), O.gammaincinv(2.69, u), rtol=1e-13)
+    np.testing.assert_allclose(probe(1, 3.5624, u), O.gammaincinv(3.5624, u), rtol=1e-13)
+    m = np.abs(u - 0.5) > 1e-9
+    np.testing.assert_allclose(probe(2, SHAPES[2][3], u[m]), O.stdtrit(SHAPES[2][3], u[m]), rtol=1e-12)
+    for b in (0, 1, 3, 4, 5):
+        np.testing.assert_allclose(probe(3, SHAPES[b][2], u), O.al_ppf(u, SHAPES[b][2]), rtol=1e-14)
+    z32 = probe(4, 0, u)
+    np.testing.assert_allclose(z32, O.ndtri(u), rtol=2e-6, atol=1e-6)
+
+
+# ------------------------------------------------------------------ reference fixtures
+@pytest.mark.parametrize("case", CHAIN_CASES)
+def test_injected_vs_reference_fixture(case):
+    d = load(case)
+    n = int(d["n_steps"])
+    chains = d["chains"]
+    mp = ModelParams(rng_mode=RNG_INJECTED, cc_mode=CC_MARKOV if bool(d["markov"]) else 0, with_pv=False)
+    sim = _sim(len(chains), str(d["start"]), tz=str(d["tz"]) or None, mp=mp, inj=streams(d), horizon=n)
+    out = sim.run(n, trace=("csi", "covered"))
+    csi, cov = _np(out["csi"]).T, _np(out["covered"]).T
+    ok = np.isfinite(d["csi"])
+    np.testing.assert_array_equal(np.isnan(csi), ~ok)
+    np.testing.assert_array_equal(cov[ok], d["covered"][ok])
+    assert (_rel(csi[ok], d["csi"][ok], 0) <= 1e-12).all()
+    codes = {"": 0, "NameError": 1, "AssertionError": 2}
+    assert list(sim.status()) == [codes[str(e)] for e in d["error"]]
+    pos = sim.state_field("pos").cpu().numpy().astype(np.int64)
+    good = sim.status() == 0
+    np.testing.assert_array_equal(pos[good], d["pos"][good, -1])
+
+
+# ------------------------------------------------------------------ keyed mode vs oracle
+CASES_KEYED = [
+    ("2019-09-05 00:00:00", "Europe/Berlin", 86400, 0),      # C2 day (scaled chains)
+    ("2019-10-27 00:00:00", "Europe/Berlin", 14400, 1),      # DST fall-back night
+    ("2019-06-21 03:00:00", None, 7200, 0),                  # naive clock, sunrise
+]
+
+
+@pytest.mark.parametrize("start,tz,steps,variant", CASES_KEYED)
+@pytest.mark.parametrize("prec", ["fp64", "fp32"])
+def test_keyed_vs_oracle(start, tz, steps, variant, prec):
+    n = 256 if steps <= 14400 else 128
+    mp = ModelParams(seed=0x5EED + variant)
+    ref = O.run(mp, 1000, n, steps, start, tz=tz, n_threads=8)
+    sim = _sim(n, start, tz=tz, mp=mp, prec=prec, chain0=1000, horizon=steps)
+    out = sim.run(steps)
+    assert (sim.status() == 0).all() and (ref["status"] == 0).all()
+    np.testing.assert_array_equal(_np(out["covered"]), ref["covered"])
+    tol = 1e-12 if prec == "fp64" else 1e-5
+    for f in ("csi", "pv", "meter", "residual"):
+        err = _rel(_np(out[f]), ref[f])
+        if prec == "fp32" and f in ("pv", "residual"):
+            # fp32 may flip the DISC kt <= 0.6 branch or the inverter p_dc < Pso cut on a
+            # handful of seconds; allow <= 1e-5 of points past tol, none past 1e-2 W/W
+            assert (err > tol).mean() <= 1e-5 and err.max() <= 1e-2, (f, err.max(), (err > tol).mean())
+        else:
+            assert err.max() <= tol, (f, err.max())
+
+
+def test_markov_keyed_vs_oracle():
+    mp = ModelParams(cc_mode=CC_MARKOV, seed=77)
+    n, steps, start = 128, 43200, "2019-09-05 06:00:00"
+    ref = O.run(mp, 0, n, steps, start, tz="Europe/Berlin", n_threads=8)
+    sim = _sim(n, start, tz="Europe/Berlin", mp=mp, horizon=steps)
+    out = sim.run(steps)
+    np.testing.assert_array_equal(sim.status(), ref["status"])
+    ok = ref["status"] == 0
+    np.testing.assert_array_equal(_np(out["covered"])[:, ok], ref["covered"][:, ok])
+    for f in ("csi", "pv", "residual"):
+        assert _rel(_np(out[f])[:, ok], ref[f][:, ok]).max() <= 1e-12
+
+
+def test_geometry_table_vs_oracle():
+    from tmhpvsim_amd.params import ModelParams
+    mp = ModelParams()
+    steps, start, tz = 86400, "2019-09-05 00:00:00", "Europe/Berlin"
+    sim = _sim(1, start, tz=tz, mp=mp, horizon=steps)
+    tab = sim.geometry(0, steps).cpu().numpy()
+    cal, utc = O.calendar(start, steps, tz)
+    P = O.make_params(mp)
+    import ctypes as C
+    idx = np.arange(0, steps, 97)
+    for s in idx:
+        g = np.zeros(16)
+        O.lib().orc_geometry(C.byref(P), int(utc[s]), int(cal[s, 4]), int(cal[s, 5]), g.ctypes.data_as(C.c_void_p))
+        # oracle geom_t order: cosz csi_max ghi_cs i0h i0 knc am disc_ok cos_zen rb dni_extra term2 gfac cos_aoi f1 f2
+        mine = tab[s, [4, 5, 6, 7, 8, 9, 10, 11, 4, 12, 13, 14, 15, 16, 17, 18]]
+        m = np.isfinite(g)
+        np.testing.assert_allclose(mine[m], g[m], rtol=1e-11, atol=1e-13)
+    np.testing.assert_array_equal(tab[:, 0], cal[:, 3] / 60.0)
+
+
+# ------------------------------------------------------------------ invariances
+def test_window_and_partition_invariance():
+    start, steps = "2019-09-05 10:00:00", 5000
+    a = _sim(128, start, tz="Europe/Berlin", prec="fp32", horizon=steps)
+    ra = a.run(steps, window=steps)
+    b = _sim(128, start, tz="Europe/Berlin", prec="fp32", horizon=steps)
+    parts = [b.run(k, window=333) for k in (1, 999, 4000)]
+    for f in ("csi", "pv", "covered", "residual"):
+        joined = torch.cat([p[f] for p in parts])
+        assert torch.equal(ra[f], joined), f
+    c0 = _sim(64, start, tz="Europe/Berlin", prec="fp32", horizon=steps)
+    c1 = _sim(64, start, tz="Europe/Berlin", prec="fp32", chain0=64, horizon=steps)
+    r0, r1 = c0.run(steps), c1.run(steps)
+    for f in ("csi", "pv", "covered", "residual"):
+        assert torch.equal(ra[f], torch.cat([r0[f], r1[f]], dim=1)), f
+
+
+def test_stats_match_trace():
+    start, steps, n = "2019-09-05 00:00:00", 20000, 512
+    s = _sim(n, start, tz="Europe/Berlin", prec="fp32", horizon=steps)
+    s.enable_stats(4096, -300.0, 9000.0)
+    out = s.run(steps, trace=("pv", "meter", "residual"))
+    res = out["residual"].double()
+    np.testing.assert_allclose(s.chain_acc[0].cpu().numpy(), out["pv"].double().sum(0).cpu().numpy(), rtol=1e-9)
+    np.testing.assert_allclose(s.chain_acc[2].cpu().numpy(), res.sum(0).cpu().numpy(), rtol=1e-9)
+    np.testing.assert_array_equal(s.chain_acc[3].cpu().numpy(), res.max(0).values.cpu().numpy())
+    x = ((res.cpu().numpy() - (-300.0)) * (4096 / 9300.0))
+    bins = np.clip(np.floor(x), 0, 4095).astype(np.int64)
+    np.testing.assert_array_equal(s.hist.cpu().numpy(), np.bincount(bins.ravel(), minlength=4096))
+
+
+# ------------------------------------------------------------------ full size (C2) properties
+def test_c2_full_size_properties():
+    """4,096 chains x 86,400 s, fp32: reference invariants + oracle spot checks."""
+    n, steps, start, tz = 4096, 86400, "2019-09-05 00:00:00", "Europe/Berlin"
+    sim = _sim(n, start, tz=tz, prec="fp32", horizon=steps)
+    out = sim.run(steps)
+    torch.cuda.synchronize()
+    assert (sim.status() == 0).all()
+    csi = out["csi"]
+    assert bool(((csi > 0) & (csi < 2)).all())                       # tests/test_clearskyindexmodel.py:13
+    assert bool((out["pv"] >= 0).all())                              # tests/test_pvmodel.py:10
+    assert bool(((out["meter"] >= 0) & (out["meter"] < 9000)).all())  # metersim.py:51
+    assert torch.equal(out["residual"], out["meter"] - out["pv"])    # pvsim.py:83
+    assert bool(out["covered"].le(1).all())
+    peak = out["pv"].max().item()
+    assert 0 < peak <= 250.0                                          # Paco of the micro-inverter
+    pick = [0, 1, 777, 2048, 4095]
+    for c in pick:
+        ref = O.run(ModelParams(), c, 1, steps, start, tz=tz)
+        np.testing.assert_array_equal(_np(out["covered"][:, c]), ref["covered"][:, 0])
+        assert _rel(_np(out["csi"][:, c]), ref["csi"][:, 0]).max() <= 1e-5

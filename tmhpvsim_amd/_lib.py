@@ -1,0 +1,135 @@
+"""ctypes binding of libtmhpvsim.so (include/tmhpvsim.h).
+
+The shared library is built in-tree (tmhpvsim_amd/build.py, driven by
+__graft_entry__.build()).  There is no CPU fallback: if the library is
+missing or fails to load, every compute entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libtmhpvsim.so")
+
+TMH_ABI_VERSION = 1
+TMH_SIGMA_CAP = 64
+TMH_GEOM_FIELDS = 20
+TMH_STATE_NFIELDS = 24
+TMH_FP32, TMH_FP64 = 0, 1
+CHAIN_STATUS = {0: "ok", 1: "NameError (init)", 2: "AssertionError (CloudCoverBinary)",
+                3: "sigma capacity exceeded", 4: "injected stream exhausted"}
+STATE_FIELDS = ["sb_cc", "sb_clear_day", "sb_cloudy_hour", "sb_cloudy_noise", "sb_clear_noise", "sb_ws",
+                "sa_cc", "sa_clear_day", "sa_cloudy_hour", "sa_cloudy_noise", "sa_clear_noise", "sa_ws",
+                "cloud_length", "clear_length", "markov_state", "sec", "sigma_len", "pos", "status",
+                "ncalls", "sigma_cloud", "sigma_clear", "reserved0", "reserved1"]
+STATE_DTYPES = {**{f: np.float64 for f in STATE_FIELDS[:15]}, "sec": np.int32, "sigma_len": np.int32,
+                "pos": np.uint32, "status": np.uint32, "ncalls": np.uint32, "sigma_cloud": np.float64,
+                "sigma_clear": np.float64}
+
+
+class Params(C.Structure):
+    _fields_ = [
+        ("cc_mode", C.c_int32), ("rng_mode", C.c_int32), ("precision", C.c_int32), ("with_pv", C.c_int32),
+        ("seed", C.c_uint64), ("shapes", (C.c_double * 4) * 6), ("shape_is_t", C.c_int32 * 6),
+        ("edges", C.c_double * 6), ("site", C.c_double * 8), ("linke", C.c_double * 12),
+        ("module", C.c_double * 26), ("inverter", C.c_double * 9),
+    ]
+
+
+class Clock(C.Structure):
+    _fields_ = [("utc0", C.c_int64), ("local0", C.c_int64), ("n_shifts", C.c_int32), ("reserved", C.c_int32),
+                ("shift_step", C.c_int64 * 8), ("shift_delta", C.c_int32 * 8)]
+
+
+class UStream(C.Structure):
+    _fields_ = [("u", C.c_void_p), ("stride", C.c_uint64), ("len", C.c_uint64)]
+
+
+class Trace(C.Structure):
+    _fields_ = [("csi", C.c_void_p), ("covered", C.c_void_p), ("pv", C.c_void_p), ("meter", C.c_void_p),
+                ("residual", C.c_void_p), ("ld", C.c_uint64)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("hist", C.c_void_p), ("n_bins", C.c_uint32), ("reserved", C.c_uint32), ("lo", C.c_double),
+                ("hi", C.c_double), ("chain_acc", C.c_void_p)]
+
+
+EXPORTS = ["tmh_abi_version", "tmh_last_error", "tmh_state_bytes", "tmh_state_offsets", "tmh_workspace_bytes",
+           "tmh_engine_create", "tmh_engine_destroy", "tmh_init", "tmh_run", "tmh_step", "tmh_geometry",
+           "tmh_probe"]
+
+_lib = None
+
+
+class TmhError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libtmhpvsim.so (raises if it is missing: no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(LIB_PATH)
+    p, u32, u64, i64, sz = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int64, C.c_size_t
+    L.tmh_abi_version.restype = C.c_int
+    L.tmh_last_error.restype = C.c_char_p
+    L.tmh_state_bytes.restype = sz
+    L.tmh_state_bytes.argtypes = [u32]
+    L.tmh_state_offsets.argtypes = [u32, p]
+    L.tmh_workspace_bytes.restype = sz
+    L.tmh_workspace_bytes.argtypes = [u32]
+    L.tmh_engine_create.argtypes = [C.POINTER(Params), C.POINTER(Clock), C.c_int, C.POINTER(p)]
+    L.tmh_engine_destroy.argtypes = [p]
+    L.tmh_init.argtypes = [p, p, u64, u32, C.POINTER(UStream), p]
+    L.tmh_run.argtypes = [p, p, u64, u32, i64, u32, C.POINTER(UStream), C.POINTER(Trace), C.POINTER(Stats), p, sz, p]
+    L.tmh_step.argtypes = [p, p, u64, u32, i64, u32, C.POINTER(UStream), C.POINTER(Trace), C.POINTER(Stats), p, p]
+    L.tmh_geometry.argtypes = [p, i64, u32, p, p]
+    L.tmh_probe.argtypes = [C.c_int, C.c_double, p, p, u32, p]
+    for name in ("tmh_state_offsets", "tmh_engine_create", "tmh_engine_destroy", "tmh_init", "tmh_run",
+                 "tmh_step", "tmh_geometry", "tmh_probe"):
+        getattr(L, name).restype = C.c_int
+    if L.tmh_abi_version() != TMH_ABI_VERSION:
+        raise ImportError(f"libtmhpvsim ABI {L.tmh_abi_version()} != {TMH_ABI_VERSION}")
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        raise TmhError(f"libtmhpvsim error {rc}: {load().tmh_last_error().decode()}")
+    return rc
+
+
+def state_offsets(n):
+    off = np.zeros(TMH_STATE_NFIELDS, dtype=np.uint64)
+    check(load().tmh_state_offsets(n, off.ctypes.data_as(C.c_void_p)))
+    return off
+
+
+def make_params(mp, precision):
+    """tmhpvsim_amd.params.ModelParams -> Params."""
+    P = Params()
+    P.cc_mode, P.rng_mode, P.precision = int(mp.cc_mode), int(mp.rng_mode), int(precision)
+    P.with_pv, P.seed = int(bool(mp.with_pv)), int(mp.seed) & (2 ** 64 - 1)
+    sh = np.asarray(mp.shapes, dtype=np.float64)
+    for i in range(6):
+        for j in range(4):
+            P.shapes[i][j] = sh[i, j]
+        P.shape_is_t[i] = int(mp.shape_is_t[i])
+        P.edges[i] = float(mp.edges[i])
+    for i, v in enumerate(mp.site.as_array()):
+        P.site[i] = v
+    for i, v in enumerate(mp.linke):
+        P.linke[i] = v
+    for i, v in enumerate(mp.module_array()):
+        P.module[i] = v
+    for i, v in enumerate(mp.inverter_array()):
+        P.inverter[i] = v
+    return P

@@ -1,0 +1,38 @@
+"""In-tree build of libtmhpvsim.so for gfx950 (hipcc, no JIT cache)."""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SRC = [os.path.join(HERE, "csrc", "tmh_engine.hip")]
+DEPS = SRC + [os.path.join(HERE, "csrc", "tmh_math.h"), os.path.join(ROOT, "include", "tmhpvsim.h")]
+LIB = os.path.join(HERE, "libtmhpvsim.so")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
+
+
+def hipcc():
+    for c in (os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc"), shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def build_lib(force=False, verbose=False):
+    if not force and os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(d) for d in DEPS):
+        return LIB
+    # -ffp-contract=off: no silent FMA contraction, so fp64 state arithmetic rounds
+    # exactly like the reference's numpy/Python scalar operations.
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+           "-I", os.path.join(ROOT, "include"), "-o", LIB + ".tmp"] + SRC
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build_lib(force=True, verbose=True))

@@ -1,0 +1,254 @@
+// Device math for the tmhpvsim kernels (gfx950).
+//
+// Random numbers: Philox4x32-10 (Random123 algorithm; counter layout in
+// DESIGN.md "Random numbers"), 52-bit midpoint uniforms u = (2k+1) 2^-53.
+// Variates: ONE uniform -> ONE variate by inverse CDF, the mapping the parity
+// harness applies to the reference:
+//   normal      ndtri(u)                      (scipy.stats.norm._rvs)
+//   gamma(a)    P^-1(a, u)                    (scipy.stats.gamma._rvs, np.random.gamma)
+//   t(df)       F_t^-1(df, u)                 (scipy.stats.t._rvs)
+//   AL(kappa)   cloud_cover_hourly.py:100-104 (generic rv_continuous._rvs)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tmh {
+
+// ---------------------------------------------------------------- Philox
+struct U4 {
+    uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                            uint32_t k0, uint32_t k1)
+{
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0;
+        c1 = lo1;
+        c2 = n2;
+        c3 = lo0;
+    }
+    return U4{c0, c1, c2, c3};
+}
+
+__device__ __forceinline__ double u52(uint32_t lo, uint32_t hi)
+{
+    const uint64_t v = ((uint64_t)hi << 32) | lo;
+    return (double)((v >> 11) | 1ull) * 0x1p-53;
+}
+
+// draw-family tags (ctr1 = tag << 28 | sub); must match oracle/philox.py
+enum : uint32_t {
+    TAG_STEP = 1,
+    TAG_BOUNDARY = 2,
+    TAG_CLOUD = 3,
+    TAG_INIT = 4,
+    TAG_INIT_CLOUD = 5,
+    TAG_INIT_SEC = 6
+};
+
+__device__ __forceinline__ U4 keyed_block(uint64_t seed, uint64_t chain, uint64_t step, uint32_t tag,
+                                          uint32_t sub)
+{
+    return philox4x32_10((uint32_t)step, (tag << 28) | (sub & 0x0FFFFFFFu), (uint32_t)chain,
+                         (uint32_t)(chain >> 32), (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+// ------------------------------------------------------------- variates
+// standard normal quantile (fp64).  ocml's ncdfinv, polished by one Halley
+// step on the erfc/erf residual so the result is within ~1 ulp of the exact
+// quantile (the oracle's and scipy's ndtri agree to ~1e-16).
+__device__ __forceinline__ double ndtri(double p)
+{
+    double x = normcdfinv(p);
+    if (!(p > 0.0) || !(p < 1.0)) return x;
+    const double q = p - 0.5;
+    double e;
+    if (fabs(q) < 0.25) e = 0.5 * erf(x * 0.70710678118654752440) - q;
+    else if (q < 0.0) e = 0.5 * erfc(-x * 0.70710678118654752440) - p;
+    else e = (1.0 - p) - 0.5 * erfc(x * 0.70710678118654752440);   // upper tail, 1-p exact
+    const double u = e * 2.50662827463100050242 * exp(0.5 * x * x);
+    return x - u / (1.0 + 0.5 * x * u);
+}
+
+// standard normal quantile from a fp64 uniform, fp32 arithmetic; the tail is
+// taken from min(u, 1-u) (exact in fp64) so u -> 1 keeps full relative precision.
+__device__ __forceinline__ float ndtri_f(double u)
+{
+    const double t = u < 0.5 ? u : 1.0 - u;
+    const float z = normcdfinvf((float)t);
+    return u < 0.5 ? z : -z;
+}
+
+__device__ inline void gamma_pq(double a, double x, double lga, double& P, double& Q)
+{
+    if (x <= 0.0) {
+        P = 0.0;
+        Q = 1.0;
+        return;
+    }
+    const double lpre = -x + a * log(x) - lga;
+    if (x < a + 1.0) {
+        double ap = a, sum = 1.0 / a, del = sum;
+        for (int n = 0; n < 1000; ++n) {
+            ap += 1.0;
+            del *= x / ap;
+            sum += del;
+            if (fabs(del) < fabs(sum) * 1e-17) break;
+        }
+        P = sum * exp(lpre);
+        Q = 1.0 - P;
+    } else {
+        double b = x + 1.0 - a, c = 1.0 / 1e-300, d = 1.0 / b, h = d;
+        for (int i = 1; i < 1000; ++i) {
+            const double an = -i * (i - a);
+            b += 2.0;
+            d = an * d + b;
+            if (fabs(d) < 1e-300) d = 1e-300;
+            c = b + an / c;
+            if (fabs(c) < 1e-300) c = 1e-300;
+            d = 1.0 / d;
+            const double del = d * c;
+            h *= del;
+            if (fabs(del - 1.0) < 1e-17) break;
+        }
+        Q = exp(lpre) * h;
+        P = 1.0 - Q;
+    }
+}
+
+// inverse regularized lower incomplete gamma (scipy.special.gammaincinv)
+__device__ inline double gammaincinv(double a, double p)
+{
+    if (!(p > 0.0)) return 0.0;
+    if (!(p < 1.0)) return INFINITY;
+    const bool upper = p >= 0.5;
+    const double target = upper ? 1.0 - p : p;
+    const double z = ndtri(p), s = 1.0 / (9.0 * a);
+    const double w = 1.0 - s + z * sqrt(s);
+    double x = a * w * w * w;
+    const double lg = lgamma(a);
+    if (!(x > 1e-3 * a)) x = exp((log(p) + lgamma(a + 1.0)) / a);
+    for (int it = 0; it < 100; ++it) {
+        double P, Q;
+        gamma_pq(a, x, lg, P, Q);
+        const double f = upper ? Q - target : P - target;
+        const double dens = exp(-x + (a - 1.0) * log(x) - lg);
+        if (dens == 0.0) break;
+        double t = f / dens;
+        if (upper) t = -t;
+        const double hstep = t / (1.0 - 0.5 * t * ((a - 1.0) / x - 1.0));
+        double xn = x - hstep;
+        if (xn <= 0.0) xn = 0.5 * x;
+        if (fabs(xn - x) <= 4e-16 * xn) {
+            x = xn;
+            break;
+        }
+        x = xn;
+    }
+    return x;
+}
+
+__device__ inline double betacf(double a, double b, double x)
+{
+    const double qab = a + b, qap = a + 1.0, qam = a - 1.0;
+    double c = 1.0, d = 1.0 - qab * x / qap;
+    if (fabs(d) < 1e-300) d = 1e-300;
+    d = 1.0 / d;
+    double h = d;
+    for (int m = 1; m < 10000; ++m) {
+        const int m2 = 2 * m;
+        double aa = m * (b - m) * x / ((qam + m2) * (a + m2));
+        d = 1.0 + aa * d;
+        if (fabs(d) < 1e-300) d = 1e-300;
+        c = 1.0 + aa / c;
+        if (fabs(c) < 1e-300) c = 1e-300;
+        d = 1.0 / d;
+        h *= d * c;
+        aa = -(a + m) * (qab + m) * x / ((a + m2) * (qap + m2));
+        d = 1.0 + aa * d;
+        if (fabs(d) < 1e-300) d = 1e-300;
+        c = 1.0 + aa / c;
+        if (fabs(c) < 1e-300) c = 1e-300;
+        d = 1.0 / d;
+        const double del = d * c;
+        h *= del;
+        if (fabs(del - 1.0) < 1e-16) break;
+    }
+    return h;
+}
+
+__device__ inline double ibeta(double a, double b, double x)
+{
+    if (x <= 0.0) return 0.0;
+    if (x >= 1.0) return 1.0;
+    const double lbt = lgamma(a + b) - lgamma(a) - lgamma(b) + a * log(x) + b * log1p(-x);
+    if (x < (a + 1.0) / (a + b + 2.0)) return exp(lbt) * betacf(a, b, x) / a;
+    return 1.0 - exp(lbt) * betacf(b, a, 1.0 - x) / b;
+}
+
+__device__ inline double t_resid(double df, double t, double p)
+{
+    const double t2 = t * t;
+    if (t2 < df) return (0.5 - p) - 0.5 * ibeta(0.5, 0.5 * df, t2 / (df + t2));
+    return 0.5 * ibeta(0.5 * df, 0.5, df / (df + t2)) - p;
+}
+
+// inverse Student-t CDF (scipy.special.stdtrit), lower half; upper by symmetry
+__device__ inline double stdtrit(double df, double p)
+{
+    if (!(p > 0.0)) return -INFINITY;
+    if (!(p < 1.0)) return INFINITY;
+    if (p == 0.5) return 0.0;
+    double sign = -1.0;
+    if (p > 0.5) {
+        p = 1.0 - p;
+        sign = 1.0;
+    }
+    const double lc = lgamma(0.5 * (df + 1.0)) - lgamma(0.5 * df) - 0.5 * log(df * 3.14159265358979323846);
+    double t;
+    if (p < 1e-5) {
+        t = -exp((lc + 0.5 * (df + 1.0) * log(df) - log(df) - log(p)) / df);
+    } else {
+        const double z = ndtri(p), z2 = z * z;
+        t = z + (z2 * z + z) / (4.0 * df) + (5.0 * z2 * z2 * z + 16.0 * z2 * z + 3.0 * z) / (96.0 * df * df);
+    }
+    if (t > -1e-300) t = -1e-300;
+    for (int it = 0; it < 200; ++it) {
+        const double f = t_resid(df, t, p);
+        const double ldens = lc - 0.5 * (df + 1.0) * log1p(t * t / df);
+        double tn;
+        if (t < -1e3) {
+            const double F = f + p;
+            const double slope = exp(ldens + log(-t) - log(F));
+            tn = -exp(log(-t) + log1p(f / p) / slope);
+        } else {
+            tn = t - f / exp(ldens);
+        }
+        if (tn >= 0.0) tn = 0.5 * t;
+        if (fabs(tn - t) <= 4e-16 * fabs(tn)) {
+            t = tn;
+            break;
+        }
+        t = tn;
+    }
+    return sign < 0.0 ? t : -t;
+}
+
+// asymmetric Laplace ppf, cloud_cover_hourly.py:100-104 (op order kept)
+__device__ __forceinline__ double al_ppf(double y, double kappa)
+{
+    const double k2 = kappa * kappa;
+    if (y < k2 / (1.0 + k2)) return kappa * log((1.0 + k2) / k2 * y);
+    return -1.0 / kappa * log((1.0 + k2) * (1.0 - y));
+}
+
+}  // namespace tmh

@@ -1,0 +1,197 @@
+"""Batched simulator: N chains (site x scenario) advanced on one MI355X.
+
+PyTorch-ROCm is used only for device memory and the stream; all compute runs
+in libtmhpvsim.so (HIP, gfx950) through the C-ABI of include/tmhpvsim.h.
+Chain state is a structure-of-arrays buffer owned by this object; traces are
+time-major [step, chain] tensors; statistics are accumulated on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from .clock import make_clock
+from .params import ModelParams, RNG_INJECTED
+
+TRACE_FIELDS = ("csi", "covered", "pv", "meter", "residual")
+DEFAULT_HIST = dict(n_bins=4096, lo=-300.0, hi=9000.0)
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+class BatchedSim:
+    """Advance chains [chain0, chain0 + n_chains) second by second.
+
+    Parameters
+    ----------
+    n_chains : chains on this device (each is one ClearskyindexModel + PVModel
+        + meter, tmhpvsim/clearskyindexmodel.py:44, pvmodel.py:11, metersim.py:49)
+    start : constructor time of every chain (datetime / str); step 0 = next(start)
+    tz : None (naive wall clock) or a zone name ("Europe/Berlin", as pvmodel.py:19)
+    params : tmhpvsim_amd.params.ModelParams (modes, seed, shape table, site, PV system)
+    precision : "fp32" (per-second CSI/PV math in fp32; Markov state fp64) or "fp64"
+    chain0 : global id of the first chain (keyed RNG -> partition-independent results)
+    injected : optional device tensor [n_chains, L] of uniforms (RNG_INJECTED mode)
+    horizon : maximum number of steps this object will run (sizes the DST table)
+    """
+
+    def __init__(self, n_chains, start, tz=None, params: ModelParams | None = None, precision="fp32",
+                 chain0=0, device=None, injected=None, horizon=400 * 86400):
+        torch = _torch()
+        L = _lib.load()
+        self.L = L
+        self.params = params or ModelParams()
+        self.n = int(n_chains)
+        self.chain0 = int(chain0)
+        self.precision = _lib.TMH_FP64 if precision in ("fp64", "f64", 64) else _lib.TMH_FP32
+        self.real = torch.float64 if self.precision == _lib.TMH_FP64 else torch.float32
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if self.device.type != "cuda":
+            raise ValueError("BatchedSim runs on a GPU device (there is no CPU path)")
+        self.horizon = int(horizon)
+        self.clock = make_clock(start, self.horizon, tz)
+        P = _lib.make_params(self.params, self.precision)
+        ck = self.clock.as_struct()
+        eng = C.c_void_p()
+        _lib.check(L.tmh_engine_create(C.byref(P), C.byref(ck), self.device.index or 0, C.byref(eng)))
+        self._eng = eng
+        self.state = torch.zeros(L.tmh_state_bytes(self.n), dtype=torch.uint8, device=self.device)
+        self._offsets = _lib.state_offsets(self.n)
+        self.injected = None
+        self._us = None
+        if self.params.rng_mode == RNG_INJECTED:
+            if injected is None:
+                raise ValueError("RNG_INJECTED mode needs `injected` uniforms [n_chains, L]")
+            inj = torch.as_tensor(injected, dtype=torch.float64, device=self.device).contiguous()
+            if inj.shape[0] != self.n:
+                raise ValueError("injected must have one row per chain")
+            self.injected = inj
+            self._us = _lib.UStream(inj.data_ptr(), inj.shape[1], inj.shape[1])
+        self.step = 0
+        self.hist = None
+        self.chain_acc = None
+        self._hist_spec = None
+        with torch.cuda.device(self.device):
+            _lib.check(L.tmh_init(self._eng, _ptr(self.state), self.chain0, self.n,
+                                  C.byref(self._us) if self._us is not None else None, self._stream()))
+
+    def _stream(self):
+        return C.c_void_p(_torch().cuda.current_stream(self.device).cuda_stream)
+
+    def __del__(self):
+        try:
+            if getattr(self, "_eng", None):
+                self.L.tmh_engine_destroy(self._eng)
+                self._eng = None
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ state
+    def state_field(self, name):
+        """Device view of one SoA state field ([n] or [TMH_SIGMA_CAP, n])."""
+        torch = _torch()
+        i = _lib.STATE_FIELDS.index(name)
+        dt = {np.float64: torch.float64, np.int32: torch.int32, np.uint32: torch.int32}[_lib.STATE_DTYPES[name]]
+        esz = 8 if dt == torch.float64 else 4
+        rows = _lib.TMH_SIGMA_CAP if name.startswith("sigma_c") else 1
+        o = int(self._offsets[i])
+        v = self.state[o:o + esz * self.n * rows].view(dt)
+        return v.view(rows, self.n) if rows > 1 else v
+
+    def status(self):
+        return self.state_field("status").cpu().numpy().astype(np.uint32)
+
+    # ------------------------------------------------------------------ stats
+    def enable_stats(self, n_bins=4096, lo=-300.0, hi=9000.0, histogram=True):
+        torch = _torch()
+        self._hist_spec = (int(n_bins), float(lo), float(hi), bool(histogram))
+        self.hist = torch.zeros(int(n_bins), dtype=torch.int64, device=self.device) if histogram else None
+        self.chain_acc = torch.zeros(4, self.n, dtype=torch.float64, device=self.device)
+        self.chain_acc[3].fill_(-float("inf"))
+
+    def _stats_struct(self):
+        if self.chain_acc is None:
+            return None
+        n_bins, lo, hi, _ = self._hist_spec
+        return _lib.Stats(self.hist.data_ptr() if self.hist is not None else None, n_bins, 0, lo, hi,
+                          self.chain_acc.data_ptr())
+
+    # ------------------------------------------------------------------ run
+    def workspace(self, n_steps):
+        return _torch().empty(self.L.tmh_workspace_bytes(n_steps), dtype=torch_uint8(), device=self.device)
+
+    def run(self, n_steps, trace=TRACE_FIELDS, window=86400, out=None):
+        """Advance n_steps seconds.  Returns {field: tensor[n_steps, n_chains]} for `trace`."""
+        torch = _torch()
+        n_steps = int(n_steps)
+        if self.step + n_steps > self.horizon:
+            raise ValueError(f"run beyond the horizon ({self.horizon} steps) given at construction")
+        trace = tuple(trace or ())
+        for f in trace:
+            if f not in TRACE_FIELDS:
+                raise ValueError(f"unknown trace field {f!r}")
+        res = out if out is not None else {}
+        for f in trace:
+            if f not in res:
+                dt = torch.uint8 if f == "covered" else self.real
+                res[f] = torch.empty(n_steps, self.n, dtype=dt, device=self.device)
+        st = self._stats_struct()
+        win = max(1, min(int(window), n_steps))
+        ws = self.workspace(win)
+        with torch.cuda.device(self.device):
+            done = 0
+            while done < n_steps:
+                k = min(win, n_steps - done)
+                tr = _lib.Trace(*(res[f][done:done + k].data_ptr() if f in trace else None
+                                  for f in ("csi", "covered", "pv", "meter", "residual")), self.n)
+                _lib.check(self.L.tmh_run(self._eng, _ptr(self.state), self.chain0, self.n, self.step + done, k,
+                                          C.byref(self._us) if self._us is not None else None,
+                                          C.byref(tr), C.byref(st) if st is not None else None,
+                                          _ptr(ws), ws.numel(), self._stream()))
+                done += k
+        self.step += n_steps
+        return res
+
+    def geometry(self, step0, n_steps):
+        torch = _torch()
+        ws = self.workspace(n_steps)
+        with torch.cuda.device(self.device):
+            _lib.check(self.L.tmh_geometry(self._eng, int(step0), int(n_steps), _ptr(ws), self._stream()))
+        return ws[: n_steps * _lib.TMH_GEOM_FIELDS * 8].view(torch.float64).view(n_steps, _lib.TMH_GEOM_FIELDS)
+
+    def stats_totals(self):
+        """Node-local totals: histogram, energy sums (W*s) and peak residual (W)."""
+        acc = self.chain_acc
+        ok = _torch().as_tensor(self.status() == 0, device=self.device)
+        tot = dict(
+            energy_pv=acc[0][ok].sum(), energy_meter=acc[1][ok].sum(), energy_residual=acc[2][ok].sum(),
+            peak_residual=acc[3][ok].max() if bool(ok.any()) else _torch().tensor(float("-inf"), device=self.device),
+        )
+        if self.hist is not None:
+            tot["hist"] = self.hist.clone()
+        return tot
+
+
+def torch_uint8():
+    return _torch().uint8
+
+
+def probe(fn, a, x, device="cuda"):
+    """Device math probe (parity tests): fn 0 ndtri, 1 gammaincinv, 2 stdtrit, 3 al_ppf, 4 ndtri fp32."""
+    torch = _torch()
+    L = _lib.load()
+    xt = torch.as_tensor(np.asarray(x, dtype=np.float64), device=device)
+    out = torch.empty_like(xt)
+    _lib.check(L.tmh_probe(int(fn), float(a), _ptr(xt), _ptr(out), xt.numel(),
+                           C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
