@@ -43,8 +43,9 @@ def parse():
     ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64"])
     ap.add_argument("--mode", default="trace", choices=["trace", "stats"])
     ap.add_argument("--start", default="2019-09-05 00:00:00")
-    ap.add_argument("--cpu-sample-chains", type=int, default=1024)
+    ap.add_argument("--cpu-sample-chains", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--path", default="auto", choices=["auto", "sequential", "time_parallel"])
     return ap.parse_args()
 
 
@@ -87,7 +88,7 @@ def main():
     L = _lib.load()
     n, secs = args.chains, args.seconds
     sim = BatchedSim(n, args.start, tz="Europe/Berlin", params=ModelParams(), precision=args.precision,
-                     chain0=rank * n, device=dev, horizon=secs)
+                     chain0=rank * n, device=dev, horizon=secs, kernel_path=args.path)
     real = sim.real
     trace = {f: torch.empty(secs, n, dtype=real, device=dev) for f in ("pv", "meter", "residual")}
     if args.mode == "stats":
@@ -95,7 +96,8 @@ def main():
     st = sim._stats_struct()
     tr = _lib.Trace(None, None, *(trace[f].data_ptr() if args.mode == "trace" else None
                                   for f in ("pv", "meter", "residual")), n)
-    ws = sim.workspace(secs)
+    plan = torch.empty(L.tmh_plan_bytes(secs), dtype=torch.uint8, device=dev)
+    scratch = torch.empty(L.tmh_scratch_bytes(n, secs), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     sptr = C.c_void_p(stream.cuda_stream)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -103,12 +105,12 @@ def main():
 
     def one_step(k):
         chain0 = (rank + k * world) * n                    # fresh global chains every batch
-        _lib.check(L.tmh_geometry(sim._eng, 0, secs, C.c_void_p(ws.data_ptr()), sptr))
+        _lib.check(L.tmh_plan(sim._eng, 0, secs, C.c_void_p(plan.data_ptr()), sptr))
         _lib.check(L.tmh_init(sim._eng, C.c_void_p(sim.state.data_ptr()), chain0, n, None, sptr))
         ev[k][0].record(stream)
         _lib.check(L.tmh_step(sim._eng, C.c_void_p(sim.state.data_ptr()), chain0, n, 0, secs, None,
                               C.byref(tr), C.byref(st) if st is not None else None,
-                              C.c_void_p(ws.data_ptr()), sptr))
+                              C.c_void_p(plan.data_ptr()), C.c_void_p(scratch.data_ptr()), scratch.numel(), sptr))
         ev[k][1].record(stream)
 
     for k in range(args.warmup):
@@ -146,7 +148,7 @@ def main():
                    "chains_per_gpu": n, "seconds": secs, "parallelism": f"chains sharded over {world} GPU(s)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "chain_kernel", "kernel_ms": kmean,
+                     "kernel": "tmh_step (" + sim.path + ")", "kernel_ms": kmean,
                      "bytes_per_launch": TRACE_BYTES * n * secs},
         "faulted_chains": bad,
     }

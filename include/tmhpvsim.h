@@ -50,6 +50,7 @@ extern "C" {
 #define TMH_CHAIN_ASSERT_BINARY 2   /* cloud_cover_binary.py:90-98 (assert not recurse) */
 #define TMH_CHAIN_SIGMA_OVERFLOW 3  /* sigma arrays exceed TMH_SIGMA_CAP (no reference analogue) */
 #define TMH_CHAIN_U_EXHAUSTED 4     /* injected uniform stream ran out */
+#define TMH_CHAIN_SEGMENT_OVERFLOW 5 /* > n_steps/8 + 64 cloud segments in one window (time-parallel path) */
 
 /* ---- modes ---- */
 #define TMH_CC_FAITHFUL 0  /* reference: a fresh get_cloud_cover generator per hourly draw */
@@ -58,8 +59,11 @@ extern "C" {
 #define TMH_RNG_INJECTED 1 /* per-chain uniform stream, consumed in reference order */
 #define TMH_FP32 0         /* per-second CSI/PV/meter arithmetic in fp32 (Markov state stays fp64) */
 #define TMH_FP64 1         /* everything in fp64 */
+#define TMH_PATH_AUTO 0          /* time-parallel when possible (keyed + faithful), else sequential */
+#define TMH_PATH_SEQUENTIAL 1    /* one work-item per chain, seconds in order */
+#define TMH_PATH_TIME_PARALLEL 2 /* segment pass + (chain x 256 s block) expansion */
 
-#define TMH_SIGMA_CAP 64   /* capacity of sigma_cloud / sigma_clear per chain */
+#define TMH_SIGMA_CAP 512  /* capacity of sigma_cloud / sigma_clear per chain (max seen: 132) */
 #define TMH_GEOM_FIELDS 20 /* doubles per step in the clock/geometry table */
 
 /* ---- SAPM module parameter order (tmh_params.module) ---- */
@@ -78,6 +82,8 @@ typedef struct tmh_params {
     int32_t rng_mode;         /* TMH_RNG_* */
     int32_t precision;        /* TMH_FP32 / TMH_FP64 */
     int32_t with_pv;          /* 0: pv = 0 (CSI-only runs, as ClearskyindexModel) */
+    int32_t kernel_path;      /* TMH_PATH_* */
+    int32_t reserved;
     uint64_t seed;            /* keyed Philox seed (the meter always draws keyed) */
     double shapes[6][4];      /* loc, scale, kappa, df per cloud-cover bin (mc_dist_shapes.csv) */
     int32_t shape_is_t[6];    /* 1: Student-t bin, 0: asymmetric Laplace */
@@ -136,12 +142,19 @@ size_t tmh_state_bytes(uint32_t n_chains);
 #define TMH_STATE_NFIELDS 24
 int tmh_state_offsets(uint32_t n_chains, uint64_t* offsets);
 
-/* Workspace for tmh_run (clock/geometry table of the window) */
-size_t tmh_workspace_bytes(uint32_t n_steps);
+/* Device buffers a window needs:
+ *  plan    (chain-independent): clock/geometry table, boundary events, block descriptors;
+ *  scratch (time-parallel path): segment records, window-end state, stats partials;
+ *  workspace = plan + scratch (tmh_run builds the plan itself). */
+size_t tmh_plan_bytes(uint32_t n_steps);
+size_t tmh_scratch_bytes(uint32_t n_chains, uint32_t n_steps);
+size_t tmh_workspace_bytes(uint32_t n_chains, uint32_t n_steps);
 
 int tmh_engine_create(const tmh_params* params, const tmh_clock* clock, int device,
                       struct tmh_engine** out);
 int tmh_engine_destroy(struct tmh_engine* eng);
+/* the kernel path the engine resolved (TMH_PATH_SEQUENTIAL or TMH_PATH_TIME_PARALLEL) */
+int tmh_engine_path(const struct tmh_engine* eng);
 
 /* ClearskyindexModel.__init__ for chains [chain0, chain0 + n_chains): the 14+
  * constructor draws and CloudCoverBinary's first cloud.  `inj` may be NULL
@@ -152,23 +165,23 @@ int tmh_init(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
 /* Advance the chains over steps [step0, step0 + n_steps): per second the
  * hourly/daily/minute resampling, the cloud-cover binary, the clear-sky index,
  * the PV chain, the meter draw and the residual, fused.  Writes traces and/or
- * accumulates statistics.  `workspace` holds tmh_workspace_bytes(n_steps). */
+ * accumulates statistics.  = tmh_plan + tmh_step on `workspace`
+ * (tmh_workspace_bytes(n_chains, n_steps) bytes). */
 int tmh_run(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains,
             int64_t step0, uint32_t n_steps, const tmh_ustream* inj, const tmh_trace* trace,
             const tmh_stats* stats, void* workspace, size_t workspace_bytes, void* stream);
 
-/* tmh_run without the table build: advance the chains over the window whose
- * clock/geometry table `table` was built by tmh_geometry(step0, n_steps).  One
- * table serves every chain batch of the same site and window. */
+/* Build the chain-independent plan of the window [step0, step0 + n_steps) into
+ * `plan` (tmh_plan_bytes(n_steps) bytes).  The first TMH_GEOM_FIELDS * n_steps
+ * doubles are the clock/geometry table (row layout in DESIGN.md).  One plan
+ * serves every chain batch of the same site and window. */
+int tmh_plan(struct tmh_engine* eng, int64_t step0, uint32_t n_steps, void* plan, void* stream);
+
+/* tmh_run on a plan built by tmh_plan(step0, n_steps) for this engine. */
 int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains,
              int64_t step0, uint32_t n_steps, const tmh_ustream* inj, const tmh_trace* trace,
-             const tmh_stats* stats, const void* table, void* stream);
-
-/* Build the clock/geometry table for steps [step0, step0 + n_steps) into
- * `table` (tmh_workspace_bytes(n_steps) bytes: n_steps * TMH_GEOM_FIELDS
- * doubles, then the fp32 copy). */
-int tmh_geometry(struct tmh_engine* eng, int64_t step0, uint32_t n_steps, double* table,
-                 void* stream);
+             const tmh_stats* stats, const void* plan, void* scratch, size_t scratch_bytes,
+             void* stream);
 
 /* Device math probes for parity tests: out[i] = f(a, x[i]) with
  * f = 0 ndtri, 1 gammaincinv, 2 stdtrit, 3 al_ppf, 4 ndtri (fp32 path). */

@@ -32,7 +32,15 @@
 #include <stdlib.h>
 #include <string.h>
 
-#define ORC_SIGMA_CAP 256
+#define ORC_SIGMA_CAP 4096
+
+/* diagnostics: histogram of len(sigma_cloud) after each successful next_cloud */
+static uint64_t g_Lhist[ORC_SIGMA_CAP + 1];
+void orc_L_hist(uint64_t* out, int reset)
+{
+    memcpy(out, g_Lhist, sizeof g_Lhist);
+    if (reset) memset(g_Lhist, 0, sizeof g_Lhist);
+}
 
 enum { ST_OK = 0, ST_NAMEERROR_INIT = 1, ST_ASSERT_BINARY = 2, ST_SIGMA_OVERFLOW = 3,
        ST_U_EXHAUSTED = 4 };
@@ -172,7 +180,7 @@ double orc_gammaincinv(double a, double p)
     double x = a * pow(1.0 - s + z * sqrt(s), 3.0);
     if (!(x > 1e-3 * a)) x = exp((log(p) + lgamma(a + 1.0)) / a);
     double lg = lgamma(a);
-    for (int it = 0; it < 100; ++it) {
+    for (int it = 0; it < 8; ++it) {   /* Halley from Wilson-Hilferty: 2-3 steps reach ~1 ulp */
         double P, Q;
         gamma_pq(a, x, &P, &Q);
         double f = upper ? Q - target : P - target;
@@ -183,7 +191,7 @@ double orc_gammaincinv(double a, double p)
         double h = t / (1.0 - 0.5 * t * ((a - 1.0) / x - 1.0));   /* Halley */
         double xn = x - h;
         if (xn <= 0.0) xn = 0.5 * x;
-        if (fabs(xn - x) <= 4e-16 * xn) { x = xn; break; }
+        if (fabs(xn - x) <= 1e-15 * xn) { x = xn; break; }
         x = xn;
     }
     return x;
@@ -259,7 +267,7 @@ double orc_stdtrit(double df, double p)
             tn = t - f / exp(ldens);
         }
         if (tn >= 0.0) tn = 0.5 * t;
-        if (fabs(tn - t) <= 4e-16 * fabs(tn)) { t = tn; break; }
+        if (fabs(tn - t) <= 1e-15 * fabs(tn)) { t = tn; break; }
         t = tn;
     }
     return t;
@@ -372,6 +380,8 @@ static int next_cloud(const ctx_t* X, chain_t* ch, uint64_t step, uint32_t tag, 
                 ch->sc[0] = cl;
                 ch->sl[0] = clr;
                 ch->L = last + 2;
+#pragma omp atomic
+                g_Lhist[ch->L] += 1;
                 ch->cl = cl;
                 ch->clr = clr;
                 ch->sec = 0;

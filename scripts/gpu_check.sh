@@ -12,7 +12,7 @@ python -c "import __graft_entry__ as g; g.build()" > "$OUT/build.log" 2>&1 || { 
 timeout -k 10 400 python __graft_entry__.py smoke > "$OUT/smoke.log" 2>&1; rc=$?
 echo "smoke rc=$rc"; tail -3 "$OUT/smoke.log"
 [ $rc -le 1 ] || exit $rc
-timeout -k 10 1500 python -m pytest tests -m gpu -q -p no:cacheprovider -rf > "$OUT/pytest_gpu.log" 2>&1; rc=$?
+timeout -k 10 700 python -m pytest tests -m gpu -q -p no:cacheprovider -rf > "$OUT/pytest_gpu.log" 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -15 "$OUT/pytest_gpu.log"
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 600 python bench.py --steps 3 --warmup 1 > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err"; rc=$?
@@ -21,5 +21,5 @@ echo "bench rc=$rc"; cat "$OUT/bench_$TAG.json"; tail -3 "$OUT/bench_$TAG.err"
 cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- \
     python "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/prof_$TAG.log" 2>&1; rc=$?
-echo "rocprof rc=$rc"; find "$OUT/prof_$TAG" -name '*stats*' | head
+echo "rocprof rc=$rc"; find "$OUT/prof_$TAG" -name "*stats*"
 exit $rc

@@ -22,7 +22,7 @@ def declared_symbols():
 def test_exports_every_declared_symbol():
     L = _lib.load()
     syms = declared_symbols()
-    assert len(syms) >= 11, syms
+    assert len(syms) >= 15, syms
     for s in syms:
         assert hasattr(L, s), f"{s} declared in include/tmhpvsim.h but not exported"
     assert set(syms) == set(_lib.EXPORTS)
@@ -39,19 +39,20 @@ def test_abi_version_and_layout():
         # sigma arrays hold CAP doubles per chain
         assert int(off[21]) - int(off[20]) >= 8 * n * _lib.TMH_SIGMA_CAP
         assert total >= int(off[21]) + 8 * n * _lib.TMH_SIGMA_CAP
-    assert L.tmh_workspace_bytes(86400) >= 86400 * 20 * 12
+    assert L.tmh_plan_bytes(86400) >= 86400 * 20 * 12
+    assert L.tmh_workspace_bytes(4096, 86400) == L.tmh_plan_bytes(86400) + L.tmh_scratch_bytes(4096, 86400)
 
 
 def test_engine_create_validates_before_touching_device():
     L = _lib.load()
     ck = _lib.Clock()
     eng = C.c_void_p()
-    for field, bad in (("cc_mode", 7), ("rng_mode", 9), ("precision", 3)):
+    for field, bad in (("cc_mode", 7), ("rng_mode", 9), ("precision", 3), ("kernel_path", 5)):
         P = _lib.make_params(ModelParams(), 0)
         setattr(P, field, bad)
         rc = L.tmh_engine_create(C.byref(P), C.byref(ck), 0, C.byref(eng))
         assert rc == -1
-        assert field.split("_")[0] in L.tmh_last_error().decode()
+        assert field in L.tmh_last_error().decode()
     ck.n_shifts = 99
     P = _lib.make_params(ModelParams(), 0)
     assert L.tmh_engine_create(C.byref(P), C.byref(ck), 0, C.byref(eng)) == -1
@@ -62,14 +63,16 @@ def test_null_arguments_rejected():
     L = _lib.load()
     assert L.tmh_init(None, None, 0, 1, None, None) == -1
     assert L.tmh_run(None, None, 0, 1, 0, 1, None, None, None, None, 0, None) == -1
-    assert L.tmh_geometry(None, 0, 1, None, None) == -1
+    assert L.tmh_step(None, None, 0, 1, 0, 1, None, None, None, None, None, 0, None) == -1
+    assert L.tmh_plan(None, 0, 1, None, None) == -1
+    assert L.tmh_engine_path(None) == -1
     assert L.tmh_probe(0, 0.0, None, None, 1, None) == -1
     assert L.tmh_state_offsets(4, None) == -1
 
 
 def test_params_struct_matches_header():
-    # tmh_params: 4 int32 + u64 + 24 + 6 int32 + 6 + 8 + 12 + 26 + 9 doubles
-    assert C.sizeof(_lib.Params) == 16 + 8 + 24 * 8 + 6 * 4 + 6 * 8 + 8 * 8 + 12 * 8 + 26 * 8 + 9 * 8
+    # tmh_params: 6 int32 + u64 + 24 + 6 int32 + 6 + 8 + 12 + 26 + 9 doubles
+    assert C.sizeof(_lib.Params) == 24 + 8 + 24 * 8 + 6 * 4 + 6 * 8 + 8 * 8 + 12 * 8 + 26 * 8 + 9 * 8
     assert C.sizeof(_lib.Clock) == 8 + 8 + 4 + 4 + 64 + 32
 
 

@@ -20,10 +20,10 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-def _sim(n, start, tz=None, mp=None, prec="fp64", chain0=0, inj=None, horizon=None):
+def _sim(n, start, tz=None, mp=None, prec="fp64", chain0=0, inj=None, horizon=None, kernel_path="auto"):
     from tmhpvsim_amd.engine import BatchedSim
     return BatchedSim(n, start, tz=tz, params=mp or ModelParams(), precision=prec, chain0=chain0,
-                      device="cuda:0", injected=inj, horizon=horizon or 400 * 86400)
+                      device="cuda:0", injected=inj, horizon=horizon or 400 * 86400, kernel_path=kernel_path)
 
 
 def _np(t):
@@ -32,6 +32,19 @@ def _np(t):
 
 def _rel(got, ref, floor=1.0):
     return np.abs(got - ref) / np.maximum(np.abs(ref), floor)
+
+
+def _err(field, got, ref):
+    """Relative error with the scale each output is conditioned on:
+    residual = meter - pv cancels, so it is measured against |meter| + |pv|."""
+    if field == "residual":
+        return np.abs(got["residual"] - ref["residual"]) / np.maximum(np.abs(ref["meter"]) + np.abs(ref["pv"]), 1.0)
+    return _rel(got[field], ref[field])
+
+
+def _where(err, tol):
+    i = np.unravel_index(np.argmax(err), err.shape)
+    return f"max {err.max():.3e} at step {i[0]} chain {i[1]}; {(err > tol).sum()} points > {tol}"
 
 
 # ------------------------------------------------------------------ device math
@@ -87,17 +100,21 @@ def test_keyed_vs_oracle(start, tz, steps, variant, prec):
     ref = O.run(mp, 1000, n, steps, start, tz=tz, n_threads=8)
     sim = _sim(n, start, tz=tz, mp=mp, prec=prec, chain0=1000, horizon=steps)
     out = sim.run(steps)
-    assert (sim.status() == 0).all() and (ref["status"] == 0).all()
+    np.testing.assert_array_equal(sim.status(), ref["status"])   # NameError chains (~1e-4) included
+    ok = ref["status"] == 0
     np.testing.assert_array_equal(_np(out["covered"]), ref["covered"])
     tol = 1e-12 if prec == "fp64" else 1e-5
+    got = {f: _np(out[f])[:, ok] for f in ("csi", "pv", "meter", "residual")}
+    rf = {f: ref[f][:, ok] for f in ("csi", "pv", "meter", "residual")}
     for f in ("csi", "pv", "meter", "residual"):
-        err = _rel(_np(out[f]), ref[f])
+        assert np.array_equal(np.isnan(_np(out[f])), np.isnan(ref[f])), f
+        err = _err(f, got, rf)
         if prec == "fp32" and f in ("pv", "residual"):
             # fp32 may flip the DISC kt <= 0.6 branch or the inverter p_dc < Pso cut on a
             # handful of seconds; allow <= 1e-5 of points past tol, none past 1e-2 W/W
-            assert (err > tol).mean() <= 1e-5 and err.max() <= 1e-2, (f, err.max(), (err > tol).mean())
+            assert (err > tol).mean() <= 1e-5 and err.max() <= 1e-2, (f, _where(err, tol))
         else:
-            assert err.max() <= tol, (f, err.max())
+            assert err.max() <= tol, (f, _where(err, tol), got["pv"][np.unravel_index(np.argmax(err), err.shape)])
 
 
 def test_markov_keyed_vs_oracle():
@@ -109,8 +126,11 @@ def test_markov_keyed_vs_oracle():
     np.testing.assert_array_equal(sim.status(), ref["status"])
     ok = ref["status"] == 0
     np.testing.assert_array_equal(_np(out["covered"])[:, ok], ref["covered"][:, ok])
+    got = {f: _np(out[f])[:, ok] for f in ("csi", "pv", "meter", "residual")}
+    rf = {f: ref[f][:, ok] for f in ("csi", "pv", "meter", "residual")}
     for f in ("csi", "pv", "residual"):
-        assert _rel(_np(out[f])[:, ok], ref[f][:, ok]).max() <= 1e-12
+        err = _err(f, got, rf)
+        assert err.max() <= 1e-12, (f, _where(err, 1e-12), got["pv"][np.unravel_index(np.argmax(err), err.shape)])
 
 
 def test_geometry_table_vs_oracle():
@@ -134,6 +154,13 @@ def test_geometry_table_vs_oracle():
 
 
 # ------------------------------------------------------------------ invariances
+def _same(a, b):
+    """bitwise equality with NaN == NaN (faulted chains emit NaN)"""
+    if a.dtype == torch.uint8:
+        return torch.equal(a, b)
+    return torch.equal(torch.nan_to_num(a, nan=-12345.0), torch.nan_to_num(b, nan=-12345.0))
+
+
 def test_window_and_partition_invariance():
     start, steps = "2019-09-05 10:00:00", 5000
     a = _sim(128, start, tz="Europe/Berlin", prec="fp32", horizon=steps)
@@ -142,12 +169,36 @@ def test_window_and_partition_invariance():
     parts = [b.run(k, window=333) for k in (1, 999, 4000)]
     for f in ("csi", "pv", "covered", "residual"):
         joined = torch.cat([p[f] for p in parts])
-        assert torch.equal(ra[f], joined), f
+        assert _same(ra[f], joined), f
     c0 = _sim(64, start, tz="Europe/Berlin", prec="fp32", horizon=steps)
     c1 = _sim(64, start, tz="Europe/Berlin", prec="fp32", chain0=64, horizon=steps)
     r0, r1 = c0.run(steps), c1.run(steps)
     for f in ("csi", "pv", "covered", "residual"):
-        assert torch.equal(ra[f], torch.cat([r0[f], r1[f]], dim=1)), f
+        assert _same(ra[f], torch.cat([r0[f], r1[f]], dim=1)), f
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp64"])
+def test_time_parallel_equals_sequential(prec):
+    """P1 segments + P2 (chain x 256 s) expansion == one-lane-per-chain sequential kernel, bit for bit,
+    over uneven windows crossing midnight and the DST fall-back (state carried between windows)."""
+    start, n = "2019-10-26 21:00:00", 192
+    windows = [7001, 30000, 1, 20000]
+    steps = sum(windows)
+    a = _sim(n, start, tz="Europe/Berlin", prec=prec, horizon=steps, kernel_path="time_parallel")
+    b = _sim(n, start, tz="Europe/Berlin", prec=prec, horizon=steps, kernel_path="sequential")
+    assert a.path == "time_parallel" and b.path == "sequential"
+    for w in windows:
+        ra, rb = a.run(w, window=w), b.run(w, window=w)
+        for f in ("csi", "covered", "pv", "meter", "residual"):
+            assert _same(ra[f], rb[f]), (w, f)
+    np.testing.assert_array_equal(a.status(), b.status())
+    for f in ("sb_cc", "sa_cc", "sb_clear_day", "sa_clear_day", "sb_cloudy_noise", "sa_clear_noise", "sa_ws",
+              "cloud_length", "clear_length", "sec", "sigma_len"):
+        assert _same(a.state_field(f), b.state_field(f)), f
+    L = a.state_field("sigma_len").long()
+    live = torch.arange(a.state_field("sigma_cloud").shape[1], device="cuda:0")[None, :] < L[:, None]
+    for f in ("sigma_cloud", "sigma_clear"):   # entries past len(sigma) are dead storage
+        assert torch.equal(a.state_field(f)[live], b.state_field(f)[live]), f
 
 
 def test_stats_match_trace():
@@ -155,6 +206,10 @@ def test_stats_match_trace():
     s = _sim(n, start, tz="Europe/Berlin", prec="fp32", horizon=steps)
     s.enable_stats(4096, -300.0, 9000.0)
     out = s.run(steps, trace=("pv", "meter", "residual"))
+    ok = torch.as_tensor(s.status() == 0, device="cuda:0")
+    for k in out:
+        out[k] = out[k][:, ok]
+    s.chain_acc = s.chain_acc[:, ok]
     res = out["residual"].double()
     np.testing.assert_allclose(s.chain_acc[0].cpu().numpy(), out["pv"].double().sum(0).cpu().numpy(), rtol=1e-9)
     np.testing.assert_allclose(s.chain_acc[2].cpu().numpy(), res.sum(0).cpu().numpy(), rtol=1e-9)
@@ -171,7 +226,10 @@ def test_c2_full_size_properties():
     sim = _sim(n, start, tz=tz, prec="fp32", horizon=steps)
     out = sim.run(steps)
     torch.cuda.synchronize()
-    assert (sim.status() == 0).all()
+    st = sim.status()
+    assert set(np.unique(st)) <= {0, 1} and (st == 1).mean() < 2e-3   # only the reference's NameError
+    ok = torch.as_tensor(st == 0, device="cuda:0")
+    out = {k: v[:, ok] for k, v in out.items()}
     csi = out["csi"]
     assert bool(((csi > 0) & (csi < 2)).all())                       # tests/test_clearskyindexmodel.py:13
     assert bool((out["pv"] >= 0).all())                              # tests/test_pvmodel.py:10
@@ -180,8 +238,9 @@ def test_c2_full_size_properties():
     assert bool(out["covered"].le(1).all())
     peak = out["pv"].max().item()
     assert 0 < peak <= 250.0                                          # Paco of the micro-inverter
-    pick = [0, 1, 777, 2048, 4095]
+    pick = [c for c in (0, 1, 777, 2048, 4095) if st[c] == 0]
+    cols = {c: int(np.nonzero(st == 0)[0].tolist().index(c)) for c in pick}
     for c in pick:
         ref = O.run(ModelParams(), c, 1, steps, start, tz=tz)
-        np.testing.assert_array_equal(_np(out["covered"][:, c]), ref["covered"][:, 0])
-        assert _rel(_np(out["csi"][:, c]), ref["csi"][:, 0]).max() <= 1e-5
+        np.testing.assert_array_equal(_np(out["covered"][:, cols[c]]), ref["covered"][:, 0])
+        assert _rel(_np(out["csi"][:, cols[c]]), ref["csi"][:, 0]).max() <= 1e-5

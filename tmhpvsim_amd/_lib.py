@@ -12,15 +12,17 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libtmhpvsim.so")
+LIB_PATH = os.environ.get("TMHPVSIM_LIB") or os.path.join(HERE, "libtmhpvsim.so")
 
 TMH_ABI_VERSION = 1
-TMH_SIGMA_CAP = 64
+TMH_SIGMA_CAP = 512
 TMH_GEOM_FIELDS = 20
 TMH_STATE_NFIELDS = 24
 TMH_FP32, TMH_FP64 = 0, 1
+PATH_AUTO, PATH_SEQUENTIAL, PATH_TIME_PARALLEL = 0, 1, 2
 CHAIN_STATUS = {0: "ok", 1: "NameError (init)", 2: "AssertionError (CloudCoverBinary)",
-                3: "sigma capacity exceeded", 4: "injected stream exhausted"}
+                3: "sigma capacity exceeded", 4: "injected stream exhausted",
+                5: "segment capacity exceeded"}
 STATE_FIELDS = ["sb_cc", "sb_clear_day", "sb_cloudy_hour", "sb_cloudy_noise", "sb_clear_noise", "sb_ws",
                 "sa_cc", "sa_clear_day", "sa_cloudy_hour", "sa_cloudy_noise", "sa_clear_noise", "sa_ws",
                 "cloud_length", "clear_length", "markov_state", "sec", "sigma_len", "pos", "status",
@@ -33,7 +35,7 @@ STATE_DTYPES = {**{f: np.float64 for f in STATE_FIELDS[:15]}, "sec": np.int32, "
 class Params(C.Structure):
     _fields_ = [
         ("cc_mode", C.c_int32), ("rng_mode", C.c_int32), ("precision", C.c_int32), ("with_pv", C.c_int32),
-        ("seed", C.c_uint64), ("shapes", (C.c_double * 4) * 6), ("shape_is_t", C.c_int32 * 6),
+        ("kernel_path", C.c_int32), ("reserved", C.c_int32), ("seed", C.c_uint64), ("shapes", (C.c_double * 4) * 6), ("shape_is_t", C.c_int32 * 6),
         ("edges", C.c_double * 6), ("site", C.c_double * 8), ("linke", C.c_double * 12),
         ("module", C.c_double * 26), ("inverter", C.c_double * 9),
     ]
@@ -58,9 +60,9 @@ class Stats(C.Structure):
                 ("hi", C.c_double), ("chain_acc", C.c_void_p)]
 
 
-EXPORTS = ["tmh_abi_version", "tmh_last_error", "tmh_state_bytes", "tmh_state_offsets", "tmh_workspace_bytes",
-           "tmh_engine_create", "tmh_engine_destroy", "tmh_init", "tmh_run", "tmh_step", "tmh_geometry",
-           "tmh_probe"]
+EXPORTS = ["tmh_abi_version", "tmh_last_error", "tmh_state_bytes", "tmh_state_offsets", "tmh_plan_bytes",
+           "tmh_scratch_bytes", "tmh_workspace_bytes", "tmh_engine_create", "tmh_engine_destroy", "tmh_engine_path",
+           "tmh_init", "tmh_run", "tmh_plan", "tmh_step", "tmh_probe"]
 
 _lib = None
 
@@ -74,6 +76,12 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
+    # torch first: the library must bind to the HIP runtime torch already uses
+    # (one libamdhip64 per process), never load a second one ahead of it.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
     L = C.CDLL(LIB_PATH)
@@ -83,17 +91,23 @@ def load():
     L.tmh_state_bytes.restype = sz
     L.tmh_state_bytes.argtypes = [u32]
     L.tmh_state_offsets.argtypes = [u32, p]
+    L.tmh_plan_bytes.restype = sz
+    L.tmh_plan_bytes.argtypes = [u32]
+    L.tmh_scratch_bytes.restype = sz
+    L.tmh_scratch_bytes.argtypes = [u32, u32]
     L.tmh_workspace_bytes.restype = sz
-    L.tmh_workspace_bytes.argtypes = [u32]
+    L.tmh_workspace_bytes.argtypes = [u32, u32]
+    L.tmh_engine_path.argtypes = [p]
     L.tmh_engine_create.argtypes = [C.POINTER(Params), C.POINTER(Clock), C.c_int, C.POINTER(p)]
     L.tmh_engine_destroy.argtypes = [p]
     L.tmh_init.argtypes = [p, p, u64, u32, C.POINTER(UStream), p]
     L.tmh_run.argtypes = [p, p, u64, u32, i64, u32, C.POINTER(UStream), C.POINTER(Trace), C.POINTER(Stats), p, sz, p]
-    L.tmh_step.argtypes = [p, p, u64, u32, i64, u32, C.POINTER(UStream), C.POINTER(Trace), C.POINTER(Stats), p, p]
-    L.tmh_geometry.argtypes = [p, i64, u32, p, p]
+    L.tmh_step.argtypes = [p, p, u64, u32, i64, u32, C.POINTER(UStream), C.POINTER(Trace), C.POINTER(Stats), p, p,
+                           sz, p]
+    L.tmh_plan.argtypes = [p, i64, u32, p, p]
     L.tmh_probe.argtypes = [C.c_int, C.c_double, p, p, u32, p]
-    for name in ("tmh_state_offsets", "tmh_engine_create", "tmh_engine_destroy", "tmh_init", "tmh_run",
-                 "tmh_step", "tmh_geometry", "tmh_probe"):
+    for name in ("tmh_state_offsets", "tmh_engine_create", "tmh_engine_destroy", "tmh_engine_path", "tmh_init",
+                 "tmh_run", "tmh_step", "tmh_plan", "tmh_probe"):
         getattr(L, name).restype = C.c_int
     if L.tmh_abi_version() != TMH_ABI_VERSION:
         raise ImportError(f"libtmhpvsim ABI {L.tmh_abi_version()} != {TMH_ABI_VERSION}")
@@ -113,9 +127,10 @@ def state_offsets(n):
     return off
 
 
-def make_params(mp, precision):
+def make_params(mp, precision, kernel_path=PATH_AUTO):
     """tmhpvsim_amd.params.ModelParams -> Params."""
     P = Params()
+    P.kernel_path = int(kernel_path)
     P.cc_mode, P.rng_mode, P.precision = int(mp.cc_mode), int(mp.rng_mode), int(precision)
     P.with_pv, P.seed = int(bool(mp.with_pv)), int(mp.seed) & (2 ** 64 - 1)
     sh = np.asarray(mp.shapes, dtype=np.float64)

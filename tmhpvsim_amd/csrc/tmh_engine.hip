@@ -1,23 +1,29 @@
 // libtmhpvsim — MI355X (gfx950) batched simulator of tmhpvsim's clear-sky-index
 // chain + PV model behind the C-ABI of include/tmhpvsim.h.
 //
-// One work-item per chain (site x scenario).  Chain state lives in registers
-// across the in-kernel time loop and in structure-of-arrays HBM buffers
-// between calls (every per-lane access is coalesced: element = field[chain]).
-// Everything that is the same for all chains at a given second (wall-clock
-// fractions, boundary flags, solar geometry, clear-sky irradiance, SAPM
-// spectral/AOI factors) is computed once per second by geom_kernel into a
-// table that the chain kernel reads with wave-uniform (scalar) loads.
+// Two execution paths over the same model code (tmh_model.h):
 //
-// Reference lines restated (tmhpvsim/...):
-//   clearskyindexmodel.py:12-40   InterpolatedSampler (interp op order kept)
-//   clearskyindexmodel.py:57-99   constructor draw sequence      -> init_kernel
-//   clearskyindexmodel.py:101-126 day/hour/minute resampling     -> chain_kernel
-//   clearskyindexmodel.py:128-160 per-second CSI                 -> chain_kernel
-//   cloud_cover_binary.py:25-117  cloud lengths, CloudCoverBinary-> next_cloud
-//   cloud_cover_hourly.py:100-104,290-316 hourly cover draw      -> draw_cc
-//   pvmodel.py:50-80              PV chain (pvlib 0.6.3 models)  -> geom_kernel + pv_power
-//   metersim.py:49-51, pvsim.py:83 meter + residual              -> chain_kernel
+//  * sequential (chain_kernel): one work-item per chain runs the seconds of a
+//    window in order, exactly like ClearskyindexModel.next.  Used for injected
+//    uniform streams (the reference's consumption order is data dependent) and
+//    for the markov cloud-cover mode.
+//
+//  * time-parallel (keyed Philox, faithful mode): the only data-dependent
+//    sequential process is CloudCoverBinary's cloud/clear segment sequence.
+//      P1 segments_kernel: one wavefront per chain walks from segment end to
+//         segment end (next_cloud with the sigma scan spread over 64 lanes and
+//         a butterfly argmin) and records each segment as (first clear step,
+//         next call step).
+//      P2 expand_kernel: one work-item per (chain, block of 256 seconds)
+//         rebuilds the sampler state at the block start from the keyed draws
+//         of the last boundary events (block descriptors), then runs the fused
+//         per-second body.  Every draw is keyed by (chain, step), so P2's
+//         outputs are bit-identical to the sequential kernel's.
+//
+// Per-window, chain-independent work (wall-clock fractions, boundary flags,
+// solar geometry, clear-sky irradiance, SAPM spectral/AOI factors, the boundary
+// event list and block descriptors) is built once by the plan kernels and read
+// by the chain kernels with wave-uniform loads.
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -28,229 +34,45 @@
 #include <string>
 
 #include "tmh_math.h"
+#include "tmh_model.h"
 #include "tmhpvsim.h"
 
 using namespace tmh;
 
-#define CAP TMH_SIGMA_CAP
-#define ROW TMH_GEOM_FIELDS
-
 namespace {
 
-// ------------------------------------------------------------ parameters
-struct KParams {
-    int32_t cc_mode, rng_mode, with_pv, precision;
-    uint64_t seed;
-    double shapes[6][4];
-    int32_t is_t[6];
-    double edges[6];
-    double module[TMH_MOD_COUNT];
-    double inverter[TMH_INV_COUNT];
-    double alpha, delta, expo, sqrt09, sqrt6;   // cloud_cover_binary.py:35-40, scales
-    double temp_air, wind;                      // sapm_celltemp inputs (pvmodel.py:69-70)
+constexpr int BLOCK_STEPS = 256;   // seconds per P2 work-item
+
+struct BlockDesc {                 // as of the step before the block start; -1 = none in the window
+    int32_t q0, q1;                // minute-draw indices of the last two minute boundaries
+    int32_t h0, h1;                // event indices of the last two hour boundaries
+    int32_t cd0, cd1;              // last two clear_day pushes: event index * 2 + (0 day | 1 hour push)
+    int32_t evi;                   // first event index at or after the block start
+    int32_t pad;
 };
 
-struct GParams {
-    double site[8];
-    double linke[12];
-    double module[TMH_MOD_COUNT];
-    tmh_clock clock;
+struct SegView {                   // P1 -> P2 scratch
+    int2* rec;                     // [n][cap] (first uncovered step, next call step), global steps
+    uint32_t cap;
+    uint32_t* count;               // [n]
+    int32_t* fault;                // [n] window-relative fault step (INT_MAX = none)
+    uint32_t* status;              // [n] status after the window
+    double* end_p1;                // [4][n] cc before/after, ws before/after at window end
+    double* end_p2;                // [6][n] clear_day, cloudy_noise, clear_noise pairs at window end
+    double* part;                  // [4][nblk][n] stats partials
+    uint32_t nblk;
+    double* evd;                   // [ev_cap][4][n] per boundary event: cc, ws, clear_day (day), clear_day (hour)
+    double* mind;                  // [nmin][2][n] per minute boundary: cloudy noise, clear noise
+    uint32_t evcap, nmin;
 };
 
-enum : uint32_t { FL_DAY = 1, FL_HOUR = 2, FL_MIN = 4, FL_NIGHT = 8 };
-// geometry table row (TMH_GEOM_FIELDS = 20)
-enum {
-    G_MINF = 0, G_HOURF = 1, G_DAYF = 2, G_FLAGS = 3, G_COSZ = 4, G_CSIMAX = 5, G_GHICS = 6,
-    G_I0H = 7, G_I0 = 8, G_KNC = 9, G_AM = 10, G_DISCOK = 11, G_RB = 12, G_DNIEXTRA = 13,
-    G_TERM2 = 14, G_GFAC = 15, G_COSAOI = 16, G_F1 = 17, G_F2 = 18
-};
-
-struct StateView {
-    double* sb[6];
-    double* sa[6];
-    double *cl, *clr, *mstate;
-    int32_t *sec, *L;
-    uint32_t *pos, *status, *ncalls;
-    double *sc, *sl;   // [CAP][n]
-    uint32_t n;
-};
-
-struct InjView {
-    const double* u;
-    uint64_t stride, len;
-};
-
-struct TraceView {
-    void *csi, *pv, *meter, *residual;
-    uint8_t* covered;
-    uint64_t ld;
-};
-
-struct StatsView {
-    uint64_t* hist;
-    uint32_t n_bins;
-    double lo, scale;
-    double* acc;
-};
-
-enum { S_CC = 0, S_CLEAR_DAY = 1, S_CLOUDY_HOUR = 2, S_CLOUDY_NOISE = 3, S_CLEAR_NOISE = 4, S_WS = 5 };
-
-struct Chain {
-    double sb[6], sa[6];
-    double cl, clr, mstate;
-    int32_t sec, L, t1, t2;
-    uint32_t pos, status, ncalls;
-};
-
-// ------------------------------------------------------------ rng sources
-template <int RNG>
-struct Draw;
-
-template <>
-struct Draw<TMH_RNG_KEYED> {
-    uint64_t seed, chain;
-    __device__ __forceinline__ double one(Chain&, uint64_t step, uint32_t tag, uint32_t sub, int half) const
-    {
-        const U4 b = keyed_block(seed, chain, step, tag, sub);
-        return half ? u52(b.z, b.w) : u52(b.x, b.y);
-    }
-    __device__ __forceinline__ void two(Chain&, uint64_t step, uint32_t tag, uint32_t sub, double& u0,
-                                        double& u1) const
-    {
-        const U4 b = keyed_block(seed, chain, step, tag, sub);
-        u0 = u52(b.x, b.y);
-        u1 = u52(b.z, b.w);
-    }
-};
-
-template <>
-struct Draw<TMH_RNG_INJECTED> {
-    const double* u;
-    uint64_t len;
-    __device__ __forceinline__ double one(Chain& ch, uint64_t, uint32_t, uint32_t, int) const
-    {
-        if (ch.pos >= len) {
-            if (!ch.status) ch.status = TMH_CHAIN_U_EXHAUSTED;
-            return 0.5;
-        }
-        return u[ch.pos++];
-    }
-    __device__ __forceinline__ void two(Chain& ch, uint64_t s, uint32_t t, uint32_t sub, double& u0,
-                                        double& u1) const
-    {
-        u0 = one(ch, s, t, sub, 0);
-        u1 = one(ch, s, t, sub, 1);
-    }
-};
-
-// ------------------------------------------------------------ model pieces
-__device__ __forceinline__ double interp(double b, double a, double f) { return f * a + (1.0 - f) * b; }
-
-__device__ __forceinline__ void push(Chain& ch, int k, double v)
-{
-    ch.sb[k] = ch.sa[k];
-    ch.sa[k] = v;
-}
-
-__device__ __forceinline__ double normal(double u, double loc, double scale) { return ndtri(u) * scale + loc; }
-
-__device__ __forceinline__ double scaled_noise(const KParams& kp, double u, double s0, double s1, double cc)
-{   // norm.rvs(loc=1., scale=np.sqrt(0.9) * (sigma0 + sigma1 * 8 * cc)), clearskyindexmodel.py:86-88
-    return normal(u, 1.0, kp.sqrt09 * (s0 + s1 * 8 * cc));
-}
-
-// hourly cloud cover: next(get_cloud_cover(distributions)); faithful = fresh generator (state 1.0)
-__device__ double draw_cc(const KParams& kp, Chain& ch, double u)
-{
-    const double state = kp.cc_mode == TMH_CC_MARKOV ? ch.mstate : 1.0;
-    int bin = 0;
-    while (bin < 5 && kp.edges[bin] < state) ++bin;   // np.searchsorted(bins, state)
-    double v = kp.is_t[bin] ? stdtrit(kp.shapes[bin][3], u) : al_ppf(u, kp.shapes[bin][2]);
-    v = v * kp.shapes[bin][1] + kp.shapes[bin][0];
-    double x = state + v;
-    x = x < 0.0 ? 0.0 : (x > 1.0 ? 1.0 : x);
-    if (kp.cc_mode == TMH_CC_MARKOV) ch.mstate = x;
-    return x;
-}
-
-__device__ __forceinline__ int32_t ceil_thr(double x)
-{   // sec < x  <=>  sec < ceil(x) for integer sec
-    if (!(x <= 2147483000.0)) return INT_MAX;
-    if (x < -2147483000.0) return INT_MIN + 1;
-    return (int32_t)ceil(x);
-}
-
-__device__ void reset_sigma(const StateView& st, uint32_t c, Chain& ch, double h)
-{   // cloud_cover_binary.py:76-78
-    int L = (int)(h * 12);
-    if (L > CAP) L = CAP;
-    const double f = 1.0 / h - 1.0;
-    double acc = 0.0;
-    for (int k = 0; k < L; ++k) {
-        acc += 300.0;
-        st.sc[(size_t)k * st.n + c] = acc;
-        st.sl[(size_t)k * st.n + c] = f * acc;
-    }
-    ch.L = L;
-}
-
-// cloud_cover_binary.py:80-107; returns 0 or a fault status
-template <int RNG>
-__device__ uint32_t next_cloud(const KParams& kp, const StateView& st, uint32_t c, Chain& ch,
-                               const Draw<RNG>& dr, double h, double ws, uint64_t step, uint32_t tag,
-                               uint32_t call)
-{
-    const double f = 1.0 / h - 1.0;
-    int tries = 0;
-    ch.ncalls++;
-    for (int rec = 0; rec < 2; ++rec) {
-        for (int i = 0; i < 20; ++i, ++tries) {
-            const double u = dr.one(ch, step, tag, (call << 8) | (uint32_t)(tries >> 1), tries & 1);
-            const double cl = pow(kp.alpha + kp.delta * u, kp.expo) / ws;
-            int last = -1;
-            double best = 0.0;
-            for (int k = 0; k < ch.L; ++k) {
-                const double nsc = cl + st.sc[(size_t)k * st.n + c];
-                const double nsl = f * nsc;
-                const double tot = nsc + nsl;
-                if (nsl - st.sl[(size_t)k * st.n + c] > 0.0 && tot < 5400.0) {
-                    const double d = fabs(tot - 3600.0);
-                    if (last < 0 || d < best) {
-                        best = d;
-                        last = k;
-                    }
-                }
-            }
-            if (last >= 0) {
-                if (last + 2 > CAP) return TMH_CHAIN_SIGMA_OVERFLOW;
-                const double clr = f * (cl + st.sc[(size_t)last * st.n + c]) - st.sl[(size_t)last * st.n + c];
-                for (int k = last; k >= 0; --k) {
-                    const double nsc = cl + st.sc[(size_t)k * st.n + c];
-                    st.sc[(size_t)(k + 1) * st.n + c] = nsc;
-                    st.sl[(size_t)(k + 1) * st.n + c] = f * nsc;
-                }
-                st.sc[c] = cl;
-                st.sl[c] = clr;
-                ch.L = last + 2;
-                ch.cl = cl;
-                ch.clr = clr;
-                ch.t1 = ceil_thr(cl);
-                ch.t2 = ceil_thr(cl + clr);
-                ch.sec = 0;
-                return 0;
-            }
-        }
-        if (rec == 0) reset_sigma(st, c, ch, h);
-    }
-    return TMH_CHAIN_ASSERT_BINARY;
-}
-
+// ------------------------------------------------------------ state I/O
 __device__ __forceinline__ void load_chain(const StateView& st, uint32_t c, Chain& ch)
 {
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-        ch.sb[k] = st.sb[k][c];
-        ch.sa[k] = st.sa[k][c];
+        ch.s.b[k] = st.sb[k][c];
+        ch.s.a[k] = st.sa[k][c];
     }
     ch.cl = st.cl[c];
     ch.clr = st.clr[c];
@@ -268,8 +90,8 @@ __device__ __forceinline__ void store_chain(const StateView& st, uint32_t c, con
 {
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-        st.sb[k][c] = ch.sb[k];
-        st.sa[k][c] = ch.sa[k];
+        st.sb[k][c] = ch.s.b[k];
+        st.sa[k][c] = ch.s.a[k];
     }
     st.cl[c] = ch.cl;
     st.clr[c] = ch.clr;
@@ -282,6 +104,7 @@ __device__ __forceinline__ void store_chain(const StateView& st, uint32_t c, con
 }
 
 // ------------------------------------------------------------ init kernel
+// ClearskyindexModel.__init__ (clearskyindexmodel.py:57-99)
 template <int RNG>
 __global__ __launch_bounds__(256) void init_kernel(KParams kp, StateView st, uint64_t chain0, uint32_t n,
                                                    double hf, InjView inj)
@@ -289,7 +112,7 @@ __global__ __launch_bounds__(256) void init_kernel(KParams kp, StateView st, uin
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n) return;
     Chain ch;
-    for (int k = 0; k < 6; ++k) ch.sb[k] = ch.sa[k] = NAN;
+    for (int k = 0; k < 6; ++k) ch.s.b[k] = ch.s.a[k] = NAN;
     ch.cl = ch.clr = NAN;
     ch.mstate = 1.0;
     ch.sec = 0;
@@ -308,157 +131,52 @@ __global__ __launch_bounds__(256) void init_kernel(KParams kp, StateView st, uin
     }
     double u[12];
     for (int d = 0; d < 12; ++d) u[d] = dr.one(ch, 0, TAG_INIT, (uint32_t)(d >> 1), d & 1);
-    // NB: injected mode consumes in exactly this order (clearskyindexmodel.py:61-97)
-    ch.sb[S_CC] = draw_cc(kp, ch, u[0]);
-    ch.sa[S_CC] = draw_cc(kp, ch, u[1]);
-    ch.sb[S_CLEAR_DAY] = normal(u[2], 0.99, 0.08);
-    ch.sa[S_CLEAR_DAY] = normal(u[3], 0.99, 0.08);
+    ch.s.b[S_CC] = draw_cc(kp, ch, u[0]);
+    ch.s.a[S_CC] = draw_cc(kp, ch, u[1]);
+    ch.s.b[S_CLEAR_DAY] = normal(u[2], 0.99, 0.08);
+    ch.s.a[S_CLEAR_DAY] = normal(u[3], 0.99, 0.08);
     bool name_error = false;
     for (int j = 0; j < 2; ++j) {   // :68-82
-        const double cc = interp(ch.sb[S_CC], ch.sa[S_CC], hf);
+        const double cc = interp(ch.s.b[S_CC], ch.s.a[S_CC], hf);
         double v;
         if (cc < 6.0 / 8) v = normal(u[4 + j], 0.6784, 0.2046);
         else if (cc < 7.0 / 8) {
-            name_error = true;
+            name_error = true;       // gamma.pdf(x, ...) with x undefined (:80)
             break;
         } else v = gammaincinv(3.5624, u[4 + j]) * 0.0867 + 0.0;
-        if (j == 0) ch.sb[S_CLOUDY_HOUR] = v;
-        else ch.sa[S_CLOUDY_HOUR] = v;
+        if (j == 0) ch.s.b[S_CLOUDY_HOUR] = v;
+        else ch.s.a[S_CLOUDY_HOUR] = v;
     }
     if (name_error) {
-        // the reference raises after consuming the 4 draws before the cloudy sampler
-        if constexpr (RNG == TMH_RNG_INJECTED) ch.pos = ch.pos < 4 ? ch.pos : 4;
+        if constexpr (RNG == TMH_RNG_INJECTED) ch.pos = ch.pos < 4 ? ch.pos : 4;   // raised after 4 draws
         ch.status = TMH_CHAIN_NAMEERROR_INIT;
         store_chain(st, c, ch);
         return;
     }
-    const double cch = interp(ch.sb[S_CC], ch.sa[S_CC], hf);
-    ch.sb[S_CLOUDY_NOISE] = scaled_noise(kp, u[6], 0.01, 0.003, cch);
-    ch.sa[S_CLOUDY_NOISE] = scaled_noise(kp, u[7], 0.01, 0.003, cch);
-    ch.sb[S_CLEAR_NOISE] = scaled_noise(kp, u[8], 0.001, 0.0015, cch);
-    ch.sa[S_CLEAR_NOISE] = scaled_noise(kp, u[9], 0.001, 0.0015, cch);
-    ch.sb[S_WS] = 2.14 * gammaincinv(2.69, u[10]);
-    ch.sa[S_WS] = 2.14 * gammaincinv(2.69, u[11]);
+    const double cch = interp(ch.s.b[S_CC], ch.s.a[S_CC], hf);
+    ch.s.b[S_CLOUDY_NOISE] = scaled_noise(kp, u[6], 0.01, 0.003, cch);
+    ch.s.a[S_CLOUDY_NOISE] = scaled_noise(kp, u[7], 0.01, 0.003, cch);
+    ch.s.b[S_CLEAR_NOISE] = scaled_noise(kp, u[8], 0.001, 0.0015, cch);
+    ch.s.a[S_CLEAR_NOISE] = scaled_noise(kp, u[9], 0.001, 0.0015, cch);
+    ch.s.b[S_WS] = 2.14 * gammaincinv(2.69, u[10]);
+    ch.s.a[S_WS] = 2.14 * gammaincinv(2.69, u[11]);
     // CloudCoverBinary(cc.interpolate(0), ws.interpolate(0)) (:98-99)
-    const double h0 = interp(ch.sb[S_CC], ch.sa[S_CC], 0.0);
+    const double h0 = interp(ch.s.b[S_CC], ch.s.a[S_CC], 0.0);
     const double h = 0.95 < h0 ? 0.95 : h0;
-    const double ws = interp(ch.sb[S_WS], ch.sa[S_WS], 0.0);
-    reset_sigma(st, c, ch, h);
-    uint32_t f = next_cloud<RNG>(kp, st, c, ch, dr, h, ws, 0, TAG_INIT_CLOUD, 0);
+    const double ws = interp(ch.s.b[S_WS], ch.s.a[S_WS], 0.0);
+    double* sc = sig_c(st, c);
+    double* sl = sig_l(st, c);
+    reset_sigma(sc, sl, ch, h);
+    const uint32_t f = next_cloud<RNG>(kp, sc, sl, ch, dr, h, ws, 0, TAG_INIT_CLOUD, 0);
     if (!f) {
         const double us = dr.one(ch, 0, TAG_INIT_SEC, 0, 0);
-        ch.sec = (int32_t)((ch.cl + ch.clr) * us);
+        ch.sec = (int32_t)((ch.cl + ch.clr) * us);   // cloud_cover_binary.py:68
     }
     if (f && !ch.status) ch.status = f;
     store_chain(st, c, ch);
 }
 
-// ------------------------------------------------------------ clock + geometry
-__device__ __forceinline__ double rad(double d) { return d * (3.14159265358979323846 / 180.0); }
-__device__ __forceinline__ double deg(double r) { return r * (180.0 / 3.14159265358979323846); }
-__device__ __forceinline__ double cosd(double d) { return cos(rad(d)); }
-__device__ __forceinline__ double sind(double d) { return sin(rad(d)); }
-
-__device__ __forceinline__ int64_t local_at(const tmh_clock& ck, int64_t s)
-{
-    int64_t l = ck.local0 + s;
-    for (int i = 0; i < ck.n_shifts && i < 8; ++i)
-        if (s >= ck.shift_step[i]) l += ck.shift_delta[i];
-    return l;
-}
-
-__device__ __forceinline__ int64_t floordiv(int64_t a, int64_t b)
-{
-    int64_t q = a / b;
-    if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
-    return q;
-}
-
-// days since 1970-01-01 -> (year, day of year 1..366, leap)
-__device__ void civil_doy(int64_t z, int& doy, int& leap)
-{
-    z += 719468;
-    const int64_t era = floordiv(z, 146097);
-    const int64_t doe = z - era * 146097;
-    const int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
-    int64_t y = yoe + era * 400;
-    const int64_t doyy = doe - (365 * yoe + yoe / 4 - yoe / 100);   // from March 1
-    const int64_t mp = (5 * doyy + 2) / 153;
-    const int64_t d = doyy - (153 * mp + 2) / 5 + 1;
-    const int64_t m = mp < 10 ? mp + 3 : mp - 9;
-    if (m <= 2) ++y;
-    leap = ((y % 4 == 0) && (y % 100 != 0)) || (y % 400 == 0);
-    static const int cum[12] = {0, 31, 59, 90, 120, 151, 181, 212, 243, 273, 304, 334};
-    doy = cum[m - 1] + (int)d + ((leap && m > 2) ? 1 : 0);
-}
-
-__device__ void solpos(int64_t utc, double lat, double lon, double pressure_pa, double temp_c, double& zen,
-                       double& azen, double& az)
-{   // NOAA / Meeus low-precision sun + SPA refraction (same restatement as the oracle)
-    const double jd = (double)utc / 86400.0 + 2440587.5;
-    const double T = (jd - 2451545.0) / 36525.0;
-    const double L0 = fmod(280.46646 + T * (36000.76983 + T * 0.0003032), 360.0);
-    const double M = 357.52911 + T * (35999.05029 - 0.0001537 * T);
-    const double e = 0.016708634 - T * (0.000042037 + 0.0000001267 * T);
-    const double Mr = rad(M);
-    const double C = sin(Mr) * (1.914602 - T * (0.004817 + 0.000014 * T)) +
-                     sin(2.0 * Mr) * (0.019993 - 0.000101 * T) + sin(3.0 * Mr) * 0.000289;
-    const double omega = 125.04 - 1934.136 * T;
-    const double lam = L0 + C - 0.00569 - 0.00478 * sin(rad(omega));
-    const double eps0 = 23.0 + (26.0 + (21.448 - T * (46.815 + T * (0.00059 - T * 0.001813))) / 60.0) / 60.0;
-    const double eps = eps0 + 0.00256 * cos(rad(omega));
-    const double decl = asin(sin(rad(eps)) * sin(rad(lam)));
-    double y = tan(rad(eps) / 2.0);
-    y *= y;
-    const double L0r = rad(L0);
-    const double eot = 4.0 * deg(y * sin(2.0 * L0r) - 2.0 * e * sin(Mr) + 4.0 * e * y * sin(Mr) * cos(2.0 * L0r) -
-                                 0.5 * y * y * sin(4.0 * L0r) - 1.25 * e * e * sin(2.0 * Mr));
-    int64_t sod = utc % 86400;
-    if (sod < 0) sod += 86400;
-    double tst = fmod((double)sod / 60.0 + eot + 4.0 * lon, 1440.0);
-    if (tst < 0) tst += 1440.0;
-    const double ha = rad(tst / 4.0 - 180.0);
-    const double latr = rad(lat);
-    double cz = sin(latr) * sin(decl) + cos(latr) * cos(decl) * cos(ha);
-    cz = cz > 1.0 ? 1.0 : (cz < -1.0 ? -1.0 : cz);
-    zen = deg(acos(cz));
-    az = deg(atan2(sin(ha), cos(ha) * sin(latr) - tan(decl) * cos(latr))) + 180.0;
-    const double e0 = 90.0 - zen;
-    double de = 0.0;
-    if (e0 >= -1.0 * (0.26667 + 0.5667))
-        de = (pressure_pa / 100.0 / 1010.0) * (283.0 / (273.0 + temp_c)) * 1.02 /
-             (60.0 * tan(rad(e0 + 10.3 / (e0 + 5.11))));
-    azen = 90.0 - (e0 + de);
-}
-
-__device__ __forceinline__ double extra_rad(int doy, double s0)
-{
-    const double B = (2.0 * 3.14159265358979323846 / 365.0) * (doy - 1);
-    return s0 * (1.00011 + 0.034221 * cos(B) + 0.00128 * sin(B) + 0.000719 * cos(2.0 * B) + 7.7e-05 * sin(2.0 * B));
-}
-
-__device__ double linke_at(const double* lts, int doy, int leap)
-{
-    const int md[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
-    double x0 = -31.0 / 2.0, y0 = lts[11], cum = 0.0;
-    for (int m = 0; m < 13; ++m) {
-        double x1, y1;
-        if (m < 12) {
-            const double d = md[m] + (leap && m == 1 ? 1 : 0);
-            cum += d;
-            x1 = cum - d / 2.0;
-            y1 = lts[m];
-        } else {
-            x1 = (leap ? 366 : 365) + 28 / 2.0;
-            y1 = lts[0];
-        }
-        if ((double)doy <= x1) return y0 + ((double)doy - x0) * (y1 - y0) / (x1 - x0);
-        x0 = x1;
-        y0 = y1;
-    }
-    return lts[0];
-}
-
+// ------------------------------------------------------------ plan kernels
 __global__ __launch_bounds__(256) void geom_kernel(GParams gp, int64_t step0, uint32_t n, double* tab64,
                                                    float* tab32)
 {
@@ -473,13 +191,13 @@ __global__ __launch_bounds__(256) void geom_kernel(GParams gp, int64_t step0, ui
     const int hourp = (int)(sodp / 3600), minutep = (int)((sodp / 60) % 60);
     double g[ROW];
     for (int i = 0; i < ROW; ++i) g[i] = 0.0;
-    g[G_MINF] = second / 60.0;                       // clearskyindexmodel.py:114-116
+    g[G_MINF] = second / 60.0;   // clearskyindexmodel.py:114-116
     g[G_HOURF] = (minute + g[G_MINF]) / 60.0;
     g[G_DAYF] = (hour + g[G_HOURF]) / 24.0;
     uint32_t fl = 0;
-    if (dn != dp) fl |= FL_DAY;                      // :121 prev.day != day
-    if (hour != hourp) fl |= FL_HOUR;                // :123
-    if (minute != minutep) fl |= FL_MIN;             // :125
+    if (dn != dp) fl |= FL_DAY;           // :121 prev.day != day
+    if (hour != hourp) fl |= FL_HOUR;     // :123
+    if (minute != minutep) fl |= FL_MIN;  // :125
     // ---- PV geometry (pvmodel.py:50-76; pvlib 0.6.3 model choices) ----
     const double lat = gp.site[0], lon = gp.site[1], alt = gp.site[2], tilt = gp.site[3], saz = gp.site[4],
                  albedo = gp.site[5];
@@ -492,8 +210,8 @@ __global__ __launch_bounds__(256) void geom_kernel(GParams gp, int64_t step0, ui
     g[G_COSZ] = ct;
     g[G_CSIMAX] = 27.21 * exp(-114 * ct) + 1.665 * exp(-4.494 * ct) + 1.08;
     const double dni_extra = extra_rad(doy, 1366.1);
-    const double am_rel = azen <= 90.0 ? 1.0 / (cos(rad(azen)) + 0.50572 * pow(6.07995 + (90.0 - azen), -1.6364))
-                                       : NAN;
+    const double am_rel =
+        azen <= 90.0 ? 1.0 / (cos(rad(azen)) + 0.50572 * pow(6.07995 + (90.0 - azen), -1.6364)) : NAN;
     const double am_abs = am_rel * pres / 101325.0;
     const double tl = linke_at(gp.linke, doy, leap);
     const double fh1 = exp(-alt / 8000.0), fh2 = exp(-alt / 1250.0);
@@ -531,7 +249,7 @@ __global__ __launch_bounds__(256) void geom_kernel(GParams gp, int64_t step0, ui
     f2 = f2 > 0.0 ? f2 : 0.0;
     if (aoi < 0.0) f2 = 0.0;
     g[G_F2] = f2;
-    if (g[G_GHICS] == 0.0) fl |= FL_NIGHT;           // ghi_cs = 0 -> pv = 0 whatever the csi
+    if (g[G_GHICS] == 0.0) fl |= FL_NIGHT;   // ghi_cs = 0 -> pv = 0 whatever the csi
     g[G_FLAGS] = (double)fl;
     double* o64 = tab64 + (size_t)j * ROW;
     float* o32 = tab32 + (size_t)j * ROW;
@@ -540,94 +258,203 @@ __global__ __launch_bounds__(256) void geom_kernel(GParams gp, int64_t step0, ui
         o32[i] = (float)g[i];
     }
     o32[G_FLAGS] = __uint_as_float(fl);
-    o32[G_I0H] = (float)(1.0 / g[G_I0H]);              // fp32 path multiplies by reciprocals
+    o32[G_I0H] = (float)(1.0 / g[G_I0H]);   // fp32 path multiplies by reciprocals
     o32[G_DNIEXTRA] = (float)(1.0 / g[G_DNIEXTRA]);
 }
 
-// ------------------------------------------------------------ PV (per chain-second)
-// pvmodel.py:53-80 on the precomputed geometry row; R = float | double.
-template <typename R>
-__device__ __forceinline__ R pv_power(const KParams& kp, const R* g, R csi)
+// Compact the window's day/hour boundary steps, in order (one workgroup).
+// Every such boundary is also a minute boundary (local second 0 = UTC second 0
+// for whole-minute offsets), so only one row per minute is inspected.
+__global__ __launch_bounds__(1024) void events_kernel(const float* __restrict__ tab32, int64_t step0, uint32_t n,
+                                                      int64_t utc0, int2* events, uint32_t cap, uint32_t* n_events)
 {
-    const double* m = kp.module;
-    const double* iv = kp.inverter;
-    R c = csi > g[G_CSIMAX] ? g[G_CSIMAX] : csi;
-    const R ghi = c * g[G_GHICS];
-    R kt;
-    if constexpr (sizeof(R) == 8) kt = ghi / g[G_I0H];
-    else kt = ghi * g[G_I0H];
-    kt = kt > R(0) ? kt : R(0);
-    kt = kt < R(1) ? kt : R(1);
-    const R am = g[G_AM], kt2 = kt * kt, kt3 = kt2 * kt;
-    R a, b, cc;
-    if (kt <= R(0.6)) {
-        a = R(0.512) - R(1.56) * kt + R(2.286) * kt2 - R(2.222) * kt3;
-        b = R(0.37) + R(0.962) * kt;
-        cc = R(-0.28) + R(0.932) * kt - R(2.048) * kt2;
-    } else {
-        a = R(-5.743) + R(21.77) * kt - R(27.49) * kt2 + R(11.56) * kt3;
-        b = R(41.4) - R(118.5) * kt + R(66.05) * kt2 + R(31.9) * kt3;
-        cc = R(-47.01) + R(184.2) * kt - R(222.0) * kt2 + R(73.81) * kt3;
+    __shared__ uint32_t cnt[1024];
+    const uint32_t t = threadIdx.x;
+    const int64_t first = (60 - (((utc0 + step0) % 60) + 60) % 60) % 60;   // first candidate (window-relative)
+    const uint32_t ncand = first < (int64_t)n ? (uint32_t)((n - 1 - first) / 60 + 1) : 0;
+    const uint32_t chunk = (ncand + 1023) / 1024;
+    const uint32_t lo = t * chunk, hi = min(lo + chunk, ncand);
+    uint32_t c = 0;
+    for (uint32_t q = lo; q < hi; ++q) {
+        const uint64_t j = (uint64_t)(first + 60 * (int64_t)q);
+        if (__float_as_uint(tab32[j * ROW + G_FLAGS]) & (FL_DAY | FL_HOUR)) ++c;
     }
-    const R dkn = a + b * exp(cc * am);
-    R dni = (g[G_KNC] - dkn) * g[G_I0];
-    if (g[G_DISCOK] == R(0) || ghi < R(0) || dni < R(0)) dni = R(0);
-    const R dhi = ghi - dni * g[G_COSZ];
-    R AI;
-    if constexpr (sizeof(R) == 8) AI = dni / g[G_DNIEXTRA];
-    else AI = dni * g[G_DNIEXTRA];
-    R sky = dhi * (AI * g[G_RB] + (R(1) - AI) * g[G_TERM2]);
-    sky = sky > R(0) ? sky : R(0);
-    const R ground = ghi * g[G_GFAC];
-    R poa_direct = dni * g[G_COSAOI];
-    poa_direct = poa_direct > R(0) ? poa_direct : R(0);
-    const R poa_diffuse = sky + ground;
-    const R poa_global = poa_direct + poa_diffuse;
-    // sapm_celltemp (pvmodel.py:69-70), open_rack_cell_glassback
-    const R tmod = poa_global * exp(R(m[TMH_MOD_TEMP_A]) + R(m[TMH_MOD_TEMP_B]) * R(kp.wind)) + R(kp.temp_air);
-    const R tcell = tmod + (poa_global / R(1000)) * R(m[TMH_MOD_TEMP_DT]);
-    // sapm_effective_irradiance, suns (pvmodel.py:74-76)
-    const R Ee = g[G_F1] * (poa_direct * g[G_F2] + R(m[TMH_MOD_FD]) * poa_diffuse) / R(1000);
-    // sapm (pvmodel.py:77)
-    const R q = R(1.60218e-19), kb = R(1.38066e-23);
-    const R Bvmpo = R(m[TMH_MOD_BVMPO]) + R(m[TMH_MOD_MBVMP]) * (R(1) - Ee);
-    R delta;
-    if constexpr (sizeof(R) == 8) delta = R(m[TMH_MOD_N]) * kb * (tcell + R(273.15)) / q;
-    else delta = R(m[TMH_MOD_N] * (1.38066e-23 / 1.60218e-19)) * (tcell + R(273.15));   // fp32: no 1e-23 subnormals
-    const R logEe = Ee > R(0) ? log(Ee) : (Ee == R(0) ? -R(INFINITY) : R(NAN));
-    const R imp = R(m[TMH_MOD_IMPO]) * (R(m[TMH_MOD_C0]) * Ee + R(m[TMH_MOD_C1]) * (Ee * Ee)) *
-                  (R(1) + R(m[TMH_MOD_AIMP]) * (tcell - R(25)));
-    const R dl = delta * logEe;
-    R vmp = R(m[TMH_MOD_VMPO]) + R(m[TMH_MOD_C2]) * R(m[TMH_MOD_NS]) * delta * logEe +
-            R(m[TMH_MOD_C3]) * R(m[TMH_MOD_NS]) * (dl * dl) + Bvmpo * (tcell - R(25));
-    if (!isnan(vmp)) vmp = vmp > R(0) ? vmp : R(0);
-    const R pdc = imp * vmp;
-    // snlinverter (pvmodel.py:78)
-    const R dv = vmp - R(iv[2]);
-    const R A = R(iv[1]) * (R(1) + R(iv[5]) * dv);
-    const R B = R(iv[3]) * (R(1) + R(iv[6]) * dv);
-    const R C = R(iv[4]) * (R(1) + R(iv[7]) * dv);
-    R ac = (R(iv[0]) / (A - B) - C * (A - B)) * (pdc - B) + C * ((pdc - B) * (pdc - B));
-    if (!isnan(ac)) ac = R(iv[0]) < ac ? R(iv[0]) : ac;
-    if (pdc < R(iv[3])) ac = R(-1) * fabs(R(iv[8]));
-    if (isnan(ac)) return R(0);                       // .fillna(0.)
-    return ac > R(0) ? ac : R(0);                      // .clip(lower=0.)
+    cnt[t] = c;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {   // inclusive scan
+        const uint32_t v = t >= off ? cnt[t - off] : 0;
+        __syncthreads();
+        cnt[t] += v;
+        __syncthreads();
+    }
+    uint32_t o = cnt[t] - c;
+    for (uint32_t q = lo; q < hi; ++q) {
+        const uint64_t j = (uint64_t)(first + 60 * (int64_t)q);
+        const uint32_t fl = __float_as_uint(tab32[j * ROW + G_FLAGS]) & (FL_DAY | FL_HOUR);
+        if (fl) {
+            if (o < cap) events[o] = make_int2((int)(step0 + (int64_t)j), (int)fl);
+            ++o;
+        }
+    }
+    if (t == 1023) *n_events = cnt[1023];
 }
 
-// ------------------------------------------------------------ chain kernel
-template <typename R>
-__device__ __forceinline__ void trace_store(void* p, uint64_t i, R v)
+__device__ __forceinline__ uint32_t ev_cap_dev(uint32_t n_steps) { return n_steps / 1800 + 64; }
+
+__device__ __forceinline__ int64_t first_minute(int64_t utc0, int64_t W0)
+{   // window-relative step of the first candidate minute boundary (UTC second 0)
+    return (60 - (((utc0 + W0) % 60) + 60) % 60) % 60;
+}
+
+// Descriptor of the sampler state after step W0 + min(b * BLOCK_STEPS, n) - 1,
+// for b = 0 .. nblk (the last one describes the window end).
+__global__ __launch_bounds__(256) void desc_kernel(int64_t step0, uint32_t n, int64_t utc0,
+                                                   const int2* __restrict__ events,
+                                                   const uint32_t* __restrict__ n_events, BlockDesc* desc,
+                                                   uint32_t nblk)
 {
-    if (p) reinterpret_cast<R*>(p)[i] = v;
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > nblk) return;
+    BlockDesc d{-1, -1, -1, -1, -1, -1, 0, 0};
+    const int64_t jb = min((int64_t)b * BLOCK_STEPS, (int64_t)n);
+    if (jb > 0) {
+        const int64_t p = step0 + jb - 1;                  // last step before the block
+        const int64_t lo = step0 > 1 ? step0 : 1;          // step 0 is the constructor time
+        const int64_t fm = first_minute(utc0, step0);
+        const int64_t m0 = p - (((utc0 + p) % 60) + 60) % 60;
+        if (m0 >= lo) d.q0 = (int32_t)((m0 - step0 - fm) / 60);
+        if (m0 - 60 >= lo) d.q1 = (int32_t)((m0 - 60 - step0 - fm) / 60);
+        const int ne = (int)min(*n_events, ev_cap_dev(n));
+        int a = 0, z = ne;                                  // last event <= p
+        while (a < z) {
+            const int mid = (a + z) / 2;
+            if (events[mid].x <= p) a = mid + 1;
+            else z = mid;
+        }
+        d.evi = a;
+        int nh = 0, ncd = 0;
+        for (int i = a - 1; i >= 0 && (nh < 2 || ncd < 2); --i) {
+            const int fl = events[i].y;
+            if (fl & FL_HOUR) {
+                if (nh == 0) d.h0 = i;
+                else if (nh == 1) d.h1 = i;
+                ++nh;
+                if (ncd < 2) {            // the hour push of clear_day follows its day push
+                    if (ncd == 0) d.cd0 = 2 * i + 1;
+                    else d.cd1 = 2 * i + 1;
+                    ++ncd;
+                }
+            }
+            if ((fl & FL_DAY) && ncd < 2) {
+                if (ncd == 0) d.cd0 = 2 * i;
+                else d.cd1 = 2 * i;
+                ++ncd;
+            }
+        }
+    }
+    desc[b] = d;
 }
 
-// Advance chains [0, n) of this call over steps [step0, step0 + nsteps).
+// ------------------------------------------------------------ boundary draws
+// _next_day / _next_hour draws of every (event, chain): clearskyindexmodel.py:101-107
+__global__ __launch_bounds__(256) void event_draws_kernel(DrawParams dp, uint64_t chain0, uint32_t n, uint32_t nsteps,
+                                                          const int2* __restrict__ events,
+                                                          const uint32_t* __restrict__ n_events, double* evd)
+{
+    const uint32_t c = blockIdx.y * blockDim.x + threadIdx.x;
+    const uint32_t e = blockIdx.x;
+    if (c >= n || e >= min(*n_events, ev_cap_dev(nsteps))) return;
+    const uint64_t chain = chain0 + c, step = (uint64_t)events[e].x;
+    const int fl = events[e].y;
+    double* o = evd + (size_t)e * 4 * n + c;
+    if (fl & FL_DAY) {
+        const U4 u = keyed_block(dp.seed, chain, step, TAG_BOUNDARY, 0);
+        o[2 * (size_t)n] = normal(u52(u.x, u.y), 0.99, 0.08);
+        o[(size_t)n] = 2.14 * gammaincinv(2.69, u52(u.z, u.w));
+    }
+    if (fl & FL_HOUR) {
+        const U4 u = keyed_block(dp.seed, chain, step, TAG_BOUNDARY, 1);
+        o[0] = cc_faithful(dp, u52(u.x, u.y));
+        o[3 * (size_t)n] = normal(u52(u.z, u.w), 0.99, 0.08);
+    }
+}
+
+// _next_min draws of every (minute boundary, chain): clearskyindexmodel.py:86-95,109-111
+__global__ __launch_bounds__(256) void minute_draws_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
+                                                           int64_t W0, uint32_t nsteps, int64_t utc0,
+                                                           const double* __restrict__ tab64,
+                                                           const int2* __restrict__ events,
+                                                           const uint32_t* __restrict__ n_events,
+                                                           const double* __restrict__ evd, double* mind)
+{
+    const uint32_t c = blockIdx.y * blockDim.x + threadIdx.x;
+    const uint32_t q = blockIdx.x;
+    const int64_t j = first_minute(utc0, W0) + 60 * (int64_t)q;
+    if (c >= n || j >= (int64_t)nsteps) return;
+    const int64_t step = W0 + j;
+    const int ne = (int)min(*n_events, ev_cap_dev(nsteps));
+    int a = 0, z = ne;   // last event <= step
+    while (a < z) {
+        const int mid = (a + z) / 2;
+        if (events[mid].x <= step) a = mid + 1;
+        else z = mid;
+    }
+    int h0 = -1, h1 = -1;
+    for (int i = a - 1; i >= 0 && h1 < 0; --i)
+        if (events[i].y & FL_HOUR) {
+            if (h0 < 0) h0 = i;
+            else h1 = i;
+        }
+    double pb, pa;   // cloud cover pair after the hour push of this second
+    if (h0 < 0) {
+        pb = st.sb[S_CC][c];
+        pa = st.sa[S_CC][c];
+    } else if (h1 < 0) {
+        pb = st.sa[S_CC][c];
+        pa = evd[(size_t)h0 * 4 * n + c];
+    } else {
+        pb = evd[(size_t)h1 * 4 * n + c];
+        pa = evd[(size_t)h0 * 4 * n + c];
+    }
+    const double cc = interp(pb, pa, tab64[(size_t)j * ROW + G_HOURF]);
+    const U4 u = keyed_block(dp.seed, chain0 + c, (uint64_t)step, TAG_BOUNDARY, 2);
+    mind[(size_t)q * 2 * n + c] = normal(u52(u.x, u.y), 1.0, dp.sqrt09 * (0.01 + 0.003 * 8 * cc));
+    mind[((size_t)q * 2 + 1) * n + c] = normal(u52(u.z, u.w), 1.0, dp.sqrt09 * (0.001 + 0.0015 * 8 * cc));
+}
+
+// cc / clear_day / noise pairs described by `d`, from the draw tables (start = window start)
+__device__ __forceinline__ void samplers_at(const BlockDesc& d, const SegView& sg, uint32_t n, uint32_t c, Samp& s)
+{
+    const double* evd = sg.evd;
+    if (d.h0 >= 0) {
+        const double na = evd[(size_t)d.h0 * 4 * n + c];
+        s.b[S_CC] = d.h1 >= 0 ? evd[(size_t)d.h1 * 4 * n + c] : s.a[S_CC];
+        s.a[S_CC] = na;
+    }
+    if (d.cd0 >= 0) {
+        auto cdv = [&](int32_t key) { return evd[((size_t)(key >> 1) * 4 + ((key & 1) ? 3 : 2)) * n + c]; };
+        const double na = cdv(d.cd0);
+        s.b[S_CLEAR_DAY] = d.cd1 >= 0 ? cdv(d.cd1) : s.a[S_CLEAR_DAY];
+        s.a[S_CLEAR_DAY] = na;
+    }
+    if (d.q0 >= 0) {
+        for (int k = 0; k < 2; ++k) {
+            const int si = k == 0 ? S_CLOUDY_NOISE : S_CLEAR_NOISE;
+            const double na = sg.mind[((size_t)d.q0 * 2 + k) * n + c];
+            s.b[si] = d.q1 >= 0 ? sg.mind[((size_t)d.q1 * 2 + k) * n + c] : s.a[si];
+            s.a[si] = na;
+        }
+    }
+}
+
+// ------------------------------------------------------------ sequential kernel
+// Advance chains [0, n) over steps [step0, step0 + nsteps), one lane per chain.
 template <typename R, int RNG>
 __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, uint64_t chain0, uint32_t n,
                                                     int64_t step0, uint32_t nsteps,
                                                     const double* __restrict__ tab64,
-                                                    const float* __restrict__ tab32, InjView inj,
-                                                    TraceView tr, StatsView sv)
+                                                    const float* __restrict__ tab32, InjView inj, TraceView tr,
+                                                    StatsView sv)
 {
     extern __shared__ uint32_t lds_hist[];
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -648,127 +475,79 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
         dr.len = inj.len;
     }
     const uint64_t chain = chain0 + c;
-    // fp32 copies of the sampler pairs (refreshed at boundaries)
-    R fb[6], fa[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        fb[k] = (R)ch.sb[k];
-        fa[k] = (R)ch.sa[k];
-    }
-    double acc_pv = 0.0, acc_m = 0.0, acc_r = 0.0, mx = -INFINITY;
-    const R sqrt6 = (R)kp.sqrt6, k15 = (R)(0.0015 * 8);
+    double* sc = live ? sig_c(st, c) : nullptr;
+    double* sl = live ? sig_l(st, c) : nullptr;
+    FSamp<R> fs;
+    to_real(fs, ch.s);
+    Acc acc{0.0, 0.0, 0.0, -INFINITY};
     for (uint32_t j = 0; j < nsteps; ++j) {
         const uint64_t step = (uint64_t)(step0 + j);
         const float* r32 = tab32 + (size_t)j * ROW;
+        const double* r64 = tab64 + (size_t)j * ROW;
         const uint32_t fl = __float_as_uint(r32[G_FLAGS]);
         R row[ROW];
-        if constexpr (sizeof(R) == 8) {
 #pragma unroll
-            for (int i = 0; i < ROW; ++i) row[i] = tab64[(size_t)j * ROW + i];
-        } else {
-#pragma unroll
-            for (int i = 0; i < ROW; ++i) row[i] = r32[i];
-        }
+        for (int i = 0; i < ROW; ++i) row[i] = sizeof(R) == 8 ? (R)r64[i] : (R)r32[i];
         R csi = R(NAN), pv = R(NAN), meter = R(NAN), res = R(NAN);
         uint8_t cov = 255;
+        bool ok = false;
         if (ch.status == 0) {
-            const double* r64 = tab64 + (size_t)j * ROW;
-            if (fl & (FL_DAY | FL_HOUR | FL_MIN)) {           // _set_time boundaries (:120-126)
+            if (fl & (FL_DAY | FL_HOUR | FL_MIN)) {   // _set_time boundaries (:120-126)
                 const double hf = r64[G_HOURF];
                 double u0, u1;
-                if (fl & FL_DAY) {                              // _next_day
+                if (fl & FL_DAY) {                     // _next_day
                     dr.two(ch, step, TAG_BOUNDARY, 0, u0, u1);
-                    push(ch, S_CLEAR_DAY, normal(u0, 0.99, 0.08));
-                    push(ch, S_WS, 2.14 * gammaincinv(2.69, u1));
+                    push(ch.s, S_CLEAR_DAY, normal(u0, 0.99, 0.08));
+                    push(ch.s, S_WS, 2.14 * gammaincinv(2.69, u1));
                 }
-                if (fl & FL_HOUR) {                             // _next_hour (advances clear_day)
+                if (fl & FL_HOUR) {                    // _next_hour (advances clear_day)
                     dr.two(ch, step, TAG_BOUNDARY, 1, u0, u1);
-                    push(ch, S_CC, draw_cc(kp, ch, u0));
-                    push(ch, S_CLEAR_DAY, normal(u1, 0.99, 0.08));
+                    push(ch.s, S_CC, draw_cc(kp, ch, u0));
+                    push(ch.s, S_CLEAR_DAY, normal(u1, 0.99, 0.08));
                 }
-                if (fl & FL_MIN) {                              // _next_min
+                if (fl & FL_MIN) {                     // _next_min
                     dr.two(ch, step, TAG_BOUNDARY, 2, u0, u1);
-                    const double cc = interp(ch.sb[S_CC], ch.sa[S_CC], hf);
-                    push(ch, S_CLOUDY_NOISE, scaled_noise(kp, u0, 0.01, 0.003, cc));
-                    push(ch, S_CLEAR_NOISE, scaled_noise(kp, u1, 0.001, 0.0015, cc));
+                    const double cc = interp(ch.s.b[S_CC], ch.s.a[S_CC], hf);
+                    push(ch.s, S_CLOUDY_NOISE, scaled_noise(kp, u0, 0.01, 0.003, cc));
+                    push(ch.s, S_CLEAR_NOISE, scaled_noise(kp, u1, 0.001, 0.0015, cc));
                 }
-#pragma unroll
-                for (int k = 0; k < 6; ++k) {
-                    fb[k] = (R)ch.sb[k];
-                    fa[k] = (R)ch.sa[k];
-                }
+                to_real(fs, ch.s);
             }
-            ch.sec += 1;                                          // CloudCoverBinary.__next__
+            ch.sec += 1;                                 // CloudCoverBinary.__next__
             uint32_t call = 0;
-            while (ch.sec >= ch.t2 && ch.status == 0) {           // segment over: next_cloud(); next(self)
-                const double hh = interp(ch.sb[S_CC], ch.sa[S_CC], r64[G_HOURF]);
-                const double h = 0.95 < hh ? 0.95 : hh;           // update_parameters
-                const double ws = interp(ch.sb[S_WS], ch.sa[S_WS], r64[G_DAYF]);
-                const uint32_t f = next_cloud<RNG>(kp, st, c, ch, dr, h, ws, step, TAG_CLOUD, call++);
+            while (ch.sec >= ch.t2 && ch.status == 0) {  // segment over: next_cloud(); next(self)
+                const double hh = interp(ch.s.b[S_CC], ch.s.a[S_CC], r64[G_HOURF]);
+                const double h = 0.95 < hh ? 0.95 : hh;  // update_parameters
+                const double ws = interp(ch.s.b[S_WS], ch.s.a[S_WS], r64[G_DAYF]);
+                const uint32_t f = next_cloud<RNG>(kp, sc, sl, ch, dr, h, ws, step, TAG_CLOUD, call++);
                 if (f) ch.status = f;
                 else ch.sec += 1;
             }
-            double ue = 0.5, um = 0.5;
             if (ch.status == 0) {
+                double ue, um;
                 if constexpr (RNG == TMH_RNG_KEYED) {
                     dr.two(ch, step, TAG_STEP, 0, ue, um);
                 } else {   // the meter is its own process in the reference: always keyed
                     ue = dr.one(ch, step, TAG_STEP, 0, 0);
-                    const U4 b = keyed_block(kp.seed, chain, step, TAG_STEP, 0);
-                    um = u52(b.z, b.w);
+                    um = keyed_u(kp.seed, chain, step, TAG_STEP, 0, 1);
                 }
-            }
-            if (ch.status == 0) {
-                const bool covered = ch.sec < ch.t1;
-                cov = covered ? 1 : 0;
-                R cloudcover, z;
-                if constexpr (sizeof(R) == 8) {
-                    cloudcover = interp(ch.sb[S_CC], ch.sa[S_CC], row[G_HOURF]);
-                    z = ndtri(ue);
-                } else {
-                    cloudcover = row[G_HOURF] * fa[S_CC] + (R(1) - row[G_HOURF]) * fb[S_CC];
-                    z = ndtri_f(ue);
-                }
-                const R eps = z * (sqrt6 * (R(0.001) + k15 * cloudcover)) + R(0);
-                if (covered)
-                    csi = (row[G_DAYF] * fa[S_CLEAR_DAY] + (R(1) - row[G_DAYF]) * fb[S_CLEAR_DAY]) *
-                          ((row[G_MINF] * fa[S_CLEAR_NOISE] + (R(1) - row[G_MINF]) * fb[S_CLEAR_NOISE]) + eps);
-                else
-                    csi = (row[G_HOURF] * fa[S_CLOUDY_HOUR] + (R(1) - row[G_HOURF]) * fb[S_CLOUDY_HOUR]) *
-                          ((row[G_MINF] * fa[S_CLOUDY_NOISE] + (R(1) - row[G_MINF]) * fb[S_CLOUDY_NOISE]) + eps);
-                pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power<R>(kp, row, csi) : R(0);
-                if constexpr (sizeof(R) == 8) meter = 9000 * um;
-                else meter = (R)(9000 * um);
-                res = meter - pv;
-                if (sv.acc) {
-                    acc_pv += (double)pv;
-                    acc_m += (double)meter;
-                    acc_r += (double)res;
-                    mx = fmax(mx, (double)res);
-                }
-                if (sv.hist) {
-                    double x = ((double)res - sv.lo) * sv.scale;
-                    int bin = x < 0.0 ? 0 : (x >= (double)(sv.n_bins - 1) ? (int)sv.n_bins - 1 : (int)x);
-                    atomicAdd(&lds_hist[bin], 1u);
+                if (ch.status == 0) {
+                    const bool covered = ch.sec < ch.t1;
+                    cov = covered ? 1 : 0;
+                    second_body<R>(kp, row, fl, fs, covered, ue, um, csi, pv, meter, res);
+                    ok = true;
                 }
             }
         }
-        if (live) {
-            const uint64_t o = (uint64_t)j * tr.ld + c;
-            trace_store<R>(tr.csi, o, csi);
-            trace_store<R>(tr.pv, o, pv);
-            trace_store<R>(tr.meter, o, meter);
-            trace_store<R>(tr.residual, o, res);
-            if (tr.covered) tr.covered[o] = cov;
-        }
+        if (live) emit<R>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok);
     }
     if (live) {
         store_chain(st, c, ch);
         if (sv.acc) {
-            sv.acc[c] += acc_pv;
-            sv.acc[(size_t)n + c] += acc_m;
-            sv.acc[2 * (size_t)n + c] += acc_r;
-            sv.acc[3 * (size_t)n + c] = fmax(sv.acc[3 * (size_t)n + c], mx);
+            sv.acc[c] += acc.pv;
+            sv.acc[(size_t)n + c] += acc.m;
+            sv.acc[2 * (size_t)n + c] += acc.r;
+            sv.acc[3 * (size_t)n + c] = fmax(sv.acc[3 * (size_t)n + c], acc.mx);
         }
     }
     if (sv.hist) {
@@ -776,6 +555,312 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
         for (uint32_t i = threadIdx.x; i < sv.n_bins; i += blockDim.x)
             if (lds_hist[i]) atomicAdd((unsigned long long*)&sv.hist[i], (unsigned long long)lds_hist[i]);
     }
+}
+
+// ------------------------------------------------------------ P1: segments
+// One wavefront per chain (keyed, faithful): jump from segment end to segment
+// end.  The chain's sigma arrays stay in VGPRs (64 lanes x NCH chunks) for the
+// whole window; hour/day fractions come from clock arithmetic (scalar).
+// hour / day fractions of step s (clearskyindexmodel.py:114-116) from the window's
+// local second-of-day at W0: 32-bit, wave-uniform arithmetic
+struct WinClock {
+    int32_t sod0;            // local second of day at W0
+    int32_t n;               // shifts inside the window
+    int32_t step[8], delta[8];   // window-relative shift steps and sizes
+};
+
+__device__ __forceinline__ WinClock win_clock(const tmh_clock& ck, int64_t W0)
+{
+    WinClock w;
+    const int64_t l0 = local_at(ck, W0);
+    w.sod0 = (int32_t)(l0 - floordiv(l0, 86400) * 86400);
+    w.n = 0;
+    for (int i = 0; i < ck.n_shifts && i < 8; ++i)
+        if (ck.shift_step[i] > W0) {
+            w.step[w.n] = (int32_t)(ck.shift_step[i] - W0);
+            w.delta[w.n] = ck.shift_delta[i];
+            ++w.n;
+        }
+    return w;
+}
+
+__device__ __forceinline__ void fractions_at(const WinClock& w, int32_t j, double& hour_f, double& day_f)
+{
+    int32_t sod = w.sod0 + j;
+    for (int i = 0; i < w.n; ++i)
+        if (j >= w.step[i]) sod += w.delta[i];
+    sod %= 86400;
+    if (sod < 0) sod += 86400;
+    const int hour = sod / 3600, minute = (sod / 60) % 60, second = sod % 60;
+    const double min_f = second / 60.0;
+    hour_f = (minute + min_f) / 60.0;
+    day_f = (hour + hour_f) / 24.0;
+}
+
+__global__ __launch_bounds__(256) void segments_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
+                                                       int64_t W0, uint32_t nsteps, tmh_clock ck,
+                                                       const int2* __restrict__ events,
+                                                       const uint32_t* __restrict__ n_events, SegView sg)
+{
+    const int lane = threadIdx.x & 63;
+    const uint32_t c = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    if (c >= n) return;   // whole wave
+    const uint64_t chain = chain0 + c;
+    const int64_t W1 = W0 + nsteps;
+    uint32_t status = st.status[c];
+    double ccb = st.sb[S_CC][c], cca = st.sa[S_CC][c], wsb = st.sb[S_WS][c], wsa = st.sa[S_WS][c];
+    int32_t fault = INT_MAX;
+    uint32_t nrec = 0;
+    if (status == 0) {
+        double cl = st.cl[c], clr = st.clr[c];
+        int L = st.L[c];
+        const int32_t sec = st.sec[c];
+        double vc[NCH], vl[NCH];
+        const double* gsc = sig_c(st, c);
+        const double* gsl = sig_l(st, c);
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+            const int k = ch * 64 + lane;
+            vc[ch] = k < L ? gsc[k] : 0.0;
+            vl[ch] = k < L ? gsl[k] : 0.0;
+        }
+        int64_t s_start = W0 - sec;   // step at which sec was 1
+        int32_t t1 = ceil_thr(cl), t2 = ceil_thr(cl + clr);
+        int64_t e = s_start + t2 - 1;
+        int2* rec = sg.rec + (size_t)c * sg.cap;
+        if (lane == 0) rec[0] = make_int2((int)(s_start + t1 - 1), (int)e);
+        nrec = 1;
+        const uint32_t nev = min(*n_events, ev_cap_dev(nsteps));
+        uint32_t ev = 0;
+        int64_t next_ev = nev > 0 ? events[0].x : INT64_MAX;
+        int64_t prev_call = INT64_MIN;
+        uint32_t call = 0;
+        auto apply_events = [&](int64_t upto) {   // _next_day / _next_hour at steps <= upto
+            while (next_ev <= upto) {
+                const int fl = events[ev].y;
+                if (fl & FL_DAY) {
+                    wsb = wsa;
+                    wsa = sg.evd[((size_t)ev * 4 + 1) * n + c];
+                }
+                if (fl & FL_HOUR) {
+                    ccb = cca;
+                    cca = sg.evd[(size_t)ev * 4 * n + c];
+                }
+                ++ev;
+                next_ev = ev < nev ? events[ev].x : INT64_MAX;
+            }
+        };
+        const WinClock wck = win_clock(ck, W0);
+        while (e < W1) {
+            apply_events(e);
+            double hf, df;
+            fractions_at(wck, (int32_t)(e - W0), hf, df);
+            const double hh = interp(ccb, cca, hf);
+            const double h = 0.95 < hh ? 0.95 : hh;   // update_parameters
+            const double ws = interp(wsb, wsa, df);
+            call = e == prev_call ? call + 1 : 0;
+            prev_call = e;
+            double ncl = 0.0, nclr = 0.0;
+            const uint32_t f = next_cloud_regs(dp, vc, vl, L, h, ws, chain, (uint64_t)e, call, lane, ncl, nclr);
+            if (f) {
+                status = f;
+                fault = (int32_t)(e - W0);
+                break;
+            }
+            cl = ncl;
+            clr = nclr;
+            t1 = ceil_thr(cl);
+            t2 = ceil_thr(cl + clr);
+            s_start = e;
+            e = s_start + t2 - 1;
+            if (nrec >= sg.cap) {
+                status = TMH_CHAIN_SEGMENT_OVERFLOW;
+                fault = (int32_t)(s_start - W0);
+                break;
+            }
+            if (lane == 0) rec[nrec] = make_int2((int)(s_start + t1 - 1), (int)e);
+            ++nrec;
+        }
+        if (status == 0) apply_events(W1 - 1);   // remaining boundaries of the window
+        double* wsc = sig_c(st, c);
+        double* wsl = sig_l(st, c);
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+            const int k = ch * 64 + lane;
+            if (k < L) {
+                wsc[k] = vc[ch];
+                wsl[k] = vl[ch];
+            }
+        }
+        if (lane == 0) {
+            st.sec[c] = (int32_t)(W1 - s_start);   // sec after step W1 - 1
+            st.cl[c] = cl;
+            st.clr[c] = clr;
+            st.L[c] = L;
+            st.ncalls[c] += nrec - 1;
+        }
+    }
+    if (lane == 0) {
+        sg.count[c] = nrec;
+        sg.fault[c] = fault;
+        sg.status[c] = status;
+        sg.end_p1[c] = ccb;
+        sg.end_p1[(size_t)n + c] = cca;
+        sg.end_p1[2 * (size_t)n + c] = wsb;
+        sg.end_p1[3 * (size_t)n + c] = wsa;
+    }
+}
+
+// ------------------------------------------------------------ P2: expand
+// One work-item per (chain, block of 256 seconds).  The boundary draws come
+// from the draw tables, so the per-second loop holds only the R copies of the
+// sampler pairs and does no fp64 work in fp32 mode.
+template <typename R>
+__global__ __launch_bounds__(256) void expand_kernel(KParams kp, StateView st, uint64_t chain0, uint32_t n,
+                                                     int64_t W0, uint32_t nsteps, int64_t utc0,
+                                                     const double* __restrict__ tab64,
+                                                     const float* __restrict__ tab32,
+                                                     const BlockDesc* __restrict__ desc, SegView sg, TraceView tr,
+                                                     StatsView sv)
+{
+    extern __shared__ uint32_t lds_hist[];
+    const uint32_t c = blockIdx.y * blockDim.x + threadIdx.x;   // grid: x = time block, y = chain block
+    const uint32_t b = blockIdx.x;
+    const bool live = c < n;
+    if (sv.hist) {
+        for (uint32_t i = threadIdx.x; i < sv.n_bins; i += blockDim.x) lds_hist[i] = 0;
+        __syncthreads();
+    }
+    const uint32_t j0 = b * BLOCK_STEPS, j1 = min(j0 + (uint32_t)BLOCK_STEPS, nsteps);
+    const uint64_t chain = chain0 + c;
+    const int64_t fm = first_minute(utc0, W0);
+    Acc acc{0.0, 0.0, 0.0, -INFINITY};
+    bool alive = false;
+    int32_t fault = INT_MAX;
+    int2 seg = make_int2(0, 0);
+    const int2* rec = sg.rec + (size_t)(live ? c : 0) * sg.cap;
+    uint32_t jr = 0, evi = 0;
+    FSamp<R> fs;
+    if (live) {
+        alive = st.status[c] == 0;
+        fault = sg.fault[c];
+        Samp s;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            s.b[k] = st.sb[k][c];
+            s.a[k] = st.sa[k][c];
+        }
+        const BlockDesc d = desc[b];
+        evi = (uint32_t)d.evi;
+        if (alive && b > 0) samplers_at(d, sg, n, c, s);
+        to_real(fs, s);
+    }
+    if (alive) {   // segment containing the block start: first record with next-call step > start
+        const int64_t s0 = W0 + j0;
+        int lo = 0, hi = (int)sg.count[c] - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if ((int64_t)rec[mid].y > s0) hi = mid;
+            else lo = mid + 1;
+        }
+        jr = (uint32_t)lo;
+        seg = rec[jr];
+    }
+    const double* evd = sg.evd + c;
+    const double* mind = sg.mind + c;
+    for (uint32_t j = j0; j < j1; ++j) {
+        const int64_t step = W0 + j;
+        const float* r32 = tab32 + (size_t)j * ROW;
+        const uint32_t fl = __float_as_uint(r32[G_FLAGS]);
+        R row[ROW];
+#pragma unroll
+        for (int i = 0; i < ROW; ++i) row[i] = sizeof(R) == 8 ? (R)tab64[(size_t)j * ROW + i] : (R)r32[i];
+        R csi = R(NAN), pv = R(NAN), meter = R(NAN), res = R(NAN);
+        uint8_t cov = 255;
+        const bool ok = alive && (int32_t)j < fault;
+        if (ok) {
+            if (fl & (FL_DAY | FL_HOUR)) {            // _next_day, _next_hour
+                const size_t eo = (size_t)evi * 4 * n;
+                if (fl & FL_DAY) {
+                    fs.b[S_CLEAR_DAY] = fs.a[S_CLEAR_DAY];
+                    fs.a[S_CLEAR_DAY] = (R)evd[eo + 2 * (size_t)n];
+                }
+                if (fl & FL_HOUR) {
+                    fs.b[S_CC] = fs.a[S_CC];
+                    fs.a[S_CC] = (R)evd[eo];
+                    fs.b[S_CLEAR_DAY] = fs.a[S_CLEAR_DAY];
+                    fs.a[S_CLEAR_DAY] = (R)evd[eo + 3 * (size_t)n];
+                }
+            }
+            if (fl & FL_MIN) {                         // _next_min
+                const size_t q = (size_t)((j - fm) / 60);
+                fs.b[S_CLOUDY_NOISE] = fs.a[S_CLOUDY_NOISE];
+                fs.a[S_CLOUDY_NOISE] = (R)mind[q * 2 * n];
+                fs.b[S_CLEAR_NOISE] = fs.a[S_CLEAR_NOISE];
+                fs.a[S_CLEAR_NOISE] = (R)mind[(q * 2 + 1) * n];
+            }
+            while (step >= (int64_t)seg.y) seg = rec[++jr];   // next_cloud happened at seg.y
+            const bool covered = step < (int64_t)seg.x;
+            cov = covered ? 1 : 0;
+            const U4 u = keyed_block(kp.seed, chain, (uint64_t)step, TAG_STEP, 0);
+            second_body<R>(kp, row, fl, fs, covered, u52(u.x, u.y), u52(u.z, u.w), csi, pv, meter, res);
+        }
+        if (fl & (FL_DAY | FL_HOUR)) ++evi;
+        if (live) emit<R>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok);
+    }
+    if (live && sv.acc) {
+        const size_t o = (size_t)b * n + c, stride = (size_t)sg.nblk * n;
+        sg.part[o] = acc.pv;
+        sg.part[stride + o] = acc.m;
+        sg.part[2 * stride + o] = acc.r;
+        sg.part[3 * stride + o] = acc.mx;
+    }
+    if (sv.hist) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < sv.n_bins; i += blockDim.x)
+            if (lds_hist[i]) atomicAdd((unsigned long long*)&sv.hist[i], (unsigned long long)lds_hist[i]);
+    }
+}
+
+// Stats partials -> per-chain accumulators (fixed order: deterministic), then
+// the window-end state of P1/P2 -> chain state.
+__global__ __launch_bounds__(256) void commit_kernel(StateView st, uint32_t n, SegView sg, StatsView sv,
+                                                     const BlockDesc* __restrict__ desc_end)
+{
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    if (sv.acc) {
+        const size_t stride = (size_t)sg.nblk * n;
+        double p = 0.0, m = 0.0, r = 0.0, mx = -INFINITY;
+        for (uint32_t b = 0; b < sg.nblk; ++b) {
+            const size_t o = (size_t)b * n + c;
+            p += sg.part[o];
+            m += sg.part[stride + o];
+            r += sg.part[2 * stride + o];
+            mx = fmax(mx, sg.part[3 * stride + o]);
+        }
+        sv.acc[c] += p;
+        sv.acc[(size_t)n + c] += m;
+        sv.acc[2 * (size_t)n + c] += r;
+        sv.acc[3 * (size_t)n + c] = fmax(sv.acc[3 * (size_t)n + c], mx);
+    }
+    if (st.status[c] != 0) return;
+    st.status[c] = sg.status[c];
+    if (sg.status[c] != 0) return;
+    Samp sp;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        sp.b[k] = st.sb[k][c];
+        sp.a[k] = st.sa[k][c];
+    }
+    samplers_at(*desc_end, sg, n, c, sp);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {   // cc, clear_day, cloudy_hour (unchanged), noises
+        st.sb[k][c] = sp.b[k];
+        st.sa[k][c] = sp.a[k];
+    }
+    st.sb[S_WS][c] = sg.end_p1[2 * (size_t)n + c];
+    st.sa[S_WS][c] = sg.end_p1[3 * (size_t)n + c];
 }
 
 __global__ void probe_kernel(int fn, double a, const double* x, double* out, uint32_t n)
@@ -789,6 +874,15 @@ __global__ void probe_kernel(int fn, double a, const double* x, double* out, uin
         case 2: v = stdtrit(a, x[i]); break;
         case 3: v = al_ppf(x[i], a); break;
         case 4: v = (double)ndtri_f(x[i]); break;
+        case 5: {   // wavefront argmin (first index on ties) of x[wave lanes]; needs full waves
+            double dm;
+            int km;
+            argmin_first(x[i], (int)(i & 63), dm, km);
+            v = (double)km;
+            break;
+        }
+        case 6: v = dpp_f64<0x138>(a, x[i]); break;            // wave_shr:1, lane 0 <- a
+        case 7: v = readlane_f64(x[i], 63); break;
         default: v = NAN;
     }
     out[i] = v;
@@ -817,7 +911,7 @@ int hip_check(hipError_t e, const char* what)
 constexpr size_t ALIGN = 256;
 size_t align_up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
-// field order: sb[6], sa[6], cl, clr, mstate, sec, L, pos, status, ncalls, sigma_cloud, sigma_clear, -, -
+// state field order: sb[6], sa[6], cl, clr, mstate, sec, L, pos, status, ncalls, sigma_cloud, sigma_clear, -, -
 void state_layout(uint32_t n, uint64_t* off, size_t* total)
 {
     size_t o = 0;
@@ -858,12 +952,80 @@ StateView make_view(void* base, uint32_t n)
     return v;
 }
 
+// plan: tab64 | tab32 | events | n_events | block descriptors
+uint32_t ev_cap(uint32_t n_steps) { return n_steps / 1800 + 64; }
+uint32_t nblk_of(uint32_t n_steps) { return (n_steps + BLOCK_STEPS - 1) / BLOCK_STEPS; }
+
+struct PlanView {
+    double* tab64;
+    float* tab32;
+    int2* events;
+    uint32_t* n_events;
+    BlockDesc* desc;
+};
+
+size_t plan_layout(uint32_t n_steps, void* base, PlanView* v)
+{
+    size_t o = 0;
+    char* b = (char*)base;
+    if (v) v->tab64 = (double*)(b + o);
+    o += align_up((size_t)n_steps * ROW * 8);
+    if (v) v->tab32 = (float*)(b + o);
+    o += align_up((size_t)n_steps * ROW * 4);
+    if (v) v->events = (int2*)(b + o);
+    o += align_up((size_t)ev_cap(n_steps) * 8);
+    if (v) v->n_events = (uint32_t*)(b + o);
+    o += ALIGN;
+    if (v) v->desc = (BlockDesc*)(b + o);
+    o += align_up((size_t)(nblk_of(n_steps) + 1) * sizeof(BlockDesc));
+    return o;
+}
+
+uint32_t seg_cap(uint32_t n_steps) { return n_steps / 8 + 64; }
+
+size_t scratch_layout(uint32_t n, uint32_t n_steps, void* base, SegView* v)
+{
+    size_t o = 0;
+    char* b = (char*)base;
+    const uint32_t nblk = nblk_of(n_steps);
+    if (v) {
+        v->cap = seg_cap(n_steps);
+        v->nblk = nblk;
+        v->rec = (int2*)(b + o);
+    }
+    o += align_up((size_t)n * seg_cap(n_steps) * 8);
+    if (v) v->count = (uint32_t*)(b + o);
+    o += align_up((size_t)n * 4);
+    if (v) v->fault = (int32_t*)(b + o);
+    o += align_up((size_t)n * 4);
+    if (v) v->status = (uint32_t*)(b + o);
+    o += align_up((size_t)n * 4);
+    if (v) v->end_p1 = (double*)(b + o);
+    o += align_up((size_t)n * 4 * 8);
+    if (v) v->end_p2 = (double*)(b + o);
+    o += align_up((size_t)n * 6 * 8);
+    if (v) v->part = (double*)(b + o);
+    o += align_up((size_t)n * nblk * 4 * 8);
+    const uint32_t evc = ev_cap(n_steps), nmin = n_steps / 60 + 2;
+    if (v) {
+        v->evcap = evc;
+        v->nmin = nmin;
+        v->evd = (double*)(b + o);
+    }
+    o += align_up((size_t)n * evc * 4 * 8);
+    if (v) v->mind = (double*)(b + o);
+    o += align_up((size_t)n * nmin * 2 * 8);
+    return o;
+}
+
 }  // namespace
 
 struct tmh_engine {
     KParams kp;
+    DrawParams dp;
     GParams gp;
     int device;
+    int path;   // resolved kernel path: 1 sequential, 2 time-parallel
 };
 
 extern "C" {
@@ -888,15 +1050,39 @@ int tmh_state_offsets(uint32_t n_chains, uint64_t* offsets)
     return TMH_OK;
 }
 
-size_t tmh_workspace_bytes(uint32_t n_steps) { return align_up((size_t)n_steps * ROW * 8) + align_up((size_t)n_steps * ROW * 4); }
+size_t tmh_plan_bytes(uint32_t n_steps) { return plan_layout(n_steps, nullptr, nullptr); }
+
+size_t tmh_scratch_bytes(uint32_t n_chains, uint32_t n_steps)
+{
+    return scratch_layout(n_chains, n_steps, nullptr, nullptr);
+}
+
+size_t tmh_workspace_bytes(uint32_t n_chains, uint32_t n_steps)
+{
+    return tmh_plan_bytes(n_steps) + tmh_scratch_bytes(n_chains, n_steps);
+}
 
 int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, struct tmh_engine** out)
 {
     if (!p || !clock || !out) return fail(TMH_E_INVAL, "NULL argument to tmh_engine_create");
-    if (p->cc_mode != TMH_CC_FAITHFUL && p->cc_mode != TMH_CC_MARKOV) return fail(TMH_E_INVAL, "bad cc_mode %d", p->cc_mode);
-    if (p->rng_mode != TMH_RNG_KEYED && p->rng_mode != TMH_RNG_INJECTED) return fail(TMH_E_INVAL, "bad rng_mode %d", p->rng_mode);
-    if (p->precision != TMH_FP32 && p->precision != TMH_FP64) return fail(TMH_E_INVAL, "bad precision %d", p->precision);
+    if (p->cc_mode != TMH_CC_FAITHFUL && p->cc_mode != TMH_CC_MARKOV)
+        return fail(TMH_E_INVAL, "bad cc_mode %d", p->cc_mode);
+    if (p->rng_mode != TMH_RNG_KEYED && p->rng_mode != TMH_RNG_INJECTED)
+        return fail(TMH_E_INVAL, "bad rng_mode %d", p->rng_mode);
+    if (p->precision != TMH_FP32 && p->precision != TMH_FP64)
+        return fail(TMH_E_INVAL, "bad precision %d", p->precision);
+    if (p->kernel_path < TMH_PATH_AUTO || p->kernel_path > TMH_PATH_TIME_PARALLEL)
+        return fail(TMH_E_INVAL, "bad kernel_path %d", p->kernel_path);
     if (clock->n_shifts < 0 || clock->n_shifts > 8) return fail(TMH_E_INVAL, "bad n_shifts %d", clock->n_shifts);
+    // the time-parallel path needs every draw keyed by step, the reference's
+    // memoryless (faithful) hourly draw, and whole-minute UTC offsets
+    bool minutes = ((clock->local0 - clock->utc0) % 60) == 0;
+    for (int i = 0; i < clock->n_shifts; ++i) minutes = minutes && (clock->shift_delta[i] % 60) == 0;
+    const bool tp_ok = p->rng_mode == TMH_RNG_KEYED && p->cc_mode == TMH_CC_FAITHFUL && minutes;
+    int path = p->kernel_path == TMH_PATH_AUTO ? (tp_ok ? TMH_PATH_TIME_PARALLEL : TMH_PATH_SEQUENTIAL)
+                                               : p->kernel_path;
+    if (path == TMH_PATH_TIME_PARALLEL && !tp_ok)
+        return fail(TMH_E_INVAL, "kernel_path time-parallel needs keyed rng, faithful cc mode, whole-minute offsets");
     int ndev = 0;
     if (int rc = hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount")) return rc;
     if (device < 0 || device >= ndev) return fail(TMH_E_INVAL, "device %d out of range (%d devices)", device, ndev);
@@ -927,7 +1113,21 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
     memcpy(e->gp.linke, p->linke, sizeof e->gp.linke);
     memcpy(e->gp.module, p->module, sizeof e->gp.module);
     e->gp.clock = *clock;
+    DrawParams& d = e->dp;
+    memset(&d, 0, sizeof d);
+    d.seed = k.seed;
+    d.alpha = k.alpha;
+    d.delta = k.delta;
+    d.expo = k.expo;
+    d.sqrt09 = k.sqrt09;
+    int fb = 0;   // bin of a fresh generator: searchsorted(edges, 1.0)
+    while (fb < 5 && p->edges[fb] < 1.0) ++fb;
+    d.fb_is_t = p->shape_is_t[fb];
+    d.fb_k = d.fb_is_t ? p->shapes[fb][3] : p->shapes[fb][2];
+    d.fb_scale = p->shapes[fb][1];
+    d.fb_loc = p->shapes[fb][0];
     e->device = device;
+    e->path = path;
     *out = e;
     return TMH_OK;
 }
@@ -937,6 +1137,8 @@ int tmh_engine_destroy(struct tmh_engine* eng)
     delete eng;
     return TMH_OK;
 }
+
+int tmh_engine_path(const struct tmh_engine* eng) { return eng ? eng->path : TMH_E_INVAL; }
 
 int tmh_init(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, const tmh_ustream* inj,
              void* stream)
@@ -961,34 +1163,48 @@ int tmh_init(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
     return hip_check(hipGetLastError(), "init_kernel launch");
 }
 
-int tmh_geometry(struct tmh_engine* eng, int64_t step0, uint32_t n_steps, double* table, void* stream)
+int tmh_plan(struct tmh_engine* eng, int64_t step0, uint32_t n_steps, void* plan, void* stream)
 {
-    if (!eng || !table) return fail(TMH_E_INVAL, "NULL engine/table");
+    if (!eng || !plan) return fail(TMH_E_INVAL, "NULL engine/plan");
     if (n_steps == 0) return TMH_OK;
-    if (step0 < 0) return fail(TMH_E_INVAL, "negative step0");
+    if (step0 < 0 || step0 + (int64_t)n_steps > (int64_t)INT_MAX - (1 << 20))
+        return fail(TMH_E_INVAL, "step window [%lld, +%u) outside [0, 2^31 - 2^20)", (long long)step0, n_steps);
     if (int rc = hip_check(hipSetDevice(eng->device), "hipSetDevice")) return rc;
-    float* t32 = (float*)((char*)table + align_up((size_t)n_steps * ROW * 8));
-    hipLaunchKernelGGL(geom_kernel, dim3((n_steps + 255) / 256), dim3(256), 0, (hipStream_t)stream, eng->gp, step0,
-                       n_steps, table, t32);
-    return hip_check(hipGetLastError(), "geom_kernel launch");
+    PlanView pv;
+    plan_layout(n_steps, plan, &pv);
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(geom_kernel, dim3((n_steps + 255) / 256), dim3(256), 0, s, eng->gp, step0, n_steps, pv.tab64,
+                       pv.tab32);
+    hipLaunchKernelGGL(events_kernel, dim3(1), dim3(1024), 0, s, pv.tab32, step0, n_steps, eng->gp.clock.utc0,
+                       pv.events, ev_cap(n_steps), pv.n_events);
+    const uint32_t nb = nblk_of(n_steps);
+    hipLaunchKernelGGL(desc_kernel, dim3((nb + 1 + 255) / 256), dim3(256), 0, s, step0, n_steps, eng->gp.clock.utc0,
+                       pv.events, pv.n_events, pv.desc, nb);
+    return hip_check(hipGetLastError(), "plan kernels launch");
 }
 
 int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, int64_t step0,
              uint32_t n_steps, const tmh_ustream* inj, const tmh_trace* trace, const tmh_stats* stats,
-             const void* table, void* stream)
+             const void* plan, void* scratch, size_t scratch_bytes, void* stream)
 {
-    if (!eng || !state || !table) return fail(TMH_E_INVAL, "NULL engine/state/table");
+    if (!eng || !state || !plan) return fail(TMH_E_INVAL, "NULL engine/state/plan");
     if (n_chains == 0 || n_steps == 0) return TMH_OK;
-    if (step0 < 0) return fail(TMH_E_INVAL, "negative step0");
+    if (step0 < 0 || step0 + (int64_t)n_steps > (int64_t)INT_MAX - (1 << 20))
+        return fail(TMH_E_INVAL, "step window [%lld, +%u) outside [0, 2^31 - 2^20)", (long long)step0, n_steps);
+    if ((n_chains + 255) / 256 > 65535) return fail(TMH_E_INVAL, "n_chains %u > 16,776,960 per call", n_chains);
     if (eng->kp.rng_mode == TMH_RNG_INJECTED && (!inj || !inj->u || inj->stride < inj->len))
         return fail(TMH_E_INVAL, "injected mode needs a stream with stride >= len");
-    if (trace && (trace->csi || trace->pv || trace->meter || trace->residual || trace->covered) && trace->ld < n_chains)
+    if (trace && (trace->csi || trace->pv || trace->meter || trace->residual || trace->covered) &&
+        trace->ld < n_chains)
         return fail(TMH_E_INVAL, "trace ld %llu < n_chains %u", (unsigned long long)trace->ld, n_chains);
     if (stats && stats->hist && (stats->n_bins == 0 || stats->n_bins > 16384 || !(stats->hi > stats->lo)))
         return fail(TMH_E_INVAL, "bad histogram spec (n_bins %u in [1,16384], hi > lo)", stats->n_bins);
+    const bool tp = eng->path == TMH_PATH_TIME_PARALLEL;
+    if (tp && (!scratch || scratch_bytes < tmh_scratch_bytes(n_chains, n_steps)))
+        return fail(TMH_E_INVAL, "scratch too small: %zu < %zu", scratch_bytes, tmh_scratch_bytes(n_chains, n_steps));
     if (int rc = hip_check(hipSetDevice(eng->device), "hipSetDevice")) return rc;
-    const double* t64 = (const double*)table;
-    const float* t32 = (const float*)((const char*)table + align_up((size_t)n_steps * ROW * 8));
+    PlanView pv;
+    plan_layout(n_steps, (void*)plan, &pv);
     StateView v = make_view(state, n_chains);
     InjView iv{inj ? inj->u : nullptr, inj ? inj->stride : 0, inj ? inj->len : 0};
     TraceView tv{};
@@ -1003,18 +1219,41 @@ int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
         sv.acc = stats->chain_acc;
         lds = stats->hist ? (size_t)stats->n_bins * 4 : 0;
     }
-    dim3 grid((n_chains + 255) / 256), block(256);
     hipStream_t s = (hipStream_t)stream;
     const bool f64 = eng->kp.precision == TMH_FP64, keyed = eng->kp.rng_mode == TMH_RNG_KEYED;
+    if (!tp) {
+        dim3 grid((n_chains + 255) / 256), block(256);
 #define LAUNCH(R, M)                                                                                                 \
-    hipLaunchKernelGGL((chain_kernel<R, M>), grid, block, lds, s, eng->kp, v, chain0, n_chains, step0, n_steps, t64, \
-                       t32, iv, tv, sv)
-    if (f64 && keyed) LAUNCH(double, TMH_RNG_KEYED);
-    else if (f64) LAUNCH(double, TMH_RNG_INJECTED);
-    else if (keyed) LAUNCH(float, TMH_RNG_KEYED);
-    else LAUNCH(float, TMH_RNG_INJECTED);
+    hipLaunchKernelGGL((chain_kernel<R, M>), grid, block, lds, s, eng->kp, v, chain0, n_chains, step0, n_steps,      \
+                       pv.tab64, pv.tab32, iv, tv, sv)
+        if (f64 && keyed) LAUNCH(double, TMH_RNG_KEYED);
+        else if (f64) LAUNCH(double, TMH_RNG_INJECTED);
+        else if (keyed) LAUNCH(float, TMH_RNG_KEYED);
+        else LAUNCH(float, TMH_RNG_INJECTED);
 #undef LAUNCH
-    return hip_check(hipGetLastError(), "chain_kernel launch");
+        return hip_check(hipGetLastError(), "chain_kernel launch");
+    }
+    SegView sg;
+    scratch_layout(n_chains, n_steps, scratch, &sg);
+    const uint32_t cb = (n_chains + 255) / 256;
+    const int64_t utc0 = eng->gp.clock.utc0;
+    hipLaunchKernelGGL(event_draws_kernel, dim3(sg.evcap, cb), dim3(256), 0, s, eng->dp, chain0, n_chains, n_steps,
+                       pv.events, pv.n_events, sg.evd);
+    hipLaunchKernelGGL(minute_draws_kernel, dim3(sg.nmin, cb), dim3(256), 0, s, eng->dp, v, chain0, n_chains, step0,
+                       n_steps, utc0, pv.tab64, pv.events, pv.n_events, sg.evd, sg.mind);
+    hipLaunchKernelGGL(segments_kernel, dim3((n_chains + 3) / 4), dim3(256), 0, s, eng->dp, v, chain0, n_chains,
+                       step0, n_steps, eng->gp.clock, pv.events, pv.n_events, sg);
+    if (int rc = hip_check(hipGetLastError(), "draws/segments kernels launch")) return rc;
+    dim3 grid2(nblk_of(n_steps), cb);
+    if (f64)
+        hipLaunchKernelGGL(expand_kernel<double>, grid2, dim3(256), lds, s, eng->kp, v, chain0, n_chains, step0,
+                           n_steps, utc0, pv.tab64, pv.tab32, pv.desc, sg, tv, sv);
+    else
+        hipLaunchKernelGGL(expand_kernel<float>, grid2, dim3(256), lds, s, eng->kp, v, chain0, n_chains, step0,
+                           n_steps, utc0, pv.tab64, pv.tab32, pv.desc, sg, tv, sv);
+    if (int rc = hip_check(hipGetLastError(), "expand_kernel launch")) return rc;
+    hipLaunchKernelGGL(commit_kernel, dim3(cb), dim3(256), 0, s, v, n_chains, sg, sv, pv.desc + nblk_of(n_steps));
+    return hip_check(hipGetLastError(), "commit_kernel launch");
 }
 
 int tmh_run(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, int64_t step0,
@@ -1023,10 +1262,13 @@ int tmh_run(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_cha
 {
     if (!eng || !state) return fail(TMH_E_INVAL, "NULL engine/state");
     if (n_chains == 0 || n_steps == 0) return TMH_OK;
-    if (!workspace || workspace_bytes < tmh_workspace_bytes(n_steps))
-        return fail(TMH_E_INVAL, "workspace too small: %zu < %zu", workspace_bytes, tmh_workspace_bytes(n_steps));
-    if (int rc = tmh_geometry(eng, step0, n_steps, (double*)workspace, stream)) return rc;
-    return tmh_step(eng, state, chain0, n_chains, step0, n_steps, inj, trace, stats, workspace, stream);
+    const size_t pb = tmh_plan_bytes(n_steps);
+    const size_t need = eng->path == TMH_PATH_TIME_PARALLEL ? pb + tmh_scratch_bytes(n_chains, n_steps) : pb;
+    if (!workspace || workspace_bytes < need)
+        return fail(TMH_E_INVAL, "workspace too small: %zu < %zu", workspace_bytes, need);
+    if (int rc = tmh_plan(eng, step0, n_steps, workspace, stream)) return rc;
+    return tmh_step(eng, state, chain0, n_chains, step0, n_steps, inj, trace, stats, workspace,
+                    (char*)workspace + pb, workspace_bytes - pb, stream);
 }
 
 int tmh_probe(int fn, double a, const double* x, double* out, uint32_t n, void* stream)

@@ -66,7 +66,7 @@ __device__ __forceinline__ U4 keyed_block(uint64_t seed, uint64_t chain, uint64_
 // standard normal quantile (fp64).  ocml's ncdfinv, polished by one Halley
 // step on the erfc/erf residual so the result is within ~1 ulp of the exact
 // quantile (the oracle's and scipy's ndtri agree to ~1e-16).
-__device__ __forceinline__ double ndtri(double p)
+__device__ __noinline__ double ndtri(double p)
 {
     double x = normcdfinv(p);
     if (!(p > 0.0) || !(p < 1.0)) return x;
@@ -88,7 +88,7 @@ __device__ __forceinline__ float ndtri_f(double u)
     return u < 0.5 ? z : -z;
 }
 
-__device__ inline void gamma_pq(double a, double x, double lga, double& P, double& Q)
+__device__ __noinline__ void gamma_pq(double a, double x, double lga, double& P, double& Q)
 {
     if (x <= 0.0) {
         P = 0.0;
@@ -126,7 +126,7 @@ __device__ inline void gamma_pq(double a, double x, double lga, double& P, doubl
 }
 
 // inverse regularized lower incomplete gamma (scipy.special.gammaincinv)
-__device__ inline double gammaincinv(double a, double p)
+__device__ __noinline__ double gammaincinv(double a, double p)
 {
     if (!(p > 0.0)) return 0.0;
     if (!(p < 1.0)) return INFINITY;
@@ -137,7 +137,7 @@ __device__ inline double gammaincinv(double a, double p)
     double x = a * w * w * w;
     const double lg = lgamma(a);
     if (!(x > 1e-3 * a)) x = exp((log(p) + lgamma(a + 1.0)) / a);
-    for (int it = 0; it < 100; ++it) {
+    for (int it = 0; it < 8; ++it) {   // Halley from Wilson-Hilferty: 2-3 steps reach ~1 ulp
         double P, Q;
         gamma_pq(a, x, lg, P, Q);
         const double f = upper ? Q - target : P - target;
@@ -148,7 +148,7 @@ __device__ inline double gammaincinv(double a, double p)
         const double hstep = t / (1.0 - 0.5 * t * ((a - 1.0) / x - 1.0));
         double xn = x - hstep;
         if (xn <= 0.0) xn = 0.5 * x;
-        if (fabs(xn - x) <= 4e-16 * xn) {
+        if (fabs(xn - x) <= 1e-15 * xn) {
             x = xn;
             break;
         }
@@ -157,7 +157,7 @@ __device__ inline double gammaincinv(double a, double p)
     return x;
 }
 
-__device__ inline double betacf(double a, double b, double x)
+__device__ __noinline__ double betacf(double a, double b, double x)
 {
     const double qab = a + b, qap = a + 1.0, qam = a - 1.0;
     double c = 1.0, d = 1.0 - qab * x / qap;
@@ -186,7 +186,7 @@ __device__ inline double betacf(double a, double b, double x)
     return h;
 }
 
-__device__ inline double ibeta(double a, double b, double x)
+__device__ __noinline__ double ibeta(double a, double b, double x)
 {
     if (x <= 0.0) return 0.0;
     if (x >= 1.0) return 1.0;
@@ -195,7 +195,7 @@ __device__ inline double ibeta(double a, double b, double x)
     return 1.0 - exp(lbt) * betacf(b, a, 1.0 - x) / b;
 }
 
-__device__ inline double t_resid(double df, double t, double p)
+__device__ __noinline__ double t_resid(double df, double t, double p)
 {
     const double t2 = t * t;
     if (t2 < df) return (0.5 - p) - 0.5 * ibeta(0.5, 0.5 * df, t2 / (df + t2));
@@ -203,7 +203,7 @@ __device__ inline double t_resid(double df, double t, double p)
 }
 
 // inverse Student-t CDF (scipy.special.stdtrit), lower half; upper by symmetry
-__device__ inline double stdtrit(double df, double p)
+__device__ __noinline__ double stdtrit(double df, double p)
 {
     if (!(p > 0.0)) return -INFINITY;
     if (!(p < 1.0)) return INFINITY;
@@ -234,7 +234,7 @@ __device__ inline double stdtrit(double df, double p)
             tn = t - f / exp(ldens);
         }
         if (tn >= 0.0) tn = 0.5 * t;
-        if (fabs(tn - t) <= 4e-16 * fabs(tn)) {
+        if (fabs(tn - t) <= 1e-15 * fabs(tn)) {
             t = tn;
             break;
         }
@@ -244,11 +244,14 @@ __device__ inline double stdtrit(double df, double p)
 }
 
 // asymmetric Laplace ppf, cloud_cover_hourly.py:100-104 (op order kept)
-__device__ __forceinline__ double al_ppf(double y, double kappa)
+__device__ __noinline__ double al_ppf(double y, double kappa)
 {
     const double k2 = kappa * kappa;
     if (y < k2 / (1.0 + k2)) return kappa * log((1.0 + k2) / k2 * y);
     return -1.0 / kappa * log((1.0 + k2) * (1.0 - y));
 }
+
+// fp64 pow out of line (cloud lengths, cloud_cover_binary.py:40): keeps callers' registers low
+__device__ __noinline__ double pow_d(double x, double y) { return pow(x, y); }
 
 }  // namespace tmh

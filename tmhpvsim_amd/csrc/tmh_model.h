@@ -1,0 +1,675 @@
+// Model pieces shared by every tmhpvsim kernel (gfx950).  Reference lines
+// restated are cited at each function (paths relative to tmhpvsim/).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <climits>
+
+#include "tmh_math.h"
+#include "tmhpvsim.h"
+
+namespace tmh {
+
+#define CAP TMH_SIGMA_CAP
+#define ROW TMH_GEOM_FIELDS
+
+// ------------------------------------------------------------ parameters
+struct KParams {
+    int32_t cc_mode, rng_mode, with_pv, precision;
+    uint64_t seed;
+    double shapes[6][4];
+    int32_t is_t[6];
+    double edges[6];
+    double module[TMH_MOD_COUNT];
+    double inverter[TMH_INV_COUNT];
+    double alpha, delta, expo, sqrt09, sqrt6;   // cloud_cover_binary.py:35-40, scales
+    double temp_air, wind;                      // sapm_celltemp inputs (pvmodel.py:69-70)
+};
+
+struct GParams {
+    double site[8];
+    double linke[12];
+    double module[TMH_MOD_COUNT];
+    tmh_clock clock;
+};
+
+enum : uint32_t { FL_DAY = 1, FL_HOUR = 2, FL_MIN = 4, FL_NIGHT = 8 };
+// clock/geometry table row (TMH_GEOM_FIELDS = 20)
+enum {
+    G_MINF = 0, G_HOURF = 1, G_DAYF = 2, G_FLAGS = 3, G_COSZ = 4, G_CSIMAX = 5, G_GHICS = 6,
+    G_I0H = 7, G_I0 = 8, G_KNC = 9, G_AM = 10, G_DISCOK = 11, G_RB = 12, G_DNIEXTRA = 13,
+    G_TERM2 = 14, G_GFAC = 15, G_COSAOI = 16, G_F1 = 17, G_F2 = 18
+};
+
+enum { S_CC = 0, S_CLEAR_DAY = 1, S_CLOUDY_HOUR = 2, S_CLOUDY_NOISE = 3, S_CLEAR_NOISE = 4, S_WS = 5 };
+
+// chain state, structure of arrays; sigma arrays chain-major [n][CAP] so the
+// wave-cooperative next_cloud scans one chain's arrays with coalesced loads
+struct StateView {
+    double* sb[6];
+    double* sa[6];
+    double *cl, *clr, *mstate;
+    int32_t *sec, *L;
+    uint32_t *pos, *status, *ncalls;
+    double *sc, *sl;
+    uint32_t n;
+};
+
+struct InjView {
+    const double* u;
+    uint64_t stride, len;
+};
+
+struct TraceView {
+    void *csi, *pv, *meter, *residual;
+    uint8_t* covered;
+    uint64_t ld;
+};
+
+struct StatsView {
+    uint64_t* hist;
+    uint32_t n_bins;
+    double lo, scale;
+    double* acc;
+};
+
+struct Samp {
+    double b[6], a[6];
+};
+
+struct Chain {
+    Samp s;
+    double cl, clr, mstate;
+    int32_t sec, L, t1, t2;
+    uint32_t pos, status, ncalls;
+};
+
+// ------------------------------------------------------------ rng sources
+template <int RNG>
+struct Draw;
+
+template <>
+struct Draw<TMH_RNG_KEYED> {
+    uint64_t seed, chain;
+    __device__ __forceinline__ double one(Chain&, uint64_t step, uint32_t tag, uint32_t sub, int half) const
+    {
+        const U4 b = keyed_block(seed, chain, step, tag, sub);
+        return half ? u52(b.z, b.w) : u52(b.x, b.y);
+    }
+    __device__ __forceinline__ void two(Chain&, uint64_t step, uint32_t tag, uint32_t sub, double& u0,
+                                        double& u1) const
+    {
+        const U4 b = keyed_block(seed, chain, step, tag, sub);
+        u0 = u52(b.x, b.y);
+        u1 = u52(b.z, b.w);
+    }
+};
+
+template <>
+struct Draw<TMH_RNG_INJECTED> {
+    const double* u;
+    uint64_t len;
+    __device__ __forceinline__ double one(Chain& ch, uint64_t, uint32_t, uint32_t, int) const
+    {
+        if (ch.pos >= len) {
+            if (!ch.status) ch.status = TMH_CHAIN_U_EXHAUSTED;
+            return 0.5;
+        }
+        return u[ch.pos++];
+    }
+    __device__ __forceinline__ void two(Chain& ch, uint64_t s, uint32_t t, uint32_t sub, double& u0,
+                                        double& u1) const
+    {
+        u0 = one(ch, s, t, sub, 0);
+        u1 = one(ch, s, t, sub, 1);
+    }
+};
+
+__device__ __forceinline__ double keyed_u(uint64_t seed, uint64_t chain, uint64_t step, uint32_t tag, uint32_t sub,
+                                          int half)
+{
+    const U4 b = keyed_block(seed, chain, step, tag, sub);
+    return half ? u52(b.z, b.w) : u52(b.x, b.y);
+}
+
+// ------------------------------------------------------------ model pieces
+// InterpolatedSampler.interpolate, clearskyindexmodel.py:39-40 (op order kept)
+__device__ __forceinline__ double interp(double b, double a, double f) { return f * a + (1.0 - f) * b; }
+
+__device__ __forceinline__ void push(Samp& s, int k, double v)
+{   // InterpolatedSampler.__next__, clearskyindexmodel.py:34-37
+    s.b[k] = s.a[k];
+    s.a[k] = v;
+}
+
+__device__ __forceinline__ double normal(double u, double loc, double scale) { return ndtri(u) * scale + loc; }
+
+__device__ __forceinline__ double scaled_noise(const KParams& kp, double u, double s0, double s1, double cc)
+{   // norm.rvs(loc=1., scale=np.sqrt(0.9) * (sigma0 + sigma1 * 8 * cc)), clearskyindexmodel.py:86-88
+    return normal(u, 1.0, kp.sqrt09 * (s0 + s1 * 8 * cc));
+}
+
+// hourly cloud cover: next(get_cloud_cover(distributions)) (cloud_cover_hourly.py:309-316);
+// faithful = a fresh generator per draw, i.e. state 1.0 (clearskyindexmodel.py:61-63)
+__device__ __forceinline__ double draw_cc_from(const KParams& kp, double state, double u)
+{
+    int bin = 0;
+    while (bin < 5 && kp.edges[bin] < state) ++bin;   // np.searchsorted(bins, state)
+    double v = kp.is_t[bin] ? stdtrit(kp.shapes[bin][3], u) : al_ppf(u, kp.shapes[bin][2]);
+    v = v * kp.shapes[bin][1] + kp.shapes[bin][0];   // scipy rvs: vals * scale + loc
+    const double x = state + v;
+    return x < 0.0 ? 0.0 : (x > 1.0 ? 1.0 : x);      // np.clip(., 0, 1)
+}
+
+__device__ __forceinline__ double draw_cc(const KParams& kp, Chain& ch, double u)
+{
+    const double state = kp.cc_mode == TMH_CC_MARKOV ? ch.mstate : 1.0;
+    const double x = draw_cc_from(kp, state, u);
+    if (kp.cc_mode == TMH_CC_MARKOV) ch.mstate = x;
+    return x;
+}
+
+__device__ __forceinline__ int32_t ceil_thr(double x)
+{   // sec < x  <=>  sec < ceil(x) for integer sec (cloud_cover_binary.py:111-113)
+    if (!(x <= 2147483000.0)) return INT_MAX;
+    if (x < -2147483000.0) return INT_MIN + 1;
+    return (int32_t)ceil(x);
+}
+
+__device__ __forceinline__ double* sig_c(const StateView& st, uint32_t c) { return st.sc + (size_t)c * CAP; }
+__device__ __forceinline__ double* sig_l(const StateView& st, uint32_t c) { return st.sl + (size_t)c * CAP; }
+
+__device__ void reset_sigma(double* sc, double* sl, Chain& ch, double h)
+{   // cloud_cover_binary.py:76-78: cumsum(300 * ones(int(12 h))) is exact
+    int L = (int)(h * 12);
+    if (L > CAP) L = CAP;
+    const double f = 1.0 / h - 1.0;
+    double acc = 0.0;
+    for (int k = 0; k < L; ++k) {
+        acc += 300.0;
+        sc[k] = acc;
+        sl[k] = f * acc;
+    }
+    ch.L = L;
+}
+
+// cloud_cover_binary.py:80-107, one lane per chain (sequential kernel / init);
+// returns 0 or a fault status
+template <int RNG>
+__device__ uint32_t next_cloud(const KParams& kp, double* sc, double* sl, Chain& ch, const Draw<RNG>& dr, double h,
+                               double ws, uint64_t step, uint32_t tag, uint32_t call)
+{
+    const double f = 1.0 / h - 1.0;
+    int tries = 0;
+    ch.ncalls++;
+    for (int rec = 0; rec < 2; ++rec) {
+        for (int i = 0; i < 20; ++i, ++tries) {
+            const double u = dr.one(ch, step, tag, (call << 8) | (uint32_t)(tries >> 1), tries & 1);
+            const double cl = pow(kp.alpha + kp.delta * u, kp.expo) / ws;
+            int last = -1;
+            double best = 0.0;
+            for (int k = 0; k < ch.L; ++k) {
+                const double nsc = cl + sc[k];
+                const double nsl = f * nsc;
+                const double tot = nsc + nsl;
+                if (nsl - sl[k] > 0.0 && tot < 5400.0) {
+                    const double d = fabs(tot - 3600.0);
+                    if (last < 0 || d < best) {
+                        best = d;
+                        last = k;
+                    }
+                }
+            }
+            if (last >= 0) {
+                if (last + 2 > CAP) return TMH_CHAIN_SIGMA_OVERFLOW;
+                const double clr = f * (cl + sc[last]) - sl[last];
+                for (int k = last; k >= 0; --k) {
+                    const double nsc = cl + sc[k];
+                    sc[k + 1] = nsc;
+                    sl[k + 1] = f * nsc;
+                }
+                sc[0] = cl;
+                sl[0] = clr;
+                ch.L = last + 2;
+                ch.cl = cl;
+                ch.clr = clr;
+                ch.t1 = ceil_thr(cl);
+                ch.t2 = ceil_thr(cl + clr);
+                ch.sec = 0;
+                return 0;
+            }
+        }
+        if (rec == 0) reset_sigma(sc, sl, ch, h);
+    }
+    return TMH_CHAIN_ASSERT_BINARY;
+}
+
+// Small by-value parameter block for the out-of-line / time-parallel paths
+// (avoids taking the address of the large kernel-argument struct).
+struct DrawParams {
+    uint64_t seed;
+    double alpha, delta, expo, sqrt09;
+    double fb_k, fb_scale, fb_loc;   // the bin a fresh generator (state 1.0) draws from
+    int32_t fb_is_t, pad;
+};
+
+// faithful hourly cloud cover: a fresh get_cloud_cover generator (state 1.0) per draw
+__device__ __forceinline__ double cc_faithful(const DrawParams& dp, double u)
+{
+    double v = dp.fb_is_t ? stdtrit(dp.fb_k, u) : al_ppf(u, dp.fb_k);
+    v = v * dp.fb_scale + dp.fb_loc;
+    const double x = 1.0 + v;
+    return x < 0.0 ? 0.0 : (x > 1.0 ? 1.0 : x);
+}
+
+// CloudCoverBinary.next_cloud (cloud_cover_binary.py:80-107) with the 64 lanes
+// of a wavefront cooperating on ONE chain whose sigma arrays live in VGPRs:
+// entry k = chunk * 64 + lane of vc[] / vl[].  The element arithmetic is the
+// reference's (identical bits); np.argmin's first-index tie rule is a butterfly
+// reduction; the r_[cl, nsc[:last+1]] shift is a lane shuffle by one.
+constexpr int NCH = CAP / 64;
+
+// ---- wavefront primitives (DPP, readlane): no LDS round trips
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t old, uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, 0xF, 0xF, false);
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double old, double v)
+{
+    const uint32_t lo = dpp_u32<CTRL>((uint32_t)__double2loint(old), (uint32_t)__double2loint(v));
+    const uint32_t hi = dpp_u32<CTRL>((uint32_t)__double2hiint(old), (uint32_t)__double2hiint(v));
+    return __hiloint2double((int)hi, (int)lo);
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int lane)
+{
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+    return __hiloint2double(hi, lo);
+}
+
+// (d, k) lexicographic min; d >= 0 or +inf, so its bit pattern orders like the value
+__device__ __forceinline__ bool key_less(uint64_t ad, int ak, uint64_t bd, int bk)
+{
+    return ad < bd || (ad == bd && ak < bk);
+}
+
+template <int CTRL>
+__device__ __forceinline__ void argmin_step(uint64_t& d, int& k)
+{
+    const uint32_t ol = dpp_u32<CTRL>((uint32_t)d, (uint32_t)d);
+    const uint32_t oh = dpp_u32<CTRL>((uint32_t)(d >> 32), (uint32_t)(d >> 32));
+    const int ok = (int)dpp_u32<CTRL>((uint32_t)k, (uint32_t)k);
+    const uint64_t od = ((uint64_t)oh << 32) | ol;
+    if (key_less(od, ok, d, k)) {
+        d = od;
+        k = ok;
+    }
+}
+
+// np.argmin semantics over the wave: minimal d, first (lowest) k on ties; result uniform
+__device__ __forceinline__ void argmin_first(double dval, int kval, double& dmin, int& kmin)
+{
+    uint64_t d = (uint64_t)__double_as_longlong(dval);
+    int k = kval;
+    argmin_step<0xB1>(d, k);    // quad_perm [1,0,3,2]
+    argmin_step<0x4E>(d, k);    // quad_perm [2,3,0,1]
+    argmin_step<0x141>(d, k);   // row_half_mirror
+    argmin_step<0x140>(d, k);   // row_mirror: every row of 16 now holds its minimum
+    uint64_t bd = 0;
+    int bk = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)d, 16 * r);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(d >> 32), 16 * r);
+        const int rk = __builtin_amdgcn_readlane(k, 16 * r);
+        const uint64_t rd = ((uint64_t)hi << 32) | lo;
+        if (r == 0 || key_less(rd, rk, bd, bk)) {
+            bd = rd;
+            bk = rk;
+        }
+    }
+    dmin = __longlong_as_double((long long)bd);
+    kmin = bk;
+}
+
+__device__ __forceinline__ uint32_t next_cloud_regs(const DrawParams& dp, double (&vc)[NCH], double (&vl)[NCH],
+                                                    int& L, double h, double ws, uint64_t chain, uint64_t step,
+                                                    uint32_t call, int lane, double& cl_out, double& clr_out)
+{
+    const double f = 1.0 / h - 1.0;
+    int tries = 0;
+    for (int rec = 0; rec < 2; ++rec) {
+        for (int i = 0; i < 20; ++i, ++tries) {
+            const double u = keyed_u(dp.seed, chain, step, TAG_CLOUD, (call << 8) | (uint32_t)(tries >> 1), tries & 1);
+            // out of line on purpose: inlining ocml pow here and capping the
+            // kernel at 128 VGPR (launch_bounds(256, 4)) broke bit-parity on gfx950
+            const double cl = pow_d(dp.alpha + dp.delta * u, dp.expo) / ws;
+            double bd = INFINITY;
+            int bk = INT_MAX;
+#pragma unroll
+            for (int ch = 0; ch < NCH; ++ch) {
+                if (ch * 64 < L) {
+                    const int k = ch * 64 + lane;
+                    if (k < L) {
+                        const double nsc = cl + vc[ch];
+                        const double nsl = f * nsc;
+                        const double tot = nsc + nsl;
+                        if (nsl - vl[ch] > 0.0 && tot < 5400.0) {
+                            const double d = fabs(tot - 3600.0);
+                            if (d < bd) {   // chunks ascend in k: ties keep the lower k
+                                bd = d;
+                                bk = k;
+                            }
+                        }
+                    }
+                }
+            }
+            double dmin;
+            int kmin;
+            argmin_first(bd, bk, dmin, kmin);
+            if (kmin != INT_MAX) {
+                const int last = kmin;
+                if (last + 2 > CAP) return TMH_CHAIN_SIGMA_OVERFLOW;
+                double sc_last = 0.0, sl_last = 0.0;
+#pragma unroll
+                for (int ch = 0; ch < NCH; ++ch)
+                    if (ch == (last >> 6)) {
+                        sc_last = readlane_f64(vc[ch], last & 63);
+                        sl_last = readlane_f64(vl[ch], last & 63);
+                    }
+                const double clr = f * (cl + sc_last) - sl_last;
+                double carry = 0.0;   // old entry 64 ch - 1 (lane 63 of the previous chunk)
+#pragma unroll
+                for (int ch = 0; ch < NCH; ++ch) {
+                    if (ch * 64 <= last + 1) {
+                        const double top = readlane_f64(vc[ch], 63);
+                        const double prev = dpp_f64<0x138>(carry, vc[ch]);   // wave_shr:1, lane 0 <- carry
+                        const int p = ch * 64 + lane;
+                        const double nsc = cl + prev;
+                        vc[ch] = p == 0 ? cl : nsc;
+                        vl[ch] = p == 0 ? clr : f * nsc;
+                        carry = top;
+                    }
+                }
+                L = last + 2;
+                cl_out = cl;
+                clr_out = clr;
+                return 0;
+            }
+        }
+        if (rec == 0) {   // reset_sigma (cloud_cover_binary.py:76-78); 300 (k+1) is exact
+            int nl = (int)(h * 12);
+            if (nl > CAP) nl = CAP;
+#pragma unroll
+            for (int ch = 0; ch < NCH; ++ch) {
+                const int k = ch * 64 + lane;
+                if (k < nl) {
+                    vc[ch] = 300.0 * (k + 1);
+                    vl[ch] = f * vc[ch];
+                }
+            }
+            L = nl;
+        }
+    }
+    return TMH_CHAIN_ASSERT_BINARY;
+}
+
+// ------------------------------------------------------------ clock + geometry
+__device__ __forceinline__ double rad(double d) { return d * (3.14159265358979323846 / 180.0); }
+__device__ __forceinline__ double deg(double r) { return r * (180.0 / 3.14159265358979323846); }
+__device__ __forceinline__ double cosd(double d) { return cos(rad(d)); }
+__device__ __forceinline__ double sind(double d) { return sin(rad(d)); }
+
+__device__ __forceinline__ int64_t local_at(const tmh_clock& ck, int64_t s)
+{
+    int64_t l = ck.local0 + s;
+    for (int i = 0; i < ck.n_shifts && i < 8; ++i)
+        if (s >= ck.shift_step[i]) l += ck.shift_delta[i];
+    return l;
+}
+
+__device__ __forceinline__ int64_t floordiv(int64_t a, int64_t b)
+{
+    int64_t q = a / b;
+    if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
+    return q;
+}
+
+// days since 1970-01-01 -> (year, day of year 1..366, leap)
+__device__ void civil_doy(int64_t z, int& doy, int& leap)
+{
+    z += 719468;
+    const int64_t era = floordiv(z, 146097);
+    const int64_t doe = z - era * 146097;
+    const int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+    int64_t y = yoe + era * 400;
+    const int64_t doyy = doe - (365 * yoe + yoe / 4 - yoe / 100);   // from March 1
+    const int64_t mp = (5 * doyy + 2) / 153;
+    const int64_t d = doyy - (153 * mp + 2) / 5 + 1;
+    const int64_t m = mp < 10 ? mp + 3 : mp - 9;
+    if (m <= 2) ++y;
+    leap = ((y % 4 == 0) && (y % 100 != 0)) || (y % 400 == 0);
+    static const int cum[12] = {0, 31, 59, 90, 120, 151, 181, 212, 243, 273, 304, 334};
+    doy = cum[m - 1] + (int)d + ((leap && m > 2) ? 1 : 0);
+}
+
+__device__ void solpos(int64_t utc, double lat, double lon, double pressure_pa, double temp_c, double& zen,
+                       double& azen, double& az)
+{   // NOAA / Meeus low-precision sun + SPA refraction (same restatement as the oracle)
+    const double jd = (double)utc / 86400.0 + 2440587.5;
+    const double T = (jd - 2451545.0) / 36525.0;
+    const double L0 = fmod(280.46646 + T * (36000.76983 + T * 0.0003032), 360.0);
+    const double M = 357.52911 + T * (35999.05029 - 0.0001537 * T);
+    const double e = 0.016708634 - T * (0.000042037 + 0.0000001267 * T);
+    const double Mr = rad(M);
+    const double C = sin(Mr) * (1.914602 - T * (0.004817 + 0.000014 * T)) +
+                     sin(2.0 * Mr) * (0.019993 - 0.000101 * T) + sin(3.0 * Mr) * 0.000289;
+    const double omega = 125.04 - 1934.136 * T;
+    const double lam = L0 + C - 0.00569 - 0.00478 * sin(rad(omega));
+    const double eps0 = 23.0 + (26.0 + (21.448 - T * (46.815 + T * (0.00059 - T * 0.001813))) / 60.0) / 60.0;
+    const double eps = eps0 + 0.00256 * cos(rad(omega));
+    const double decl = asin(sin(rad(eps)) * sin(rad(lam)));
+    double y = tan(rad(eps) / 2.0);
+    y *= y;
+    const double L0r = rad(L0);
+    const double eot = 4.0 * deg(y * sin(2.0 * L0r) - 2.0 * e * sin(Mr) + 4.0 * e * y * sin(Mr) * cos(2.0 * L0r) -
+                                 0.5 * y * y * sin(4.0 * L0r) - 1.25 * e * e * sin(2.0 * Mr));
+    int64_t sod = utc % 86400;
+    if (sod < 0) sod += 86400;
+    double tst = fmod((double)sod / 60.0 + eot + 4.0 * lon, 1440.0);
+    if (tst < 0) tst += 1440.0;
+    const double ha = rad(tst / 4.0 - 180.0);
+    const double latr = rad(lat);
+    double cz = sin(latr) * sin(decl) + cos(latr) * cos(decl) * cos(ha);
+    cz = cz > 1.0 ? 1.0 : (cz < -1.0 ? -1.0 : cz);
+    zen = deg(acos(cz));
+    az = deg(atan2(sin(ha), cos(ha) * sin(latr) - tan(decl) * cos(latr))) + 180.0;
+    const double e0 = 90.0 - zen;
+    double de = 0.0;
+    if (e0 >= -1.0 * (0.26667 + 0.5667))
+        de = (pressure_pa / 100.0 / 1010.0) * (283.0 / (273.0 + temp_c)) * 1.02 /
+             (60.0 * tan(rad(e0 + 10.3 / (e0 + 5.11))));
+    azen = 90.0 - (e0 + de);
+}
+
+__device__ __forceinline__ double extra_rad(int doy, double s0)
+{
+    const double B = (2.0 * 3.14159265358979323846 / 365.0) * (doy - 1);
+    return s0 * (1.00011 + 0.034221 * cos(B) + 0.00128 * sin(B) + 0.000719 * cos(2.0 * B) + 7.7e-05 * sin(2.0 * B));
+}
+
+__device__ double linke_at(const double* lts, int doy, int leap)
+{
+    const int md[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+    double x0 = -31.0 / 2.0, y0 = lts[11], cum = 0.0;
+    for (int m = 0; m < 13; ++m) {
+        double x1, y1;
+        if (m < 12) {
+            const double d = md[m] + (leap && m == 1 ? 1 : 0);
+            cum += d;
+            x1 = cum - d / 2.0;
+            y1 = lts[m];
+        } else {
+            x1 = (leap ? 366 : 365) + 28 / 2.0;
+            y1 = lts[0];
+        }
+        if ((double)doy <= x1) return y0 + ((double)doy - x0) * (y1 - y0) / (x1 - x0);
+        x0 = x1;
+        y0 = y1;
+    }
+    return lts[0];
+}
+
+
+// ------------------------------------------------------------ PV (per chain-second)
+// pvmodel.py:53-80 on the precomputed geometry row; R = float | double.
+template <typename R>
+__device__ __forceinline__ R pv_power(const KParams& kp, const R* g, R csi)
+{
+    const double* m = kp.module;
+    const double* iv = kp.inverter;
+    R c = csi > g[G_CSIMAX] ? g[G_CSIMAX] : csi;
+    const R ghi = c * g[G_GHICS];
+    R kt;
+    if constexpr (sizeof(R) == 8) kt = ghi / g[G_I0H];
+    else kt = ghi * g[G_I0H];
+    kt = kt > R(0) ? kt : R(0);
+    kt = kt < R(1) ? kt : R(1);
+    const R am = g[G_AM], kt2 = kt * kt, kt3 = kt2 * kt;
+    R a, b, cc;
+    if (kt <= R(0.6)) {
+        a = R(0.512) - R(1.56) * kt + R(2.286) * kt2 - R(2.222) * kt3;
+        b = R(0.37) + R(0.962) * kt;
+        cc = R(-0.28) + R(0.932) * kt - R(2.048) * kt2;
+    } else {
+        a = R(-5.743) + R(21.77) * kt - R(27.49) * kt2 + R(11.56) * kt3;
+        b = R(41.4) - R(118.5) * kt + R(66.05) * kt2 + R(31.9) * kt3;
+        cc = R(-47.01) + R(184.2) * kt - R(222.0) * kt2 + R(73.81) * kt3;
+    }
+    const R dkn = a + b * exp(cc * am);
+    R dni = (g[G_KNC] - dkn) * g[G_I0];
+    if (g[G_DISCOK] == R(0) || ghi < R(0) || dni < R(0)) dni = R(0);
+    const R dhi = ghi - dni * g[G_COSZ];
+    R AI;
+    if constexpr (sizeof(R) == 8) AI = dni / g[G_DNIEXTRA];
+    else AI = dni * g[G_DNIEXTRA];
+    R sky = dhi * (AI * g[G_RB] + (R(1) - AI) * g[G_TERM2]);
+    sky = sky > R(0) ? sky : R(0);
+    const R ground = ghi * g[G_GFAC];
+    R poa_direct = dni * g[G_COSAOI];
+    poa_direct = poa_direct > R(0) ? poa_direct : R(0);
+    const R poa_diffuse = sky + ground;
+    const R poa_global = poa_direct + poa_diffuse;
+    // sapm_celltemp (pvmodel.py:69-70), open_rack_cell_glassback
+    const R tmod = poa_global * exp(R(m[TMH_MOD_TEMP_A]) + R(m[TMH_MOD_TEMP_B]) * R(kp.wind)) + R(kp.temp_air);
+    const R tcell = tmod + (poa_global / R(1000)) * R(m[TMH_MOD_TEMP_DT]);
+    // sapm_effective_irradiance, suns (pvmodel.py:74-76)
+    const R Ee = g[G_F1] * (poa_direct * g[G_F2] + R(m[TMH_MOD_FD]) * poa_diffuse) / R(1000);
+    // sapm (pvmodel.py:77)
+    const R q = R(1.60218e-19), kb = R(1.38066e-23);
+    const R Bvmpo = R(m[TMH_MOD_BVMPO]) + R(m[TMH_MOD_MBVMP]) * (R(1) - Ee);
+    R delta;
+    if constexpr (sizeof(R) == 8) delta = R(m[TMH_MOD_N]) * kb * (tcell + R(273.15)) / q;
+    else delta = R(m[TMH_MOD_N] * (1.38066e-23 / 1.60218e-19)) * (tcell + R(273.15));   // fp32: no 1e-23 subnormals
+    const R logEe = Ee > R(0) ? log(Ee) : (Ee == R(0) ? -R(INFINITY) : R(NAN));
+    const R imp = R(m[TMH_MOD_IMPO]) * (R(m[TMH_MOD_C0]) * Ee + R(m[TMH_MOD_C1]) * (Ee * Ee)) *
+                  (R(1) + R(m[TMH_MOD_AIMP]) * (tcell - R(25)));
+    const R dl = delta * logEe;
+    R vmp = R(m[TMH_MOD_VMPO]) + R(m[TMH_MOD_C2]) * R(m[TMH_MOD_NS]) * delta * logEe +
+            R(m[TMH_MOD_C3]) * R(m[TMH_MOD_NS]) * (dl * dl) + Bvmpo * (tcell - R(25));
+    if (!isnan(vmp)) vmp = vmp > R(0) ? vmp : R(0);
+    const R pdc = imp * vmp;
+    // snlinverter (pvmodel.py:78)
+    const R dv = vmp - R(iv[2]);
+    const R A = R(iv[1]) * (R(1) + R(iv[5]) * dv);
+    const R B = R(iv[3]) * (R(1) + R(iv[6]) * dv);
+    const R C = R(iv[4]) * (R(1) + R(iv[7]) * dv);
+    R ac = (R(iv[0]) / (A - B) - C * (A - B)) * (pdc - B) + C * ((pdc - B) * (pdc - B));
+    if (!isnan(ac)) ac = R(iv[0]) < ac ? R(iv[0]) : ac;
+    if (pdc < R(iv[3])) ac = R(-1) * fabs(R(iv[8]));
+    if (isnan(ac)) return R(0);                       // .fillna(0.)
+    return ac > R(0) ? ac : R(0);                      // .clip(lower=0.)
+}
+
+
+// ------------------------------------------------------------ fused per-second body
+template <typename R>
+struct FSamp {
+    R b[6], a[6];
+};
+
+template <typename R>
+__device__ __forceinline__ void to_real(FSamp<R>& f, const Samp& s)
+{
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        f.b[k] = (R)s.b[k];
+        f.a[k] = (R)s.a[k];
+    }
+}
+
+template <typename R>
+__device__ __forceinline__ R rinterp(const FSamp<R>& f, int k, R frac)
+{
+    return frac * f.a[k] + (R(1) - frac) * f.b[k];
+}
+
+// clearskyindexmodel.py:146-160 + pvmodel.py:53-80 + metersim.py:51 + pvsim.py:83
+template <typename R>
+__device__ __forceinline__ void second_body(const KParams& kp, const R* row, uint32_t fl, const FSamp<R>& fs,
+                                            bool covered, double ue, double um, R& csi, R& pv, R& meter, R& res)
+{
+    const R cloudcover = rinterp(fs, S_CC, row[G_HOURF]);   // == interp() bit for bit when R = double
+    R z;
+    if constexpr (sizeof(R) == 8) z = ndtri(ue);
+    else z = ndtri_f(ue);
+    const R eps = z * (R(kp.sqrt6) * (R(0.001) + R(0.0015 * 8) * cloudcover)) + R(0);
+    if (covered)
+        csi = rinterp(fs, S_CLEAR_DAY, row[G_DAYF]) * (rinterp(fs, S_CLEAR_NOISE, row[G_MINF]) + eps);
+    else
+        csi = rinterp(fs, S_CLOUDY_HOUR, row[G_HOURF]) * (rinterp(fs, S_CLOUDY_NOISE, row[G_MINF]) + eps);
+    pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power<R>(kp, row, csi) : R(0);
+    if constexpr (sizeof(R) == 8) meter = 9000 * um;
+    else meter = fminf((float)(9000 * um), 8999.9990234375f);   // largest float < 9000: keep [0, 9000)
+    res = meter - pv;
+}
+
+template <typename R>
+__device__ __forceinline__ void trace_store(void* p, uint64_t i, R v)
+{
+    if (p) reinterpret_cast<R*>(p)[i] = v;
+}
+
+struct Acc {
+    double pv, m, r, mx;
+};
+
+template <typename R>
+__device__ __forceinline__ void emit(const TraceView& tr, const StatsView& sv, uint32_t* lds_hist, uint64_t o,
+                                     uint8_t cov, R csi, R pv, R meter, R res, Acc& acc, bool ok)
+{
+    trace_store<R>(tr.csi, o, csi);
+    trace_store<R>(tr.pv, o, pv);
+    trace_store<R>(tr.meter, o, meter);
+    trace_store<R>(tr.residual, o, res);
+    if (tr.covered) tr.covered[o] = cov;
+    if (ok) {
+        if (sv.acc) {
+            acc.pv += (double)pv;
+            acc.m += (double)meter;
+            acc.r += (double)res;
+            acc.mx = fmax(acc.mx, (double)res);
+        }
+        if (sv.hist) {
+            const double x = ((double)res - sv.lo) * sv.scale;
+            const int bin = x < 0.0 ? 0 : (x >= (double)(sv.n_bins - 1) ? (int)sv.n_bins - 1 : (int)x);
+            atomicAdd(&lds_hist[bin], 1u);
+        }
+    }
+}
+
+}  // namespace tmh

@@ -45,7 +45,7 @@ class BatchedSim:
     """
 
     def __init__(self, n_chains, start, tz=None, params: ModelParams | None = None, precision="fp32",
-                 chain0=0, device=None, injected=None, horizon=400 * 86400):
+                 chain0=0, device=None, injected=None, horizon=400 * 86400, kernel_path="auto"):
         torch = _torch()
         L = _lib.load()
         self.L = L
@@ -59,11 +59,14 @@ class BatchedSim:
             raise ValueError("BatchedSim runs on a GPU device (there is no CPU path)")
         self.horizon = int(horizon)
         self.clock = make_clock(start, self.horizon, tz)
-        P = _lib.make_params(self.params, self.precision)
+        kp = {"auto": _lib.PATH_AUTO, "sequential": _lib.PATH_SEQUENTIAL,
+              "time_parallel": _lib.PATH_TIME_PARALLEL}[kernel_path]
+        P = _lib.make_params(self.params, self.precision, kp)
         ck = self.clock.as_struct()
         eng = C.c_void_p()
         _lib.check(L.tmh_engine_create(C.byref(P), C.byref(ck), self.device.index or 0, C.byref(eng)))
         self._eng = eng
+        self.path = {1: "sequential", 2: "time_parallel"}[L.tmh_engine_path(eng)]
         self.state = torch.zeros(L.tmh_state_bytes(self.n), dtype=torch.uint8, device=self.device)
         self._offsets = _lib.state_offsets(self.n)
         self.injected = None
@@ -97,7 +100,7 @@ class BatchedSim:
 
     # ------------------------------------------------------------------ state
     def state_field(self, name):
-        """Device view of one SoA state field ([n] or [TMH_SIGMA_CAP, n])."""
+        """Device view of one SoA state field ([n], or [n, TMH_SIGMA_CAP] for the sigma arrays)."""
         torch = _torch()
         i = _lib.STATE_FIELDS.index(name)
         dt = {np.float64: torch.float64, np.int32: torch.int32, np.uint32: torch.int32}[_lib.STATE_DTYPES[name]]
@@ -105,7 +108,7 @@ class BatchedSim:
         rows = _lib.TMH_SIGMA_CAP if name.startswith("sigma_c") else 1
         o = int(self._offsets[i])
         v = self.state[o:o + esz * self.n * rows].view(dt)
-        return v.view(rows, self.n) if rows > 1 else v
+        return v.view(self.n, rows) if rows > 1 else v
 
     def status(self):
         return self.state_field("status").cpu().numpy().astype(np.uint32)
@@ -127,7 +130,7 @@ class BatchedSim:
 
     # ------------------------------------------------------------------ run
     def workspace(self, n_steps):
-        return _torch().empty(self.L.tmh_workspace_bytes(n_steps), dtype=torch_uint8(), device=self.device)
+        return _torch().empty(self.L.tmh_workspace_bytes(self.n, n_steps), dtype=torch_uint8(), device=self.device)
 
     def run(self, n_steps, trace=TRACE_FIELDS, window=86400, out=None):
         """Advance n_steps seconds.  Returns {field: tensor[n_steps, n_chains]} for `trace`."""
@@ -161,12 +164,19 @@ class BatchedSim:
         self.step += n_steps
         return res
 
-    def geometry(self, step0, n_steps):
+    def plan(self, step0, n_steps):
+        """Build the chain-independent plan of a window (tmh_plan); returns the uint8 buffer."""
         torch = _torch()
-        ws = self.workspace(n_steps)
+        plan = torch.empty(self.L.tmh_plan_bytes(int(n_steps)), dtype=torch.uint8, device=self.device)
         with torch.cuda.device(self.device):
-            _lib.check(self.L.tmh_geometry(self._eng, int(step0), int(n_steps), _ptr(ws), self._stream()))
-        return ws[: n_steps * _lib.TMH_GEOM_FIELDS * 8].view(torch.float64).view(n_steps, _lib.TMH_GEOM_FIELDS)
+            _lib.check(self.L.tmh_plan(self._eng, int(step0), int(n_steps), _ptr(plan), self._stream()))
+        return plan
+
+    def geometry(self, step0, n_steps):
+        """The clock/geometry table rows [n_steps, TMH_GEOM_FIELDS] (fp64) of a window."""
+        torch = _torch()
+        plan = self.plan(step0, n_steps)
+        return plan[: n_steps * _lib.TMH_GEOM_FIELDS * 8].view(torch.float64).view(n_steps, _lib.TMH_GEOM_FIELDS)
 
     def stats_totals(self):
         """Node-local totals: histogram, energy sums (W*s) and peak residual (W)."""
