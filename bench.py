@@ -85,16 +85,20 @@ def main():
     from tmhpvsim_amd.engine import BatchedSim
     from tmhpvsim_amd.params import ModelParams
 
+    from tmhpvsim_amd.dist import all_reduce_stats
+
+    totals = [None]
     L = _lib.load()
     n, secs = args.chains, args.seconds
     sim = BatchedSim(n, args.start, tz="Europe/Berlin", params=ModelParams(), precision=args.precision,
                      chain0=rank * n, device=dev, horizon=secs, kernel_path=args.path)
     real = sim.real
-    trace = {f: torch.empty(secs, n, dtype=real, device=dev) for f in ("pv", "meter", "residual")}
+    trace = {f: torch.empty(secs, n, dtype=real, device=dev) for f in ("pv", "meter", "residual")} \
+        if args.mode == "trace" else {}
     if args.mode == "stats":
         sim.enable_stats()
     st = sim._stats_struct()
-    tr = _lib.Trace(None, None, *(trace[f].data_ptr() if args.mode == "trace" else None
+    tr = _lib.Trace(None, None, *(trace[f].data_ptr() if f in trace else None
                                   for f in ("pv", "meter", "residual")), n)
     plan = torch.empty(L.tmh_plan_bytes(secs), dtype=torch.uint8, device=dev)
     scratch = torch.empty(L.tmh_scratch_bytes(n, secs), dtype=torch.uint8, device=dev)
@@ -112,6 +116,8 @@ def main():
                               C.byref(tr), C.byref(st) if st is not None else None,
                               C.c_void_p(plan.data_ptr()), C.c_void_p(scratch.data_ptr()), scratch.numel(), sptr))
         ev[k][1].record(stream)
+        if args.mode == "stats":                           # the one exchange step: RCCL all-reduce
+            totals[0] = all_reduce_stats(sim.stats_totals())
 
     for k in range(args.warmup):
         one_step(k)
@@ -146,10 +152,13 @@ def main():
         "config": {"workload": f"C2: {n} chains/GPU x {secs} s at 1 s, Munich, Europe/Berlin, "
                                f"{args.start[:10]}, {args.mode} mode ({'meter+pv+residual fp32 trace' if args.mode == 'trace' else 'on-GPU stats'})",
                    "chains_per_gpu": n, "seconds": secs, "parallelism": f"chains sharded over {world} GPU(s)"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "tmh_step (" + sim.path + ")", "kernel_ms": kmean,
-                     "bytes_per_launch": TRACE_BYTES * n * secs},
+        "roofline": ({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                      "kernel": "tmh_step (" + sim.path + ")", "kernel_ms": kmean,
+                      "bytes_per_launch": TRACE_BYTES * n * secs} if args.mode == "trace" else
+                     {"bound": "valu", "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
+                      "kernel": "tmh_step (" + sim.path + ")", "kernel_ms": kmean,
+                      "note": "stats mode stores no trace; VALU counters under profiles/"}),
         "faulted_chains": bad,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
