@@ -41,6 +41,13 @@ void orc_L_hist(uint64_t* out, int reset)
     memcpy(out, g_Lhist, sizeof g_Lhist);
     if (reset) memset(g_Lhist, 0, sizeof g_Lhist);
 }
+/* diagnostics: histogram of tries per successful next_cloud call (index = tries, 0..40) */
+static uint64_t g_Thist[41];
+void orc_T_hist(uint64_t* out, int reset)
+{
+    memcpy(out, g_Thist, sizeof g_Thist);
+    if (reset) memset(g_Thist, 0, sizeof g_Thist);
+}
 
 enum { ST_OK = 0, ST_NAMEERROR_INIT = 1, ST_ASSERT_BINARY = 2, ST_SIGMA_OVERFLOW = 3,
        ST_U_EXHAUSTED = 4 };
@@ -290,6 +297,7 @@ typedef struct {
     int L;
     double sc[ORC_SIGMA_CAP], sl[ORC_SIGMA_CAP];
     double mstate;                /* markov-mode persistent hourly state */
+    uint64_t ncalls;              /* next_cloud calls so far (keyed counter of CLOUD draws) */
     int status;
     /* rng */
     uint64_t chain;
@@ -353,13 +361,15 @@ static void reset_sigma(chain_t* ch)                        /* cloud_cover_binar
 }
 
 /* cloud_cover_binary.py:80-107.  Returns 0 or a fault status. */
-static int next_cloud(const ctx_t* X, chain_t* ch, uint64_t step, uint32_t tag, uint32_t call)
+static int next_cloud(const ctx_t* X, chain_t* ch, uint32_t tag)
 {
     double nsc[ORC_SIGMA_CAP], nsl[ORC_SIGMA_CAP];
     int tries = 0;
+    /* keyed counter: the chain's next_cloud call number (0 = constructor's call) */
+    const uint64_t ctr = ch->ncalls++;
     for (int rec = 0; rec < 2; ++rec) {
         for (int i = 0; i < 20; ++i, ++tries) {
-            double u = draw_u(X, ch, step, tag, (call << 8) | (uint32_t)(tries >> 1), tries & 1);
+            double u = draw_u(X, ch, ctr, tag, (uint32_t)(tries >> 1), tries & 1);
             double cl = pow(X->alpha + X->delta * u, X->expo) / ch->ws;
             double f = 1.0 / ch->h - 1.0;
             int last = -1;
@@ -382,6 +392,8 @@ static int next_cloud(const ctx_t* X, chain_t* ch, uint64_t step, uint32_t tag, 
                 ch->L = last + 2;
 #pragma omp atomic
                 g_Lhist[ch->L] += 1;
+#pragma omp atomic
+                g_Thist[tries + 1] += 1;
                 ch->cl = cl;
                 ch->clr = clr;
                 ch->sec = 0;
@@ -432,7 +444,7 @@ static void chain_init(const ctx_t* X, chain_t* ch, const fields_t* t0)
     ch->h = 0.95 < h0 ? 0.95 : h0;
     ch->ws = w0;
     reset_sigma(ch);
-    int st = next_cloud(X, ch, 0, TAG_INIT_CLOUD, 0);
+    int st = next_cloud(X, ch, TAG_INIT_CLOUD);
     if (st) { ch->status = st; return; }
     double u = draw_u(X, ch, 0, TAG_INIT_SEC, 0, 0);
     ch->sec = (int64_t)((ch->cl + ch->clr) * u);           /* :68, int() truncates */
@@ -739,11 +751,10 @@ int orc_run(const orc_params* P, uint64_t chain0, uint32_t n_chains, uint32_t n_
                 ch->h = 0.95 < hh ? 0.95 : hh;                 /* update_parameters */
                 ch->ws = interp(ch->s[S_WS], df);
                 ch->sec += 1;                                  /* CloudCoverBinary.__next__ */
-                uint32_t call = 0;
                 for (;;) {
                     if ((double)ch->sec < ch->cl) { cov = 1; break; }
                     if ((double)ch->sec < ch->cl + ch->clr) { cov = 0; break; }
-                    int st = next_cloud(&X, ch, step, TAG_CLOUD, call++);
+                    int st = next_cloud(&X, ch, TAG_CLOUD);
                     if (st) { ch->status = st; break; }
                     ch->sec += 1;
                 }
@@ -783,4 +794,28 @@ void orc_constants(double* out4)
     out4[1] = pow(0.1e3, omb) - out4[0];
     out4[2] = 1.0 / omb;
     out4[3] = sqrt(0.1 * 60);
+}
+
+/* The device computes the wall-clock fractions (clearskyindexmodel.py:114-116)
+ * as q = x * (1/d) plus one FMA residual correction instead of an IEEE division.
+ * Returns the number of the 86,400 seconds of a day for which that differs from
+ * the divisions the reference performs (expected 0). */
+int orc_check_fractions(void)
+{
+    int bad = 0;
+    for (int h = 0; h < 24; ++h)
+        for (int m = 0; m < 60; ++m)
+            for (int s = 0; s < 60; ++s) {
+                double mf = s / 60.0, hf = (m + mf) / 60.0, df = (h + hf) / 24.0;
+                double q = s * (1.0 / 60.0);
+                double mf2 = fma(fma(-q, 60.0, (double)s), 1.0 / 60.0, q);
+                double x = m + mf2;
+                q = x * (1.0 / 60.0);
+                double hf2 = fma(fma(-q, 60.0, x), 1.0 / 60.0, q);
+                x = h + hf2;
+                q = x * (1.0 / 24.0);
+                double df2 = fma(fma(-q, 24.0, x), 1.0 / 24.0, q);
+                bad += (mf2 != mf) + (hf2 != hf) + (df2 != df);
+            }
+    return bad;
 }

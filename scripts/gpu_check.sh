@@ -12,7 +12,7 @@ python -c "import __graft_entry__ as g; g.build()" > "$OUT/build.log" 2>&1 || { 
 timeout -k 10 400 python __graft_entry__.py smoke > "$OUT/smoke.log" 2>&1; rc=$?
 echo "smoke rc=$rc"; tail -3 "$OUT/smoke.log"
 [ $rc -le 1 ] || exit $rc
-timeout -k 10 700 python -m pytest tests -m gpu -q -p no:cacheprovider -rf > "$OUT/pytest_gpu.log" 2>&1; rc=$?
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider -rf --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -15 "$OUT/pytest_gpu.log"
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 600 python bench.py --steps 3 --warmup 1 > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err"; rc=$?

@@ -87,3 +87,13 @@ def test_standalone_markov_chain():
         # plus the discrete bin sequence exactly.
         np.testing.assert_allclose(out, ref, rtol=0, atol=5e-11)
         np.testing.assert_array_equal(np.searchsorted(edges, out), np.searchsorted(edges, ref))
+
+
+def test_fast_clock_fractions_are_exact():
+    """The device's division-free wall-clock fractions equal the reference's
+    IEEE divisions (clearskyindexmodel.py:114-116) for all 86,400 seconds."""
+    import ctypes as C
+    from oracle import oracle as O
+    f = O.lib().orc_check_fractions
+    f.restype = C.c_int
+    assert f() == 0

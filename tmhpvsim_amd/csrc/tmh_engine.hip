@@ -167,7 +167,7 @@ __global__ __launch_bounds__(256) void init_kernel(KParams kp, StateView st, uin
     double* sc = sig_c(st, c);
     double* sl = sig_l(st, c);
     reset_sigma(sc, sl, ch, h);
-    const uint32_t f = next_cloud<RNG>(kp, sc, sl, ch, dr, h, ws, 0, TAG_INIT_CLOUD, 0);
+    const uint32_t f = next_cloud<RNG>(kp, sc, sl, ch, dr, h, ws, TAG_INIT_CLOUD);
     if (!f) {
         const double us = dr.one(ch, 0, TAG_INIT_SEC, 0, 0);
         ch.sec = (int32_t)((ch.cl + ch.clr) * us);   // cloud_cover_binary.py:68
@@ -191,9 +191,7 @@ __global__ __launch_bounds__(256) void geom_kernel(GParams gp, int64_t step0, ui
     const int hourp = (int)(sodp / 3600), minutep = (int)((sodp / 60) % 60);
     double g[ROW];
     for (int i = 0; i < ROW; ++i) g[i] = 0.0;
-    g[G_MINF] = second / 60.0;   // clearskyindexmodel.py:114-116
-    g[G_HOURF] = (minute + g[G_MINF]) / 60.0;
-    g[G_DAYF] = (hour + g[G_HOURF]) / 24.0;
+    clock_fractions(hour, minute, second, g[G_MINF], g[G_HOURF], g[G_DAYF]);   // clearskyindexmodel.py:114-116
     uint32_t fl = 0;
     if (dn != dp) fl |= FL_DAY;           // :121 prev.day != day
     if (hour != hourp) fl |= FL_HOUR;     // :123
@@ -514,12 +512,11 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
                 to_real(fs, ch.s);
             }
             ch.sec += 1;                                 // CloudCoverBinary.__next__
-            uint32_t call = 0;
             while (ch.sec >= ch.t2 && ch.status == 0) {  // segment over: next_cloud(); next(self)
                 const double hh = interp(ch.s.b[S_CC], ch.s.a[S_CC], r64[G_HOURF]);
                 const double h = 0.95 < hh ? 0.95 : hh;  // update_parameters
                 const double ws = interp(ch.s.b[S_WS], ch.s.a[S_WS], r64[G_DAYF]);
-                const uint32_t f = next_cloud<RNG>(kp, sc, sl, ch, dr, h, ws, step, TAG_CLOUD, call++);
+                const uint32_t f = next_cloud<RNG>(kp, sc, sl, ch, dr, h, ws, TAG_CLOUD);
                 if (f) ch.status = f;
                 else ch.sec += 1;
             }
@@ -592,9 +589,8 @@ __device__ __forceinline__ void fractions_at(const WinClock& w, int32_t j, doubl
     sod %= 86400;
     if (sod < 0) sod += 86400;
     const int hour = sod / 3600, minute = (sod / 60) % 60, second = sod % 60;
-    const double min_f = second / 60.0;
-    hour_f = (minute + min_f) / 60.0;
-    day_f = (hour + hour_f) / 24.0;
+    double min_f;
+    clock_fractions(hour, minute, second, min_f, hour_f, day_f);
 }
 
 __global__ __launch_bounds__(256) void segments_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
@@ -616,8 +612,8 @@ __global__ __launch_bounds__(256) void segments_kernel(DrawParams dp, StateView 
         int L = st.L[c];
         const int32_t sec = st.sec[c];
         double vc[NCH], vl[NCH];
-        const double* gsc = sig_c(st, c);
-        const double* gsl = sig_l(st, c);
+        double* gsc = sig_c(st, c);
+        double* gsl = sig_l(st, c);
 #pragma unroll
         for (int ch = 0; ch < NCH; ++ch) {
             const int k = ch * 64 + lane;
@@ -632,24 +628,41 @@ __global__ __launch_bounds__(256) void segments_kernel(DrawParams dp, StateView 
         nrec = 1;
         const uint32_t nev = min(*n_events, ev_cap_dev(nsteps));
         uint32_t ev = 0;
-        int64_t next_ev = nev > 0 ? events[0].x : INT64_MAX;
-        int64_t prev_call = INT64_MIN;
-        uint32_t call = 0;
-        auto apply_events = [&](int64_t upto) {   // _next_day / _next_hour at steps <= upto
-            while (next_ev <= upto) {
-                const int fl = events[ev].y;
-                if (fl & FL_DAY) {
-                    wsb = wsa;
-                    wsa = sg.evd[((size_t)ev * 4 + 1) * n + c];
-                }
-                if (fl & FL_HOUR) {
-                    ccb = cca;
-                    cca = sg.evd[(size_t)ev * 4 * n + c];
-                }
-                ++ev;
-                next_ev = ev < nev ? events[ev].x : INT64_MAX;
+        // the next boundary event and its draws, loaded one event ahead of use
+        int64_t next_ev = INT64_MAX;
+        int ev_fl = 0;
+        double ev_cc = 0.0, ev_ws = 0.0;
+        auto fetch_event = [&]() {
+            if (ev < nev) {
+                const int2 r = events[ev];
+                next_ev = r.x;
+                ev_fl = r.y;
+                ev_cc = sg.evd[(size_t)ev * 4 * n + c];
+                ev_ws = sg.evd[((size_t)ev * 4 + 1) * n + c];
+            } else {
+                next_ev = INT64_MAX;
             }
         };
+        fetch_event();
+        auto apply_events = [&](int64_t upto) {   // _next_day / _next_hour at steps <= upto
+            while (next_ev <= upto) {
+                if (ev_fl & FL_DAY) {
+                    wsb = wsa;
+                    wsa = ev_ws;
+                }
+                if (ev_fl & FL_HOUR) {
+                    ccb = cca;
+                    cca = ev_cc;
+                }
+                ++ev;
+                fetch_event();
+            }
+        };
+        // try-0 candidates of the next 64 calls (keyed by call number, so they
+        // can be drawn before the calls' steps are known)
+        uint32_t ncall = st.ncalls[c], kb = ncall;
+        double cand_x, cand_u;
+        cloud_candidates(dp, chain, kb, lane, cand_x, cand_u);
         const WinClock wck = win_clock(ck, W0);
         while (e < W1) {
             apply_events(e);
@@ -658,10 +671,18 @@ __global__ __launch_bounds__(256) void segments_kernel(DrawParams dp, StateView 
             const double hh = interp(ccb, cca, hf);
             const double h = 0.95 < hh ? 0.95 : hh;   // update_parameters
             const double ws = interp(wsb, wsa, df);
-            call = e == prev_call ? call + 1 : 0;
-            prev_call = e;
-            double ncl = 0.0, nclr = 0.0;
-            const uint32_t f = next_cloud_regs(dp, vc, vl, L, h, ws, chain, (uint64_t)e, call, lane, ncl, nclr);
+            if (ncall - kb >= 64u) {
+                kb = ncall;
+                cloud_candidates(dp, chain, kb, lane, cand_x, cand_u);
+            }
+            const int slot = (int)(ncall - kb);
+            const double x0 = readlane_f64(cand_x, slot);
+            double ncl = x0 / ws, nclr = 0.0;
+            uint32_t f = 0;
+            if (!next_cloud_fast(vc, vl, L, ncl, 1.0 / h - 1.0, lane, nclr))
+                f = next_cloud_regs(dp, vc, vl, gsc, gsl, L, h, ws, chain, ncall, x0, readlane_f64(cand_u, slot), lane,
+                                    ncl, nclr);
+            ++ncall;
             if (f) {
                 status = f;
                 fault = (int32_t)(e - W0);
@@ -682,14 +703,12 @@ __global__ __launch_bounds__(256) void segments_kernel(DrawParams dp, StateView 
             ++nrec;
         }
         if (status == 0) apply_events(W1 - 1);   // remaining boundaries of the window
-        double* wsc = sig_c(st, c);
-        double* wsl = sig_l(st, c);
 #pragma unroll
-        for (int ch = 0; ch < NCH; ++ch) {
+        for (int ch = 0; ch < NCH; ++ch) {   // register chunks back to the state row
             const int k = ch * 64 + lane;
             if (k < L) {
-                wsc[k] = vc[ch];
-                wsl[k] = vl[ch];
+                gsc[k] = vc[ch];
+                gsl[k] = vl[ch];
             }
         }
         if (lane == 0) {
@@ -697,7 +716,7 @@ __global__ __launch_bounds__(256) void segments_kernel(DrawParams dp, StateView 
             st.cl[c] = cl;
             st.clr[c] = clr;
             st.L[c] = L;
-            st.ncalls[c] += nrec - 1;
+            st.ncalls[c] = ncall;
         }
     }
     if (lane == 0) {
@@ -802,11 +821,20 @@ __global__ __launch_bounds__(256) void expand_kernel(KParams kp, StateView st, u
             while (step >= (int64_t)seg.y) seg = rec[++jr];   // next_cloud happened at seg.y
             const bool covered = step < (int64_t)seg.x;
             cov = covered ? 1 : 0;
+#ifdef TMH_DIAG_NO_RNG   // diagnostic builds only (scripts/diag_variants.sh): cost breakdown
+            const uint32_t hsh = (uint32_t)chain * 0x9E3779B9u ^ (uint32_t)step * 0x85EBCA6Bu;
+            const U4 u{hsh, hsh >> 3, hsh ^ 0x5555u, hsh >> 5};
+#else
             const U4 u = keyed_block(kp.seed, chain, (uint64_t)step, TAG_STEP, 0);
+#endif
             second_body<R>(kp, row, fl, fs, covered, u52(u.x, u.y), u52(u.z, u.w), csi, pv, meter, res);
         }
         if (fl & (FL_DAY | FL_HOUR)) ++evi;
+#ifdef TMH_DIAG_NO_STORE
+        if (live && csi == R(-12345)) emit<R>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok);
+#else
         if (live) emit<R>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok);
+#endif
     }
     if (live && sv.acc) {
         const size_t o = (size_t)b * n + c, stride = (size_t)sg.nblk * n;
@@ -1109,6 +1137,7 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
     k.sqrt6 = sqrt(0.1 * 60);
     k.temp_air = p->site[6];
     k.wind = p->site[7];
+    k.tmod_k = std::exp(k.module[TMH_MOD_TEMP_A] + k.module[TMH_MOD_TEMP_B] * k.wind);   // sapm_celltemp factor
     memcpy(e->gp.site, p->site, sizeof e->gp.site);
     memcpy(e->gp.linke, p->linke, sizeof e->gp.linke);
     memcpy(e->gp.module, p->module, sizeof e->gp.module);

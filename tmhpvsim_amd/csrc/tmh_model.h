@@ -24,6 +24,7 @@ struct KParams {
     double inverter[TMH_INV_COUNT];
     double alpha, delta, expo, sqrt09, sqrt6;   // cloud_cover_binary.py:35-40, scales
     double temp_air, wind;                      // sapm_celltemp inputs (pvmodel.py:69-70)
+    double tmod_k;                              // exp(a + b * wind): constant for the run (wind fixed at 0)
 };
 
 struct GParams {
@@ -194,17 +195,19 @@ __device__ void reset_sigma(double* sc, double* sl, Chain& ch, double h)
 }
 
 // cloud_cover_binary.py:80-107, one lane per chain (sequential kernel / init);
-// returns 0 or a fault status
+// returns 0 or a fault status.  Keyed draws: counter = the chain's next_cloud
+// call number (0 = the constructor's call), sub = try >> 1, half = try & 1, so
+// the candidate lengths of a call do not depend on the step it happens at.
 template <int RNG>
 __device__ uint32_t next_cloud(const KParams& kp, double* sc, double* sl, Chain& ch, const Draw<RNG>& dr, double h,
-                               double ws, uint64_t step, uint32_t tag, uint32_t call)
+                               double ws, uint32_t tag)
 {
     const double f = 1.0 / h - 1.0;
     int tries = 0;
-    ch.ncalls++;
+    const uint64_t ctr = ch.ncalls++;
     for (int rec = 0; rec < 2; ++rec) {
         for (int i = 0; i < 20; ++i, ++tries) {
-            const double u = dr.one(ch, step, tag, (call << 8) | (uint32_t)(tries >> 1), tries & 1);
+            const double u = dr.one(ch, ctr, tag, (uint32_t)(tries >> 1), tries & 1);
             const double cl = pow(kp.alpha + kp.delta * u, kp.expo) / ws;
             int last = -1;
             double best = 0.0;
@@ -263,11 +266,15 @@ __device__ __forceinline__ double cc_faithful(const DrawParams& dp, double u)
 }
 
 // CloudCoverBinary.next_cloud (cloud_cover_binary.py:80-107) with the 64 lanes
-// of a wavefront cooperating on ONE chain whose sigma arrays live in VGPRs:
-// entry k = chunk * 64 + lane of vc[] / vl[].  The element arithmetic is the
+// of a wavefront cooperating on ONE chain: entry k = chunk * 64 + lane.  The
+// first NCH chunks (128 entries: all but ~1e-6 of calls) live in
+// VGPRs for the whole window; chunks NCH.. stay in the chain's global sigma row
+// and are touched only while L > 128.  The element arithmetic is the
 // reference's (identical bits); np.argmin's first-index tie rule is a butterfly
 // reduction; the r_[cl, nsc[:last+1]] shift is a lane shuffle by one.
-constexpr int NCH = CAP / 64;
+constexpr int NCH = 2;
+constexpr int NCH_ALL = CAP / 64;
+
 
 // ---- wavefront primitives (DPP, readlane): no LDS round trips
 template <int CTRL>
@@ -336,37 +343,58 @@ __device__ __forceinline__ void argmin_first(double dval, int kval, double& dmin
     kmin = bk;
 }
 
+// Unscaled candidate lengths pow(alpha + delta u, expo) (cloud_cover_binary.py:35-40)
+// of try 0 for the 64 calls [kb, kb + 64): lane i holds call kb + i, plus the
+// uniform of try 1 (the other half of the same Philox block).  One pass of
+// 64 independent Philox + pow replaces 64 sequential, wave-redundant ones.
+__device__ __forceinline__ void cloud_candidates(const DrawParams& dp, uint64_t chain, uint32_t kb, int lane,
+                                                 double& x0, double& u1)
+{
+    const U4 b = keyed_block(dp.seed, chain, (uint64_t)(kb + (uint32_t)lane), TAG_CLOUD, 0);
+    u1 = u52(b.z, b.w);
+    x0 = pow_d(dp.alpha + dp.delta * u52(b.x, b.y), dp.expo);
+}
+
 __device__ __forceinline__ uint32_t next_cloud_regs(const DrawParams& dp, double (&vc)[NCH], double (&vl)[NCH],
-                                                    int& L, double h, double ws, uint64_t chain, uint64_t step,
-                                                    uint32_t call, int lane, double& cl_out, double& clr_out)
+                                                    double* gsc, double* gsl, int& L, double h, double ws,
+                                                    uint64_t chain, uint32_t ctr, double x0, double u1, int lane,
+                                                    double& cl_out, double& clr_out)
 {
     const double f = 1.0 / h - 1.0;
     int tries = 0;
     for (int rec = 0; rec < 2; ++rec) {
         for (int i = 0; i < 20; ++i, ++tries) {
-            const double u = keyed_u(dp.seed, chain, step, TAG_CLOUD, (call << 8) | (uint32_t)(tries >> 1), tries & 1);
-            // out of line on purpose: inlining ocml pow here and capping the
-            // kernel at 128 VGPR (launch_bounds(256, 4)) broke bit-parity on gfx950
-            const double cl = pow_d(dp.alpha + dp.delta * u, dp.expo) / ws;
+            // try 0 comes precomputed; later tries (about 3 % of calls) are drawn here.
+            // pow stays out of line: inlining ocml pow and capping the kernel at
+            // 128 VGPR (launch_bounds(256, 4)) once broke bit-parity on gfx950
+            double x;
+            if (tries == 0) x = x0;
+            else if (tries == 1) x = pow_d(dp.alpha + dp.delta * u1, dp.expo);
+            else x = pow_d(dp.alpha + dp.delta * keyed_u(dp.seed, chain, ctr, TAG_CLOUD, (uint32_t)(tries >> 1), tries & 1),
+                           dp.expo);
+            const double cl = x / ws;
             double bd = INFINITY;
             int bk = INT_MAX;
-#pragma unroll
-            for (int ch = 0; ch < NCH; ++ch) {
-                if (ch * 64 < L) {
-                    const int k = ch * 64 + lane;
-                    if (k < L) {
-                        const double nsc = cl + vc[ch];
-                        const double nsl = f * nsc;
-                        const double tot = nsc + nsl;
-                        if (nsl - vl[ch] > 0.0 && tot < 5400.0) {
-                            const double d = fabs(tot - 3600.0);
-                            if (d < bd) {   // chunks ascend in k: ties keep the lower k
-                                bd = d;
-                                bk = k;
-                            }
+            auto scan = [&](int k, double sc, double sl) {   // :83-88
+                if (k < L) {
+                    const double nsc = cl + sc;
+                    const double nsl = f * nsc;
+                    const double tot = nsc + nsl;
+                    if (nsl - sl > 0.0 && tot < 5400.0) {
+                        const double d = fabs(tot - 3600.0);
+                        if (d < bd) {   // chunks ascend in k: ties keep the lower k
+                            bd = d;
+                            bk = k;
                         }
                     }
                 }
+            };
+#pragma unroll
+            for (int ch = 0; ch < NCH; ++ch)
+                if (ch * 64 < L) scan(ch * 64 + lane, vc[ch], vl[ch]);
+            for (int ch = NCH; ch * 64 < L; ++ch) {
+                const int k = ch * 64 + lane;
+                if (k < L) scan(k, gsc[k], gsl[k]);
             }
             double dmin;
             int kmin;
@@ -375,12 +403,17 @@ __device__ __forceinline__ uint32_t next_cloud_regs(const DrawParams& dp, double
                 const int last = kmin;
                 if (last + 2 > CAP) return TMH_CHAIN_SIGMA_OVERFLOW;
                 double sc_last = 0.0, sl_last = 0.0;
+                if (last < NCH * 64) {
 #pragma unroll
-                for (int ch = 0; ch < NCH; ++ch)
-                    if (ch == (last >> 6)) {
-                        sc_last = readlane_f64(vc[ch], last & 63);
-                        sl_last = readlane_f64(vl[ch], last & 63);
-                    }
+                    for (int ch = 0; ch < NCH; ++ch)
+                        if (ch == (last >> 6)) {
+                            sc_last = readlane_f64(vc[ch], last & 63);
+                            sl_last = readlane_f64(vl[ch], last & 63);
+                        }
+                } else {
+                    sc_last = gsc[last];
+                    sl_last = gsl[last];
+                }
                 const double clr = f * (cl + sc_last) - sl_last;
                 double carry = 0.0;   // old entry 64 ch - 1 (lane 63 of the previous chunk)
 #pragma unroll
@@ -394,6 +427,16 @@ __device__ __forceinline__ uint32_t next_cloud_regs(const DrawParams& dp, double
                         vl[ch] = p == 0 ? clr : f * nsc;
                         carry = top;
                     }
+                }
+                for (int ch = NCH; ch * 64 <= last + 1; ++ch) {   // rare: entries 128.. in memory
+                    const int k = ch * 64 + lane;
+                    const double old = gsc[k];
+                    const double top = readlane_f64(old, 63);
+                    const double prev = dpp_f64<0x138>(carry, old);
+                    const double nsc = cl + prev;
+                    gsc[k] = nsc;
+                    gsl[k] = f * nsc;
+                    carry = top;
                 }
                 L = last + 2;
                 cl_out = cl;
@@ -412,13 +455,119 @@ __device__ __forceinline__ uint32_t next_cloud_regs(const DrawParams& dp, double
                     vl[ch] = f * vc[ch];
                 }
             }
+            for (int ch = NCH; ch * 64 < nl; ++ch) {
+                const int k = ch * 64 + lane;
+                if (k < nl) {
+                    gsc[k] = 300.0 * (k + 1);
+                    gsl[k] = f * gsc[k];
+                }
+            }
             L = nl;
         }
     }
     return TMH_CHAIN_ASSERT_BINARY;
 }
 
+// ---- wave min of a double (every lane's value >= 0 or +inf), result uniform
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ double dpp_f64_rows(double v)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(__double2loint(v), __double2loint(v), CTRL, ROWS, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(__double2hiint(v), __double2hiint(v), CTRL, ROWS, 0xF, false);
+    return __hiloint2double((int)hi, (int)lo);
+}
+
+__device__ __forceinline__ double wave_min_f64(double v)
+{
+    v = fmin(v, dpp_f64_rows<0xB1>(v));        // quad_perm [1,0,3,2]
+    v = fmin(v, dpp_f64_rows<0x4E>(v));        // quad_perm [2,3,0,1]
+    v = fmin(v, dpp_f64_rows<0x141>(v));       // row_half_mirror
+    v = fmin(v, dpp_f64_rows<0x140>(v));       // row_mirror: each row of 16 holds its min
+    v = fmin(v, dpp_f64_rows<0x142, 0xA>(v));  // row_bcast:15 -> rows 1, 3
+    v = fmin(v, dpp_f64_rows<0x143, 0xC>(v));  // row_bcast:31 -> rows 2, 3: lane 63 = wave min
+    return readlane_f64(v, 63);
+}
+
+// next_cloud fast path (cloud_cover_binary.py:80-107) for the common case: the
+// sigma arrays fit the two register chunks (L <= 128) and try 0 finds a
+// possible index (97 % of calls).  np.argmin's first-index rule = min over
+// the wave, then the lowest set lane of ballot(d == min).  Returns false (no
+// state touched) when the general path must run.
+__device__ __forceinline__ bool next_cloud_fast(double (&vc)[NCH], double (&vl)[NCH], int& L, double cl, double f,
+                                                int lane, double& clr_out)
+{
+    static_assert(NCH == 2, "fast path written for two register chunks");
+    if (L > 128) return false;
+    bool ok0, ok1;
+    double d0, d1;
+    {
+        const double nsc = cl + vc[0];
+        const double nsl = f * nsc;
+        const double tot = nsc + nsl;
+        ok0 = lane < L && nsl - vl[0] > 0.0 && tot < 5400.0;
+        d0 = ok0 ? fabs(tot - 3600.0) : INFINITY;
+    }
+    {
+        const double nsc = cl + vc[1];
+        const double nsl = f * nsc;
+        const double tot = nsc + nsl;
+        ok1 = 64 + lane < L && nsl - vl[1] > 0.0 && tot < 5400.0;
+        d1 = ok1 ? fabs(tot - 3600.0) : INFINITY;
+    }
+    const double dmin = wave_min_f64(fmin(d0, d1));
+    if (!(dmin < INFINITY)) return false;
+    const uint64_t m0 = __builtin_amdgcn_ballot_w64(ok0 && d0 == dmin);
+    const uint64_t m1 = __builtin_amdgcn_ballot_w64(ok1 && d1 == dmin);
+    int last;
+    double sc_last, sl_last;
+    if (m0) {
+        last = __builtin_ctzll(m0);
+        sc_last = readlane_f64(vc[0], last);
+        sl_last = readlane_f64(vl[0], last);
+    } else {
+        last = 64 + __builtin_ctzll(m1);
+        sc_last = readlane_f64(vc[1], last - 64);
+        sl_last = readlane_f64(vl[1], last - 64);
+    }
+    const double clr = f * (cl + sc_last) - sl_last;
+    // sigma_cloud = r_[cl, nsc[:last+1]], sigma_clear = r_[clr, nsl[:last+1]]
+    const double top0 = readlane_f64(vc[0], 63);
+    {
+        const double prev = dpp_f64<0x138>(0.0, vc[0]);   // wave_shr:1
+        const double nsc = cl + prev;
+        vc[0] = lane == 0 ? cl : nsc;
+        vl[0] = lane == 0 ? clr : f * nsc;
+    }
+    if (last + 1 >= 64) {
+        const double prev = dpp_f64<0x138>(top0, vc[1]);   // lane 0 <- old entry 63
+        const double nsc = cl + prev;
+        vc[1] = nsc;
+        vl[1] = f * nsc;
+    }
+    L = last + 2;
+    clr_out = clr;
+    return true;
+}
+
 // ------------------------------------------------------------ clock + geometry
+// min_f = s / 60, hour_f = (m + min_f) / 60, day_f = (h + hour_f) / 24
+// (clearskyindexmodel.py:114-116) without fp64 divisions: q = x * (1/d) plus
+// one FMA residual correction.  Equal to the IEEE quotient for every one of
+// the 86,400 wall-clock seconds (checked exhaustively: oracle orc_check_fractions).
+__device__ __forceinline__ double div_exact(double x, double d, double rd)
+{
+    const double q = x * rd;
+    return fma(fma(-q, d, x), rd, q);
+}
+
+__device__ __forceinline__ void clock_fractions(int hour, int minute, int second, double& min_f, double& hour_f,
+                                                double& day_f)
+{
+    min_f = div_exact((double)second, 60.0, 1.0 / 60.0);
+    hour_f = div_exact(minute + min_f, 60.0, 1.0 / 60.0);
+    day_f = div_exact(hour + hour_f, 24.0, 1.0 / 24.0);
+}
+
 __device__ __forceinline__ double rad(double d) { return d * (3.14159265358979323846 / 180.0); }
 __device__ __forceinline__ double deg(double r) { return r * (180.0 / 3.14159265358979323846); }
 __device__ __forceinline__ double cosd(double d) { return cos(rad(d)); }
@@ -565,10 +714,17 @@ __device__ __forceinline__ R pv_power(const KParams& kp, const R* g, R csi)
     const R poa_diffuse = sky + ground;
     const R poa_global = poa_direct + poa_diffuse;
     // sapm_celltemp (pvmodel.py:69-70), open_rack_cell_glassback
-    const R tmod = poa_global * exp(R(m[TMH_MOD_TEMP_A]) + R(m[TMH_MOD_TEMP_B]) * R(kp.wind)) + R(kp.temp_air);
-    const R tcell = tmod + (poa_global / R(1000)) * R(m[TMH_MOD_TEMP_DT]);
-    // sapm_effective_irradiance, suns (pvmodel.py:74-76)
-    const R Ee = g[G_F1] * (poa_direct * g[G_F2] + R(m[TMH_MOD_FD]) * poa_diffuse) / R(1000);
+    // (fp32: the divisions by 1000 become products with 1e-3, within the fp32 tolerance)
+    const R tmod = poa_global * R(kp.tmod_k) + R(kp.temp_air);
+    R tcell, Ee;
+    if constexpr (sizeof(R) == 8) {
+        tcell = tmod + (poa_global / R(1000)) * R(m[TMH_MOD_TEMP_DT]);
+        // sapm_effective_irradiance, suns (pvmodel.py:74-76)
+        Ee = g[G_F1] * (poa_direct * g[G_F2] + R(m[TMH_MOD_FD]) * poa_diffuse) / R(1000);
+    } else {
+        tcell = tmod + (poa_global * R(1e-3)) * R(m[TMH_MOD_TEMP_DT]);
+        Ee = g[G_F1] * (poa_direct * g[G_F2] + R(m[TMH_MOD_FD]) * poa_diffuse) * R(1e-3);
+    }
     // sapm (pvmodel.py:77)
     const R q = R(1.60218e-19), kb = R(1.38066e-23);
     const R Bvmpo = R(m[TMH_MOD_BVMPO]) + R(m[TMH_MOD_MBVMP]) * (R(1) - Ee);
@@ -588,7 +744,9 @@ __device__ __forceinline__ R pv_power(const KParams& kp, const R* g, R csi)
     const R A = R(iv[1]) * (R(1) + R(iv[5]) * dv);
     const R B = R(iv[3]) * (R(1) + R(iv[6]) * dv);
     const R C = R(iv[4]) * (R(1) + R(iv[7]) * dv);
-    R ac = (R(iv[0]) / (A - B) - C * (A - B)) * (pdc - B) + C * ((pdc - B) * (pdc - B));
+    R ac;
+    if constexpr (sizeof(R) == 8) ac = (R(iv[0]) / (A - B) - C * (A - B)) * (pdc - B) + C * ((pdc - B) * (pdc - B));
+    else ac = (__fdividef(R(iv[0]), A - B) - C * (A - B)) * (pdc - B) + C * ((pdc - B) * (pdc - B));
     if (!isnan(ac)) ac = R(iv[0]) < ac ? R(iv[0]) : ac;
     if (pdc < R(iv[3])) ac = R(-1) * fabs(R(iv[8]));
     if (isnan(ac)) return R(0);                       // .fillna(0.)
@@ -625,23 +783,33 @@ __device__ __forceinline__ void second_body(const KParams& kp, const R* row, uin
 {
     const R cloudcover = rinterp(fs, S_CC, row[G_HOURF]);   // == interp() bit for bit when R = double
     R z;
+#ifdef TMH_DIAG_NO_NDTRI
+    z = R(ue - 0.5);
+#else
     if constexpr (sizeof(R) == 8) z = ndtri(ue);
     else z = ndtri_f(ue);
+#endif
     const R eps = z * (R(kp.sqrt6) * (R(0.001) + R(0.0015 * 8) * cloudcover)) + R(0);
     if (covered)
         csi = rinterp(fs, S_CLEAR_DAY, row[G_DAYF]) * (rinterp(fs, S_CLEAR_NOISE, row[G_MINF]) + eps);
     else
         csi = rinterp(fs, S_CLOUDY_HOUR, row[G_HOURF]) * (rinterp(fs, S_CLOUDY_NOISE, row[G_MINF]) + eps);
+#ifdef TMH_DIAG_NO_PV
+    pv = csi * row[G_GHICS];
+#else
     pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power<R>(kp, row, csi) : R(0);
+#endif
     if constexpr (sizeof(R) == 8) meter = 9000 * um;
     else meter = fminf((float)(9000 * um), 8999.9990234375f);   // largest float < 9000: keep [0, 9000)
     res = meter - pv;
 }
 
+// streaming trace stores: non-temporal, so the write-once trace does not
+// evict the tables and draw buffers the block re-reads
 template <typename R>
 __device__ __forceinline__ void trace_store(void* p, uint64_t i, R v)
 {
-    if (p) reinterpret_cast<R*>(p)[i] = v;
+    if (p) __builtin_nontemporal_store(v, reinterpret_cast<R*>(p) + i);
 }
 
 struct Acc {
