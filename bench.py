@@ -12,9 +12,13 @@ Multi-GPU (torchrun, one rank per GPU): weak scaling, every rank runs its own
 4,096 chains with distinct global ids; no data-path collective (chains are
 independent).  value = chain-seconds of all ranks / max rank time.
 
-Roofline: the dominant kernel (chain_kernel) is timed alone with HIP events on
-the stream it runs on; achieved = 12 B x chains x seconds per launch / mean
-launch time, against 8 TB/s.  cpu_baseline: the C oracle (oracle/tmh_oracle.c,
+Roofline: the dominant kernel (expand_kernel, P2 of the time-parallel path) is
+timed with HIP events the library records on the stream it runs on
+(tmh_profile_enable / tmh_profile_read); achieved = 12 B x chains x seconds per
+launch / mean launch time, against 8 TB/s.  `traffic` = HBM bytes per launch of
+that kernel from the rocprofv3 PMC passes (scripts/pmc.sh, FETCH_SIZE x 2 +
+WRITE_SIZE, MI355X_MICROARCH.md), read from profiles/pmc_traffic.json when it
+was measured on this same workload, else null.  cpu_baseline: the C oracle (oracle/tmh_oracle.c,
 "port") on a bounded sample of the same workload on this host, rank 0, N = 1.
 """
 from __future__ import annotations
@@ -65,6 +69,19 @@ def cpu_baseline(args):
                       f"{dt:.1f} s wall)"}
 
 
+def traffic(args, n, secs):
+    """HBM bytes per expand_kernel launch from the committed PMC summary, when it
+    was measured on this workload (scripts/pmc.sh + scripts/pmc_summary.py)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if (d.get("chains"), d.get("seconds"), d.get("precision"), d.get("mode")) != (n, secs, args.precision, args.mode):
+        return None
+    return d.get("traffic_bytes_per_launch")
+
+
 def main():
     args = parse()
     import torch
@@ -104,24 +121,24 @@ def main():
     scratch = torch.empty(L.tmh_scratch_bytes(n, secs), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     sptr = C.c_void_p(stream.cuda_stream)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.warmup + args.steps)]
+
+    L.tmh_profile_enable(sim._eng, 1)
 
     def one_step(k):
         chain0 = (rank + k * world) * n                    # fresh global chains every batch
         _lib.check(L.tmh_plan(sim._eng, 0, secs, C.c_void_p(plan.data_ptr()), sptr))
         _lib.check(L.tmh_init(sim._eng, C.c_void_p(sim.state.data_ptr()), chain0, n, None, sptr))
-        ev[k][0].record(stream)
         _lib.check(L.tmh_step(sim._eng, C.c_void_p(sim.state.data_ptr()), chain0, n, 0, secs, None,
                               C.byref(tr), C.byref(st) if st is not None else None,
                               C.c_void_p(plan.data_ptr()), C.c_void_p(scratch.data_ptr()), scratch.numel(), sptr))
-        ev[k][1].record(stream)
         if args.mode == "stats":                           # the one exchange step: RCCL all-reduce
             totals[0] = all_reduce_stats(sim.stats_totals())
 
     for k in range(args.warmup):
         one_step(k)
     torch.cuda.synchronize()
+    for kk in (_lib.K_EXPAND, _lib.K_SEGMENTS, _lib.K_MINUTE_DRAWS, _lib.K_STEP):
+        _lib.profile_read(sim._eng, kk)                    # drop the warmup launches
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -133,14 +150,17 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = [ev[k][0].elapsed_time(ev[k][1]) for k in range(args.warmup, args.warmup + args.steps)]
+    phases = {}
+    for name, kk in (("expand", _lib.K_EXPAND), ("segments", _lib.K_SEGMENTS),
+                     ("minute_draws", _lib.K_MINUTE_DRAWS), ("tmh_step", _lib.K_STEP)):
+        ms, cnt = _lib.profile_read(sim._eng, kk)
+        phases[name] = ms / cnt if cnt else None
     bad = int((sim.status() != 0).sum())
+    kmean = phases["expand"] if phases["expand"] else float("nan")
     if world > 1:
-        t = torch.tensor([elapsed, sum(kern_ms) / len(kern_ms)], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, kmean], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kmean = float(t[0]), float(t[1])
-    else:
-        kmean = sum(kern_ms) / len(kern_ms)
     chain_seconds = world * n * secs * args.steps
     value = chain_seconds / elapsed
     achieved = TRACE_BYTES * n * secs / (kmean / 1e3) / 1e9
@@ -153,12 +173,13 @@ def main():
                                f"{args.start[:10]}, {args.mode} mode ({'meter+pv+residual fp32 trace' if args.mode == 'trace' else 'on-GPU stats'})",
                    "chains_per_gpu": n, "seconds": secs, "parallelism": f"chains sharded over {world} GPU(s)"},
         "roofline": ({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                      "kernel": "tmh_step (" + sim.path + ")", "kernel_ms": kmean,
+                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic(args, n, secs),
+                      "kernel": "expand_kernel (P2, " + sim.path + ")", "kernel_ms": kmean,
                       "bytes_per_launch": TRACE_BYTES * n * secs} if args.mode == "trace" else
                      {"bound": "valu", "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
-                      "kernel": "tmh_step (" + sim.path + ")", "kernel_ms": kmean,
+                      "kernel": "expand_kernel (P2, " + sim.path + ")", "kernel_ms": kmean,
                       "note": "stats mode stores no trace; VALU counters under profiles/"}),
+        "phases_ms": phases,
         "faulted_chains": bad,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -183,6 +183,16 @@ int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
              const tmh_stats* stats, const void* plan, void* scratch, size_t scratch_bytes,
              void* stream);
 
+/* Kernel timing (measurement only).  While enabled, tmh_step records HIP
+ * events, on the stream each kernel runs on, around the kernels of the
+ * time-parallel path; tmh_profile_read waits for them and returns the summed
+ * milliseconds and launch count of one kernel since the last read, then resets
+ * it.  kernel: TMH_K_EXPAND (P2 trace/stats expansion), TMH_K_SEGMENTS (P1
+ * segment walk), TMH_K_MINUTE_DRAWS, TMH_K_STEP (the whole tmh_step). */
+enum { TMH_K_EXPAND = 0, TMH_K_SEGMENTS = 1, TMH_K_MINUTE_DRAWS = 2, TMH_K_STEP = 3, TMH_K_COUNT = 4 };
+int tmh_profile_enable(struct tmh_engine* eng, int on);
+int tmh_profile_read(struct tmh_engine* eng, int kernel, double* total_ms, int* launches);
+
 /* Device math probes for parity tests: out[i] = f(a, x[i]) with
  * f = 0 ndtri, 1 gammaincinv, 2 stdtrit, 3 al_ppf, 4 ndtri (fp32 path). */
 int tmh_probe(int fn, double a, const double* x, double* out, uint32_t n, void* stream);

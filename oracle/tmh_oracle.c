@@ -51,7 +51,7 @@ void orc_T_hist(uint64_t* out, int reset)
 
 enum { ST_OK = 0, ST_NAMEERROR_INIT = 1, ST_ASSERT_BINARY = 2, ST_SIGMA_OVERFLOW = 3,
        ST_U_EXHAUSTED = 4 };
-enum { TAG_STEP = 1, TAG_BOUNDARY = 2, TAG_CLOUD = 3, TAG_INIT = 4, TAG_INIT_CLOUD = 5,
+enum { TAG_STEP = 1, TAG_BOUNDARY = 2, TAG_CLOUD = 3, TAG_INIT = 4, TAG_INIT_CLOUD = 5, TAG_STEP2 = 7,
        TAG_INIT_SEC = 6 };
 enum { S_CC = 0, S_CLEAR_DAY = 1, S_CLOUDY_HOUR = 2, S_CLOUDY_NOISE = 3, S_CLEAR_NOISE = 4,
        S_WS = 5 };
@@ -104,6 +104,18 @@ static double keyed_u(uint64_t seed, uint64_t chain, uint64_t step, uint32_t tag
     uint32_t k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)}, o[4];
     philox4x32_10(c, k, o);
     return half ? u52(o[2], o[3]) : u52(o[0], o[1]);
+}
+
+/* per-second draws: one block per step pair p = step >> 1, 32-bit midpoint
+ * uniforms (w + 1/2) 2^-32; (x, y) = (noise, meter) of step 2p, (z, w) of 2p + 1 */
+static void step_u(uint64_t seed, uint64_t chain, uint64_t step, double* ue, double* um)
+{
+    uint32_t c[4] = {(uint32_t)(step >> 1), (uint32_t)TAG_STEP2 << 28, (uint32_t)chain, (uint32_t)(chain >> 32)};
+    uint32_t k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)}, o[4];
+    philox4x32_10(c, k, o);
+    const int odd = (int)(step & 1);
+    *ue = ((double)o[odd ? 2 : 0] + 0.5) * 0x1p-32;
+    *um = ((double)o[odd ? 3 : 1] + 0.5) * 0x1p-32;
 }
 
 /* --------------------------------------------------------------- variates */
@@ -759,7 +771,10 @@ int orc_run(const orc_params* P, uint64_t chain0, uint32_t n_chains, uint32_t n_
                     ch->sec += 1;
                 }
                 if (!ch->status) {
-                    double eps = orc_ndtri(draw_u(&X, ch, step, TAG_STEP, 0, 0)) *
+                    double ue, um_unused;
+                    step_u(P->seed, ch->chain, step, &ue, &um_unused);
+                    if (P->rng_mode == 1) ue = draw_u(&X, ch, step, TAG_STEP, 0, 0);
+                    double eps = orc_ndtri(ue) *
                                  (X.sqrt6 * (0.001 + 0.0015 * 8 * cloudcover)) + 0.0;
                     if (cov) csi = interp(ch->s[S_CLEAR_DAY], df) * (interp(ch->s[S_CLEAR_NOISE], mf) + eps);
                     else csi = interp(ch->s[S_CLOUDY_HOUR], hf) * (interp(ch->s[S_CLOUDY_NOISE], mf) + eps);
@@ -773,7 +788,9 @@ int orc_run(const orc_params* P, uint64_t chain0, uint32_t n_chains, uint32_t n_
             double pv = NAN, meter = NAN;
             if (!ch->status) {
                 pv = P->with_pv ? pv_power(P, &G[s], csi) : 0.0;
-                meter = 9000 * keyed_u(P->seed, ch->chain, s, TAG_STEP, 0, 1);
+                double ue_unused, um;
+                step_u(P->seed, ch->chain, s, &ue_unused, &um);
+                meter = 9000 * um;
             }
             if (pv_out) pv_out[o] = pv;
             if (meter_out) meter_out[o] = meter;

@@ -32,6 +32,8 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "tmh_math.h"
 #include "tmh_model.h"
@@ -521,13 +523,13 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
                 else ch.sec += 1;
             }
             if (ch.status == 0) {
-                double ue, um;
-                if constexpr (RNG == TMH_RNG_KEYED) {
-                    dr.two(ch, step, TAG_STEP, 0, ue, um);
-                } else {   // the meter is its own process in the reference: always keyed
-                    ue = dr.one(ch, step, TAG_STEP, 0, 0);
-                    um = keyed_u(kp.seed, chain, step, TAG_STEP, 0, 1);
-                }
+                // keyed: one Philox block per step pair, 32-bit words;
+                // the meter is its own process in the reference: always keyed
+                const U4 pb = keyed_block(kp.seed, chain, (uint64_t)step >> 1, TAG_STEP2, 0);
+                const bool odd = step & 1;
+                double ue = u32d(odd ? pb.z : pb.x);
+                const double um = u32d(odd ? pb.w : pb.y);
+                if constexpr (RNG == TMH_RNG_INJECTED) ue = dr.one(ch, step, TAG_STEP, 0, 0);
                 if (ch.status == 0) {
                     const bool covered = ch.sec < ch.t1;
                     cov = covered ? 1 : 0;
@@ -734,7 +736,7 @@ __global__ __launch_bounds__(256) void segments_kernel(DrawParams dp, StateView 
 // One work-item per (chain, block of 256 seconds).  The boundary draws come
 // from the draw tables, so the per-second loop holds only the R copies of the
 // sampler pairs and does no fp64 work in fp32 mode.
-template <typename R>
+template <typename R, int OUT>
 __global__ __launch_bounds__(256) void expand_kernel(KParams kp, StateView st, uint64_t chain0, uint32_t n,
                                                      int64_t W0, uint32_t nsteps, int64_t utc0,
                                                      const double* __restrict__ tab64,
@@ -787,6 +789,8 @@ __global__ __launch_bounds__(256) void expand_kernel(KParams kp, StateView st, u
     }
     const double* evd = sg.evd + c;
     const double* mind = sg.mind + c;
+    U4 pair{0, 0, 0, 0};
+    bool have_pair = false;
     for (uint32_t j = j0; j < j1; ++j) {
         const int64_t step = W0 + j;
         const float* r32 = tab32 + (size_t)j * ROW;
@@ -821,19 +825,25 @@ __global__ __launch_bounds__(256) void expand_kernel(KParams kp, StateView st, u
             while (step >= (int64_t)seg.y) seg = rec[++jr];   // next_cloud happened at seg.y
             const bool covered = step < (int64_t)seg.x;
             cov = covered ? 1 : 0;
+            if (!(step & 1) || !have_pair) {   // one Philox block per step pair (uniform branch)
 #ifdef TMH_DIAG_NO_RNG   // diagnostic builds only (scripts/diag_variants.sh): cost breakdown
-            const uint32_t hsh = (uint32_t)chain * 0x9E3779B9u ^ (uint32_t)step * 0x85EBCA6Bu;
-            const U4 u{hsh, hsh >> 3, hsh ^ 0x5555u, hsh >> 5};
+                const uint32_t hsh = (uint32_t)chain * 0x9E3779B9u ^ (uint32_t)step * 0x85EBCA6Bu;
+                pair = U4{hsh, hsh >> 3, hsh ^ 0x5555u, hsh >> 5};
 #else
-            const U4 u = keyed_block(kp.seed, chain, (uint64_t)step, TAG_STEP, 0);
+                pair = keyed_block(kp.seed, chain, (uint64_t)step >> 1, TAG_STEP2, 0);
 #endif
-            second_body<R>(kp, row, fl, fs, covered, u52(u.x, u.y), u52(u.z, u.w), csi, pv, meter, res);
+                have_pair = true;
+            }
+            const bool odd = step & 1;
+            second_body<R>(kp, row, fl, fs, covered, u32d(odd ? pair.z : pair.x), u32d(odd ? pair.w : pair.y), csi, pv,
+                           meter, res);
         }
         if (fl & (FL_DAY | FL_HOUR)) ++evi;
 #ifdef TMH_DIAG_NO_STORE
-        if (live && csi == R(-12345)) emit<R>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok);
+        if (live && csi == R(-12345))
+            emit<R, OUT>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok);
 #else
-        if (live) emit<R>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok);
+        if (live) emit<R, OUT>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok);
 #endif
     }
     if (live && sv.acc) {
@@ -1054,6 +1064,52 @@ struct tmh_engine {
     GParams gp;
     int device;
     int path;   // resolved kernel path: 1 sequential, 2 time-parallel
+    // side stream: the minute draws run beside the segment walk (both need only
+    // the event draws); created on first use, never holds device memory
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // kernel timing (tmh_profile_*): event pairs per kernel, read and recycled
+    bool profiling = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[TMH_K_COUNT];
+    std::vector<hipEvent_t> pool;
+    hipEvent_t event()
+    {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e = nullptr;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+    // returns the start event of a timed region (nullptr when not profiling)
+    hipEvent_t mark(hipStream_t s)
+    {
+        if (!profiling) return nullptr;
+        hipEvent_t a = event();
+        (void)hipEventRecord(a, s);
+        return a;
+    }
+    void close(int k, hipEvent_t a, hipStream_t s)
+    {
+        if (!a) return;
+        hipEvent_t b = event();
+        (void)hipEventRecord(b, s);
+        prof[k].emplace_back(a, b);
+    }
+    ~tmh_engine()
+    {
+        for (auto& v : prof)
+            for (auto& p : v) {
+                (void)hipEventDestroy(p.first);
+                (void)hipEventDestroy(p.second);
+            }
+        for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+        if (ev_join) (void)hipEventDestroy(ev_join);
+        if (aux) (void)hipStreamDestroy(aux);
+    }
 };
 
 extern "C" {
@@ -1169,6 +1225,34 @@ int tmh_engine_destroy(struct tmh_engine* eng)
 
 int tmh_engine_path(const struct tmh_engine* eng) { return eng ? eng->path : TMH_E_INVAL; }
 
+int tmh_profile_enable(struct tmh_engine* eng, int on)
+{
+    if (!eng) return fail(TMH_E_INVAL, "NULL engine");
+    eng->profiling = on != 0;
+    return TMH_OK;
+}
+
+int tmh_profile_read(struct tmh_engine* eng, int kernel, double* total_ms, int* launches)
+{
+    if (!eng || !total_ms || kernel < 0 || kernel >= TMH_K_COUNT) return fail(TMH_E_INVAL, "bad profile_read args");
+    if (int rc = hip_check(hipSetDevice(eng->device), "hipSetDevice")) return rc;
+    double t = 0.0;
+    int n = 0;
+    for (auto& p : eng->prof[kernel]) {
+        if (int rc = hip_check(hipEventSynchronize(p.second), "hipEventSynchronize")) return rc;
+        float ms = 0.f;
+        if (int rc = hip_check(hipEventElapsedTime(&ms, p.first, p.second), "hipEventElapsedTime")) return rc;
+        t += ms;
+        ++n;
+        eng->pool.push_back(p.first);
+        eng->pool.push_back(p.second);
+    }
+    eng->prof[kernel].clear();
+    *total_ms = t;
+    if (launches) *launches = n;
+    return TMH_OK;
+}
+
 int tmh_init(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, const tmh_ustream* inj,
              void* stream)
 {
@@ -1266,22 +1350,53 @@ int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
     scratch_layout(n_chains, n_steps, scratch, &sg);
     const uint32_t cb = (n_chains + 255) / 256;
     const int64_t utc0 = eng->gp.clock.utc0;
+    if (!eng->aux) {
+        if (int rc = hip_check(hipStreamCreateWithFlags(&eng->aux, hipStreamNonBlocking), "hipStreamCreate")) return rc;
+        if (int rc = hip_check(hipEventCreateWithFlags(&eng->ev_fork, hipEventDisableTiming), "hipEventCreate"))
+            return rc;
+        if (int rc = hip_check(hipEventCreateWithFlags(&eng->ev_join, hipEventDisableTiming), "hipEventCreate"))
+            return rc;
+    }
+    hipEvent_t t_step = eng->mark(s);
     hipLaunchKernelGGL(event_draws_kernel, dim3(sg.evcap, cb), dim3(256), 0, s, eng->dp, chain0, n_chains, n_steps,
                        pv.events, pv.n_events, sg.evd);
-    hipLaunchKernelGGL(minute_draws_kernel, dim3(sg.nmin, cb), dim3(256), 0, s, eng->dp, v, chain0, n_chains, step0,
-                       n_steps, utc0, pv.tab64, pv.events, pv.n_events, sg.evd, sg.mind);
+    // fork: minute draws on the side stream, segment walk on `s`; join before P2
+    if (int rc = hip_check(hipEventRecord(eng->ev_fork, s), "hipEventRecord")) return rc;
+    if (int rc = hip_check(hipStreamWaitEvent(eng->aux, eng->ev_fork, 0), "hipStreamWaitEvent")) return rc;
+    hipEvent_t t_min = eng->mark(eng->aux);
+    hipLaunchKernelGGL(minute_draws_kernel, dim3(sg.nmin, cb), dim3(256), 0, eng->aux, eng->dp, v, chain0, n_chains,
+                       step0, n_steps, utc0, pv.tab64, pv.events, pv.n_events, sg.evd, sg.mind);
+    eng->close(TMH_K_MINUTE_DRAWS, t_min, eng->aux);
+    if (int rc = hip_check(hipEventRecord(eng->ev_join, eng->aux), "hipEventRecord")) return rc;
+    hipEvent_t t_seg = eng->mark(s);
     hipLaunchKernelGGL(segments_kernel, dim3((n_chains + 3) / 4), dim3(256), 0, s, eng->dp, v, chain0, n_chains,
                        step0, n_steps, eng->gp.clock, pv.events, pv.n_events, sg);
+    eng->close(TMH_K_SEGMENTS, t_seg, s);
+    if (int rc = hip_check(hipStreamWaitEvent(s, eng->ev_join, 0), "hipStreamWaitEvent")) return rc;
     if (int rc = hip_check(hipGetLastError(), "draws/segments kernels launch")) return rc;
+    hipEvent_t t_exp = eng->mark(s);
     dim3 grid2(nblk_of(n_steps), cb);
-    if (f64)
-        hipLaunchKernelGGL(expand_kernel<double>, grid2, dim3(256), lds, s, eng->kp, v, chain0, n_chains, step0,
-                           n_steps, utc0, pv.tab64, pv.tab32, pv.desc, sg, tv, sv);
-    else
-        hipLaunchKernelGGL(expand_kernel<float>, grid2, dim3(256), lds, s, eng->kp, v, chain0, n_chains, step0,
-                           n_steps, utc0, pv.tab64, pv.tab32, pv.desc, sg, tv, sv);
+    const bool no_stats = !sv.hist && !sv.acc;
+    const int out = (no_stats && tv.pv && tv.meter && tv.residual && !tv.csi && !tv.covered) ? OUT_TRACE3
+                    : (!tv.pv && !tv.meter && !tv.residual && !tv.csi && !tv.covered) ? OUT_STATS
+                                                                                      : OUT_ANY;
+#define LAUNCH(R, O)                                                                                                 \
+    hipLaunchKernelGGL((expand_kernel<R, O>), grid2, dim3(256), lds, s, eng->kp, v, chain0, n_chains, step0, n_steps, \
+                       utc0, pv.tab64, pv.tab32, pv.desc, sg, tv, sv)
+    if (f64) {
+        if (out == OUT_TRACE3) LAUNCH(double, OUT_TRACE3);
+        else if (out == OUT_STATS) LAUNCH(double, OUT_STATS);
+        else LAUNCH(double, OUT_ANY);
+    } else {
+        if (out == OUT_TRACE3) LAUNCH(float, OUT_TRACE3);
+        else if (out == OUT_STATS) LAUNCH(float, OUT_STATS);
+        else LAUNCH(float, OUT_ANY);
+    }
+#undef LAUNCH
+    eng->close(TMH_K_EXPAND, t_exp, s);
     if (int rc = hip_check(hipGetLastError(), "expand_kernel launch")) return rc;
     hipLaunchKernelGGL(commit_kernel, dim3(cb), dim3(256), 0, s, v, n_chains, sg, sv, pv.desc + nblk_of(n_steps));
+    eng->close(TMH_K_STEP, t_step, s);
     return hip_check(hipGetLastError(), "commit_kernel launch");
 }
 

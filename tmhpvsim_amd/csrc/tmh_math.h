@@ -47,6 +47,9 @@ __device__ __forceinline__ double u52(uint32_t lo, uint32_t hi)
     return (double)((v >> 11) | 1ull) * 0x1p-53;
 }
 
+// 32-bit midpoint uniform (w + 1/2) 2^-32, exact in fp64 (per-second draws)
+__device__ __forceinline__ double u32d(uint32_t w) { return ((double)w + 0.5) * 0x1p-32; }
+
 // draw-family tags (ctr1 = tag << 28 | sub); must match oracle/philox.py
 enum : uint32_t {
     TAG_STEP = 1,
@@ -54,7 +57,8 @@ enum : uint32_t {
     TAG_CLOUD = 3,
     TAG_INIT = 4,
     TAG_INIT_CLOUD = 5,
-    TAG_INIT_SEC = 6
+    TAG_INIT_SEC = 6,
+    TAG_STEP2 = 7   // per step pair p = step >> 1: (x, y) = (noise, meter) of step 2p, (z, w) of 2p + 1
 };
 
 __device__ __forceinline__ U4 keyed_block(uint64_t seed, uint64_t chain, uint64_t step, uint32_t tag,

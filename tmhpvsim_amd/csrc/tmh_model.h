@@ -816,15 +816,30 @@ struct Acc {
     double pv, m, r, mx;
 };
 
-template <typename R>
+// output specialisations of the time-parallel expansion (chosen on the host)
+enum : int {
+    OUT_ANY = 0,      // any combination of trace fields and statistics
+    OUT_TRACE3 = 1,   // exactly pv, meter, residual traces (the trace-mode hot path)
+    OUT_STATS = 2     // statistics only, no trace
+};
+
+template <typename R, int OUT = OUT_ANY>
 __device__ __forceinline__ void emit(const TraceView& tr, const StatsView& sv, uint32_t* lds_hist, uint64_t o,
                                      uint8_t cov, R csi, R pv, R meter, R res, Acc& acc, bool ok)
 {
-    trace_store<R>(tr.csi, o, csi);
-    trace_store<R>(tr.pv, o, pv);
-    trace_store<R>(tr.meter, o, meter);
-    trace_store<R>(tr.residual, o, res);
-    if (tr.covered) tr.covered[o] = cov;
+    if constexpr (OUT == OUT_TRACE3) {
+        __builtin_nontemporal_store(pv, reinterpret_cast<R*>(tr.pv) + o);
+        __builtin_nontemporal_store(meter, reinterpret_cast<R*>(tr.meter) + o);
+        __builtin_nontemporal_store(res, reinterpret_cast<R*>(tr.residual) + o);
+        return;
+    }
+    if constexpr (OUT == OUT_ANY) {
+        trace_store<R>(tr.csi, o, csi);
+        trace_store<R>(tr.pv, o, pv);
+        trace_store<R>(tr.meter, o, meter);
+        trace_store<R>(tr.residual, o, res);
+        if (tr.covered) tr.covered[o] = cov;
+    }
     if (ok) {
         if (sv.acc) {
             acc.pv += (double)pv;
