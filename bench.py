@@ -41,7 +41,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--chains", type=int, default=4096, help="chains per GPU")
     ap.add_argument("--seconds", type=int, default=86400)
     ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64"])
@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--cpu-sample-chains", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--path", default="auto", choices=["auto", "sequential", "time_parallel"])
+    ap.add_argument("--pipeline", type=int, default=2,
+                    help="batches in flight on separate HIP streams (1 = no overlap): batch k+1's segment "
+                         "walk (latency-bound, one wave per SIMD) runs beside batch k's expansion")
     return ap.parse_args()
 
 
@@ -104,40 +107,64 @@ def main():
 
     from tmhpvsim_amd.dist import all_reduce_stats
 
-    totals = [None]
     L = _lib.load()
     n, secs = args.chains, args.seconds
     sim = BatchedSim(n, args.start, tz="Europe/Berlin", params=ModelParams(), precision=args.precision,
                      chain0=rank * n, device=dev, horizon=secs, kernel_path=args.path)
     real = sim.real
-    trace = {f: torch.empty(secs, n, dtype=real, device=dev) for f in ("pv", "meter", "residual")} \
-        if args.mode == "trace" else {}
-    if args.mode == "stats":
-        sim.enable_stats()
-    st = sim._stats_struct()
-    tr = _lib.Trace(None, None, *(trace[f].data_ptr() if f in trace else None
-                                  for f in ("pv", "meter", "residual")), n)
-    plan = torch.empty(L.tmh_plan_bytes(secs), dtype=torch.uint8, device=dev)
-    scratch = torch.empty(L.tmh_scratch_bytes(n, secs), dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    sptr = C.c_void_p(stream.cuda_stream)
 
+    class Ctx:   # one batch in flight: its own state, plan, scratch, outputs and HIP stream
+        def __init__(self):
+            self.stream = torch.cuda.Stream(dev)
+            self.sptr = C.c_void_p(self.stream.cuda_stream)
+            self.state = torch.zeros(L.tmh_state_bytes(n), dtype=torch.uint8, device=dev)
+            self.plan = torch.empty(L.tmh_plan_bytes(secs), dtype=torch.uint8, device=dev)
+            self.scratch = torch.empty(L.tmh_scratch_bytes(n, secs), dtype=torch.uint8, device=dev)
+            self.trace = {f: torch.empty(secs, n, dtype=real, device=dev) for f in ("pv", "meter", "residual")} \
+                if args.mode == "trace" else {}
+            self.tr = _lib.Trace(None, None, *(self.trace[f].data_ptr() if f in self.trace else None
+                                               for f in ("pv", "meter", "residual")), n)
+            self.st = None
+            if args.mode == "stats":
+                self.hist = torch.zeros(4096, dtype=torch.int64, device=dev)
+                self.acc = torch.zeros(4, n, dtype=torch.float64, device=dev)
+                self.acc[3].fill_(-float("inf"))
+                self.st = _lib.Stats(self.hist.data_ptr(), 4096, 0, -300.0, 9000.0, self.acc.data_ptr())
+
+    ctxs = [Ctx() for _ in range(max(1, args.pipeline))]
+    torch.cuda.synchronize()
     L.tmh_profile_enable(sim._eng, 1)
 
     def one_step(k):
+        cx = ctxs[k % len(ctxs)]
         chain0 = (rank + k * world) * n                    # fresh global chains every batch
-        _lib.check(L.tmh_plan(sim._eng, 0, secs, C.c_void_p(plan.data_ptr()), sptr))
-        _lib.check(L.tmh_init(sim._eng, C.c_void_p(sim.state.data_ptr()), chain0, n, None, sptr))
-        _lib.check(L.tmh_step(sim._eng, C.c_void_p(sim.state.data_ptr()), chain0, n, 0, secs, None,
-                              C.byref(tr), C.byref(st) if st is not None else None,
-                              C.c_void_p(plan.data_ptr()), C.c_void_p(scratch.data_ptr()), scratch.numel(), sptr))
-        if args.mode == "stats":                           # the one exchange step: RCCL all-reduce
-            totals[0] = all_reduce_stats(sim.stats_totals())
+        _lib.check(L.tmh_plan(sim._eng, 0, secs, C.c_void_p(cx.plan.data_ptr()), cx.sptr))
+        _lib.check(L.tmh_init(sim._eng, C.c_void_p(cx.state.data_ptr()), chain0, n, None, cx.sptr))
+        _lib.check(L.tmh_step(sim._eng, C.c_void_p(cx.state.data_ptr()), chain0, n, 0, secs, None,
+                              C.byref(cx.tr), C.byref(cx.st) if cx.st is not None else None,
+                              C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()), cx.scratch.numel(),
+                              cx.sptr))
+
+    def exchange():
+        """stats mode: the one cross-GPU step, an RCCL all-reduce of the aggregate statistics"""
+        for cx in ctxs:
+            cx.stream.synchronize()
+        hist = sum(cx.hist for cx in ctxs)
+        acc = torch.stack([cx.acc for cx in ctxs])
+        tot = dict(energy_pv=acc[:, 0].sum(), energy_meter=acc[:, 1].sum(), energy_residual=acc[:, 2].sum(),
+                   peak_residual=acc[:, 3].max(), hist=hist)
+        return all_reduce_stats(tot)
 
     for k in range(args.warmup):
         one_step(k)
+    if args.mode == "stats":
+        exchange()                                         # loads torch's reduction kernels outside the timing
+        for cx in ctxs:
+            cx.hist.zero_()
+            cx.acc[:3].zero_()
+            cx.acc[3].fill_(-float("inf"))
     torch.cuda.synchronize()
-    for kk in (_lib.K_EXPAND, _lib.K_SEGMENTS, _lib.K_MINUTE_DRAWS, _lib.K_STEP):
+    for kk in (_lib.K_EXPAND, _lib.K_SEGMENTS, _lib.K_CANDIDATES, _lib.K_STEP):
         _lib.profile_read(sim._eng, kk)                    # drop the warmup launches
     if world > 1:
         dist.barrier()
@@ -145,6 +172,8 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.warmup, args.warmup + args.steps):
         one_step(k)
+    if args.mode == "stats":
+        exchange()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -152,10 +181,13 @@ def main():
     elapsed = time.perf_counter() - t0
     phases = {}
     for name, kk in (("expand", _lib.K_EXPAND), ("segments", _lib.K_SEGMENTS),
-                     ("minute_draws", _lib.K_MINUTE_DRAWS), ("tmh_step", _lib.K_STEP)):
+                     ("candidates", _lib.K_CANDIDATES), ("tmh_step", _lib.K_STEP)):
         ms, cnt = _lib.profile_read(sim._eng, kk)
         phases[name] = ms / cnt if cnt else None
-    bad = int((sim.status() != 0).sum())
+    bad = 0
+    for cx in ctxs:
+        sim.state = cx.state
+        bad += int((sim.status() != 0).sum())
     kmean = phases["expand"] if phases["expand"] else float("nan")
     if world > 1:
         t = torch.tensor([elapsed, kmean], device=dev, dtype=torch.float64)
@@ -171,7 +203,8 @@ def main():
         "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic (keyed Philox)",
         "config": {"workload": f"C2: {n} chains/GPU x {secs} s at 1 s, Munich, Europe/Berlin, "
                                f"{args.start[:10]}, {args.mode} mode ({'meter+pv+residual fp32 trace' if args.mode == 'trace' else 'on-GPU stats'})",
-                   "chains_per_gpu": n, "seconds": secs, "parallelism": f"chains sharded over {world} GPU(s)"},
+                   "chains_per_gpu": n, "seconds": secs, "parallelism": f"chains sharded over {world} GPU(s)",
+                   "batches_in_flight": len(ctxs)},
         "roofline": ({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": achieved / HBM_PEAK_GBS, "traffic": traffic(args, n, secs),
                       "kernel": "expand_kernel (P2, " + sim.path + ")", "kernel_ms": kmean,

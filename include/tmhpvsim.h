@@ -188,8 +188,9 @@ int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
  * time-parallel path; tmh_profile_read waits for them and returns the summed
  * milliseconds and launch count of one kernel since the last read, then resets
  * it.  kernel: TMH_K_EXPAND (P2 trace/stats expansion), TMH_K_SEGMENTS (P1
- * segment walk), TMH_K_MINUTE_DRAWS, TMH_K_STEP (the whole tmh_step). */
-enum { TMH_K_EXPAND = 0, TMH_K_SEGMENTS = 1, TMH_K_MINUTE_DRAWS = 2, TMH_K_STEP = 3, TMH_K_COUNT = 4 };
+ * segment walk), TMH_K_CANDIDATES (P1's candidate table), TMH_K_STEP (the
+ * whole tmh_step). */
+enum { TMH_K_EXPAND = 0, TMH_K_SEGMENTS = 1, TMH_K_CANDIDATES = 2, TMH_K_STEP = 3, TMH_K_COUNT = 4 };
 int tmh_profile_enable(struct tmh_engine* eng, int on);
 int tmh_profile_read(struct tmh_engine* eng, int kernel, double* total_ms, int* launches);
 

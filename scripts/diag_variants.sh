@@ -5,7 +5,7 @@
 set -u
 ROOT="${GRAFT_REPO_ROOT:-/root/repo}"
 cd "$ROOT"
-VARIANTS="base:- norng:-DTMH_DIAG_NO_RNG nondtri:-DTMH_DIAG_NO_NDTRI nopv:-DTMH_DIAG_NO_PV nostore:-DTMH_DIAG_NO_STORE"
+VARIANTS="${VARIANTS:-base:- norng:-DTMH_DIAG_NO_RNG nondtri:-DTMH_DIAG_NO_NDTRI nopv:-DTMH_DIAG_NO_PV nostore:-DTMH_DIAG_NO_STORE}"
 if [ "${1:-run}" = build ]; then
   for v in $VARIANTS; do
     name=${v%%:*}; flag=${v#*:}; [ "$flag" = "-" ] && flag=""

@@ -63,7 +63,7 @@ class Stats(C.Structure):
 EXPORTS = ["tmh_abi_version", "tmh_last_error", "tmh_state_bytes", "tmh_state_offsets", "tmh_plan_bytes",
            "tmh_scratch_bytes", "tmh_workspace_bytes", "tmh_engine_create", "tmh_engine_destroy", "tmh_engine_path",
            "tmh_init", "tmh_run", "tmh_plan", "tmh_step", "tmh_probe", "tmh_profile_enable", "tmh_profile_read"]
-K_EXPAND, K_SEGMENTS, K_MINUTE_DRAWS, K_STEP = 0, 1, 2, 3
+K_EXPAND, K_SEGMENTS, K_CANDIDATES, K_STEP = 0, 1, 2, 3
 
 _lib = None
 

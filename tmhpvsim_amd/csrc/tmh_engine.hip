@@ -50,7 +50,7 @@ struct BlockDesc {                 // as of the step before the block start; -1 
     int32_t h0, h1;                // event indices of the last two hour boundaries
     int32_t cd0, cd1;              // last two clear_day pushes: event index * 2 + (0 day | 1 hour push)
     int32_t evi;                   // first event index at or after the block start
-    int32_t pad;
+    int32_t h2;                    // event index of the third-last hour boundary
 };
 
 struct SegView {                   // P1 -> P2 scratch
@@ -64,8 +64,9 @@ struct SegView {                   // P1 -> P2 scratch
     double* part;                  // [4][nblk][n] stats partials
     uint32_t nblk;
     double* evd;                   // [ev_cap][4][n] per boundary event: cc, ws, clear_day (day), clear_day (hour)
-    double* mind;                  // [nmin][2][n] per minute boundary: cloudy noise, clear noise
-    uint32_t evcap, nmin;
+    uint32_t evcap;
+    double* cand;                  // [kcap][n] try-0 cloud lengths (before / ws) of the window's next kcap calls
+    uint32_t kcap;
 };
 
 // ------------------------------------------------------------ state I/O
@@ -301,10 +302,11 @@ __global__ __launch_bounds__(1024) void events_kernel(const float* __restrict__ 
 
 __device__ __forceinline__ uint32_t ev_cap_dev(uint32_t n_steps) { return n_steps / 1800 + 64; }
 
-__device__ __forceinline__ int64_t first_minute(int64_t utc0, int64_t W0)
+__host__ __device__ __forceinline__ int64_t first_minute(int64_t utc0, int64_t W0)
 {   // window-relative step of the first candidate minute boundary (UTC second 0)
     return (60 - (((utc0 + W0) % 60) + 60) % 60) % 60;
 }
+inline int64_t first_minute_host(int64_t utc0, int64_t W0) { return first_minute(utc0, W0); }
 
 // Descriptor of the sampler state after step W0 + min(b * BLOCK_STEPS, n) - 1,
 // for b = 0 .. nblk (the last one describes the window end).
@@ -315,7 +317,7 @@ __global__ __launch_bounds__(256) void desc_kernel(int64_t step0, uint32_t n, in
 {
     const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b > nblk) return;
-    BlockDesc d{-1, -1, -1, -1, -1, -1, 0, 0};
+    BlockDesc d{-1, -1, -1, -1, -1, -1, 0, -1};
     const int64_t jb = min((int64_t)b * BLOCK_STEPS, (int64_t)n);
     if (jb > 0) {
         const int64_t p = step0 + jb - 1;                  // last step before the block
@@ -333,11 +335,12 @@ __global__ __launch_bounds__(256) void desc_kernel(int64_t step0, uint32_t n, in
         }
         d.evi = a;
         int nh = 0, ncd = 0;
-        for (int i = a - 1; i >= 0 && (nh < 2 || ncd < 2); --i) {
+        for (int i = a - 1; i >= 0 && (nh < 3 || ncd < 2); --i) {
             const int fl = events[i].y;
             if (fl & FL_HOUR) {
                 if (nh == 0) d.h0 = i;
                 else if (nh == 1) d.h1 = i;
+                else if (nh == 2) d.h2 = i;
                 ++nh;
                 if (ncd < 2) {            // the hour push of clear_day follows its day push
                     if (ncd == 0) d.cd0 = 2 * i + 1;
@@ -380,50 +383,30 @@ __global__ __launch_bounds__(256) void event_draws_kernel(DrawParams dp, uint64_
 }
 
 // _next_min draws of every (minute boundary, chain): clearskyindexmodel.py:86-95,109-111
-__global__ __launch_bounds__(256) void minute_draws_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
-                                                           int64_t W0, uint32_t nsteps, int64_t utc0,
-                                                           const double* __restrict__ tab64,
-                                                           const int2* __restrict__ events,
-                                                           const uint32_t* __restrict__ n_events,
-                                                           const double* __restrict__ evd, double* mind)
+// the two _next_min draws of the minute boundary at window step j (keyed by step)
+template <typename R>
+__device__ __forceinline__ void minute_draws(const DrawParams& dp, uint64_t chain, int64_t step, double cc,
+                                             double& cloudy, double& clear)
 {
-    const uint32_t c = blockIdx.y * blockDim.x + threadIdx.x;
-    const uint32_t q = blockIdx.x;
-    const int64_t j = first_minute(utc0, W0) + 60 * (int64_t)q;
-    if (c >= n || j >= (int64_t)nsteps) return;
-    const int64_t step = W0 + j;
-    const int ne = (int)min(*n_events, ev_cap_dev(nsteps));
-    int a = 0, z = ne;   // last event <= step
-    while (a < z) {
-        const int mid = (a + z) / 2;
-        if (events[mid].x <= step) a = mid + 1;
-        else z = mid;
-    }
-    int h0 = -1, h1 = -1;
-    for (int i = a - 1; i >= 0 && h1 < 0; --i)
-        if (events[i].y & FL_HOUR) {
-            if (h0 < 0) h0 = i;
-            else h1 = i;
-        }
-    double pb, pa;   // cloud cover pair after the hour push of this second
-    if (h0 < 0) {
-        pb = st.sb[S_CC][c];
-        pa = st.sa[S_CC][c];
-    } else if (h1 < 0) {
-        pb = st.sa[S_CC][c];
-        pa = evd[(size_t)h0 * 4 * n + c];
-    } else {
-        pb = evd[(size_t)h1 * 4 * n + c];
-        pa = evd[(size_t)h0 * 4 * n + c];
-    }
-    const double cc = interp(pb, pa, tab64[(size_t)j * ROW + G_HOURF]);
-    const U4 u = keyed_block(dp.seed, chain0 + c, (uint64_t)step, TAG_BOUNDARY, 2);
-    mind[(size_t)q * 2 * n + c] = normal(u52(u.x, u.y), 1.0, dp.sqrt09 * (0.01 + 0.003 * 8 * cc));
-    mind[((size_t)q * 2 + 1) * n + c] = normal(u52(u.z, u.w), 1.0, dp.sqrt09 * (0.001 + 0.0015 * 8 * cc));
+    const U4 u = keyed_block(dp.seed, chain, (uint64_t)step, TAG_BOUNDARY, 2);
+    cloudy = minute_noise<R>(u52(u.x, u.y), 0.01, 0.003, cc, dp.sqrt09);
+    clear = minute_noise<R>(u52(u.z, u.w), 0.001, 0.0015, cc, dp.sqrt09);
 }
 
 // cc / clear_day / noise pairs described by `d`, from the draw tables (start = window start)
-__device__ __forceinline__ void samplers_at(const BlockDesc& d, const SegView& sg, uint32_t n, uint32_t c, Samp& s)
+// what the minute draws of a block start / window end need
+struct MinuteCtx {
+    DrawParams dp;
+    uint64_t chain;
+    int64_t W0, fm;
+    const int2* events;
+    int ne;
+    const double* tab64;
+};
+
+template <typename R>
+__device__ __forceinline__ void samplers_at(const BlockDesc& d, const SegView& sg, uint32_t n, uint32_t c, Samp& s,
+                                            const MinuteCtx& mc, const StateView& st)
 {
     const double* evd = sg.evd;
     if (d.h0 >= 0) {
@@ -437,13 +420,36 @@ __device__ __forceinline__ void samplers_at(const BlockDesc& d, const SegView& s
         s.b[S_CLEAR_DAY] = d.cd1 >= 0 ? cdv(d.cd1) : s.a[S_CLEAR_DAY];
         s.a[S_CLEAR_DAY] = na;
     }
-    if (d.q0 >= 0) {
-        for (int k = 0; k < 2; ++k) {
-            const int si = k == 0 ? S_CLOUDY_NOISE : S_CLEAR_NOISE;
-            const double na = sg.mind[((size_t)d.q0 * 2 + k) * n + c];
-            s.b[si] = d.q1 >= 0 ? sg.mind[((size_t)d.q1 * 2 + k) * n + c] : s.a[si];
-            s.a[si] = na;
+    if (d.q0 >= 0) {   // the last two minute boundaries: draws recomputed from their keys
+        // cloud-cover pair in force at a minute boundary: hour events sit on minute
+        // boundaries, so at q0 it is the pair of the block start; at q1 it is the
+        // one before h0 when h0 happened at q0
+        const double cc_st_b = st.sb[S_CC][c], cc_st_a = st.sa[S_CC][c];
+        auto hour_val = [&](int32_t h, double fallback) { return h >= 0 ? evd[(size_t)h * 4 * n + c] : fallback; };
+        auto draw_q = [&](int32_t q, bool before_h0, double& cloudy, double& clear) {
+            const int64_t jq = mc.fm + 60 * (int64_t)q;
+            double pb, pa;
+            if (!before_h0 || d.h0 < 0) {       // pair after h0 (or the window-start pair)
+                pa = hour_val(d.h0, cc_st_a);
+                pb = d.h0 < 0 ? cc_st_b : hour_val(d.h1, cc_st_a);
+            } else {                            // pair after h1
+                pa = hour_val(d.h1, cc_st_a);
+                pb = d.h1 < 0 ? cc_st_b : hour_val(d.h2, cc_st_a);
+            }
+            const double cc = interp(pb, pa, mc.tab64[(size_t)jq * ROW + G_HOURF]);
+            minute_draws<R>(mc.dp, mc.chain, mc.W0 + jq, cc, cloudy, clear);
+        };
+        double ca, la;
+        draw_q(d.q0, false, ca, la);
+        if (d.q1 >= 0) {
+            const bool h0_at_q0 = d.h0 >= 0 && (int64_t)mc.events[d.h0].x == mc.W0 + mc.fm + 60 * (int64_t)d.q0;
+            draw_q(d.q1, h0_at_q0, s.b[S_CLOUDY_NOISE], s.b[S_CLEAR_NOISE]);
+        } else {
+            s.b[S_CLOUDY_NOISE] = s.a[S_CLOUDY_NOISE];
+            s.b[S_CLEAR_NOISE] = s.a[S_CLEAR_NOISE];
         }
+        s.a[S_CLOUDY_NOISE] = ca;
+        s.a[S_CLEAR_NOISE] = la;
     }
 }
 
@@ -508,8 +514,8 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
                 if (fl & FL_MIN) {                     // _next_min
                     dr.two(ch, step, TAG_BOUNDARY, 2, u0, u1);
                     const double cc = interp(ch.s.b[S_CC], ch.s.a[S_CC], hf);
-                    push(ch.s, S_CLOUDY_NOISE, scaled_noise(kp, u0, 0.01, 0.003, cc));
-                    push(ch.s, S_CLEAR_NOISE, scaled_noise(kp, u1, 0.001, 0.0015, cc));
+                    push(ch.s, S_CLOUDY_NOISE, minute_noise<R>(u0, 0.01, 0.003, cc, kp.sqrt09));
+                    push(ch.s, S_CLEAR_NOISE, minute_noise<R>(u1, 0.001, 0.0015, cc, kp.sqrt09));
                 }
                 to_real(fs, ch.s);
             }
@@ -557,15 +563,11 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
 }
 
 // ------------------------------------------------------------ P1: segments
-// One wavefront per chain (keyed, faithful): jump from segment end to segment
-// end.  The chain's sigma arrays stay in VGPRs (64 lanes x NCH chunks) for the
-// whole window; hour/day fractions come from clock arithmetic (scalar).
 // hour / day fractions of step s (clearskyindexmodel.py:114-116) from the window's
-// local second-of-day at W0: 32-bit, wave-uniform arithmetic
+// local second-of-day at W0: 32-bit arithmetic, shift table in registers
 struct WinClock {
-    int32_t sod0;            // local second of day at W0
-    int32_t n;               // shifts inside the window
-    int32_t step[8], delta[8];   // window-relative shift steps and sizes
+    int32_t sod0;                 // local second of day at W0
+    int32_t step[8], delta[8];    // window-relative shift steps (INT_MAX = unused) and sizes
 };
 
 __device__ __forceinline__ WinClock win_clock(const tmh_clock& ck, int64_t W0)
@@ -573,20 +575,20 @@ __device__ __forceinline__ WinClock win_clock(const tmh_clock& ck, int64_t W0)
     WinClock w;
     const int64_t l0 = local_at(ck, W0);
     w.sod0 = (int32_t)(l0 - floordiv(l0, 86400) * 86400);
-    w.n = 0;
-    for (int i = 0; i < ck.n_shifts && i < 8; ++i)
-        if (ck.shift_step[i] > W0) {
-            w.step[w.n] = (int32_t)(ck.shift_step[i] - W0);
-            w.delta[w.n] = ck.shift_delta[i];
-            ++w.n;
-        }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const bool use = i < ck.n_shifts && ck.shift_step[i] > W0;
+        w.step[i] = use ? (int32_t)(ck.shift_step[i] - W0) : INT_MAX;
+        w.delta[i] = use ? ck.shift_delta[i] : 0;
+    }
     return w;
 }
 
 __device__ __forceinline__ void fractions_at(const WinClock& w, int32_t j, double& hour_f, double& day_f)
 {
     int32_t sod = w.sod0 + j;
-    for (int i = 0; i < w.n; ++i)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
         if (j >= w.step[i]) sod += w.delta[i];
     sod %= 86400;
     if (sod < 0) sod += 86400;
@@ -595,125 +597,383 @@ __device__ __forceinline__ void fractions_at(const WinClock& w, int32_t j, doubl
     clock_fractions(hour, minute, second, min_f, hour_f, day_f);
 }
 
-__global__ __launch_bounds__(256) void segments_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
-                                                       int64_t W0, uint32_t nsteps, tmh_clock ck,
-                                                       const int2* __restrict__ events,
-                                                       const uint32_t* __restrict__ n_events, SegView sg)
+// try-0 candidate lengths of the next kcap next_cloud calls of every chain:
+// keyed by (chain, call number) only, so they are drawn before the walk, at
+// full occupancy, instead of one wave-redundant Philox + pow per call inside it
+__global__ __launch_bounds__(256) void candidates_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
+                                                         SegView sg)
 {
-    const int lane = threadIdx.x & 63;
-    const uint32_t c = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    if (c >= n) return;   // whole wave
-    const uint64_t chain = chain0 + c;
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t k = blockIdx.y;
+    if (c >= n || st.status[c] != 0) return;
+    const U4 b = keyed_block(dp.seed, chain0 + c, (uint64_t)(st.ncalls[c] + k), TAG_CLOUD, 0);
+    sg.cand[(size_t)k * n + c] = pow_d(dp.alpha + dp.delta * u52(b.x, b.y), dp.expo);
+}
+
+#ifdef TMH_DIAG_P1
+__device__ uint64_t g_p1diag[65536 * 8];
+#endif
+
+// ---- 16-lane row primitives (DPP inside each row of 16 lanes: one chain per row)
+template <int CTRL>
+__device__ __forceinline__ double dpp_row_f64(double old, double v)
+{
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(old), __double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double row_min_f64(double v)
+{
+    v = fmin(v, dpp_row_f64<0xB1>(v, v));    // quad_perm [1,0,3,2]
+    v = fmin(v, dpp_row_f64<0x4E>(v, v));    // quad_perm [2,3,0,1]
+    v = fmin(v, dpp_row_f64<0x141>(v, v));   // row_half_mirror
+    v = fmin(v, dpp_row_f64<0x140>(v, v));   // row_mirror
+    return v;
+}
+
+__device__ __forceinline__ int row_min_i32(int v)
+{
+    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false));
+    return v;
+}
+
+// max over the four rows of a row-uniform value (wave-uniform result, SGPR)
+__device__ __forceinline__ int rows_max(int v)
+{
+    const int a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+    const int c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+    return max(max(a, b), max(c, d));
+}
+
+__device__ __forceinline__ double bperm_f64(int src_lane, double v)
+{
+    const int lo = __builtin_amdgcn_ds_bpermute(src_lane << 2, __double2loint(v));
+    const int hi = __builtin_amdgcn_ds_bpermute(src_lane << 2, __double2hiint(v));
+    return __hiloint2double(hi, lo);
+}
+
+constexpr int RCH = 8;         // register chunks of 16 entries: sigma entries 0..127 (all but ~1e-5 of calls)
+constexpr int RCH_FIXED = 4;   // chunks always processed (L <= 64 for 99.7 % of calls)
+
+// P1: segment walk.  Four chains per wavefront, one per row of 16 lanes; entry
+// k of a chain's sigma arrays lives in chunk k / 16, lane k % 16 of its row
+// (entries 128.. stay in the chain's global sigma row).  Each loop iteration
+// is one CloudCoverBinary.next_cloud call (cloud_cover_binary.py:80-107) of
+// every row that still has a call inside the window; the per-call scalar work
+// (clock fractions, update_parameters, the two divisions) is shared by four
+// chains, the argmin is a DPP row reduction with np.argmin's first-index rule,
+// the r_[cl, nsc[:last+1]] shift is row_shr:1 / row_ror:1.  Output per chain:
+// segment records (first uncovered step, next call step) and the window-end
+// binary state.
+__global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
+                                                          int64_t W0, uint32_t nsteps, tmh_clock ck,
+                                                          const int2* __restrict__ events,
+                                                          const uint32_t* __restrict__ n_events, SegView sg)
+{
+    const int lane = threadIdx.x & 63, p = lane & 15, row0 = lane & ~15;
+    const uint32_t c = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    const bool live = c < n;
+    const uint32_t cs = live ? c : 0;
+    const uint64_t chain = chain0 + cs;
     const int64_t W1 = W0 + nsteps;
-    uint32_t status = st.status[c];
-    double ccb = st.sb[S_CC][c], cca = st.sa[S_CC][c], wsb = st.sb[S_WS][c], wsa = st.sa[S_WS][c];
+    uint32_t status = live ? st.status[cs] : 0xFFFFFFFFu;
+    double ccb = st.sb[S_CC][cs], cca = st.sa[S_CC][cs], wsb = st.sb[S_WS][cs], wsa = st.sa[S_WS][cs];
     int32_t fault = INT_MAX;
     uint32_t nrec = 0;
+    double cl = st.cl[cs], clr = st.clr[cs];
+    int L = st.L[cs];
+    const int32_t sec0 = st.sec[cs];
+    double* gsc = sig_c(st, cs);
+    double* gsl = sig_l(st, cs);
+    double vc[RCH], vl[RCH];
+#pragma unroll
+    for (int ch = 0; ch < RCH; ++ch) {
+        const int k = ch * 16 + p;
+        vc[ch] = k < L ? gsc[k] : 0.0;
+        vl[ch] = k < L ? gsl[k] : 0.0;
+    }
+    int64_t s_start = W0 - sec0;   // step at which sec was 1
+    int64_t e = s_start + ceil_thr(cl + clr) - 1;
+    // No global load or store sits on the per-call path: records, boundary
+    // events and candidates move through 16-entry lane-distributed buffers
+    // (lane p of a row = entry p), flushed / refilled once per 16 uses, and
+    // are read back with ds_bpermute.  (A per-call load behind a per-call
+    // store makes every call wait for the store's round trip: vmcnt counts both.)
+    int2* rec = sg.rec + (size_t)cs * sg.cap;
+    int rb_x = 0, rb_y = 0;       // record buffer: lane p = record rbase + p
+    uint32_t rbase = 0;
+    auto put_rec = [&](uint32_t i, int x, int y) {
+        const uint32_t slot = i - rbase;
+        const bool mine = (uint32_t)p == slot;
+        rb_x = mine ? x : rb_x;
+        rb_y = mine ? y : rb_y;
+        if (slot == 15) {
+            rec[rbase + p] = make_int2(rb_x, rb_y);
+            rbase += 16;
+        }
+    };
+    put_rec(0, (int)(s_start + ceil_thr(cl) - 1), (int)e);
+    nrec = 1;
+    const uint32_t nev = min(*n_events, ev_cap_dev(nsteps));
+    uint32_t ev = 0, evb = 0;
+    int eb_step = INT_MAX, eb_fl = 0;   // event buffer: lane p = event evb + p
+    double eb_cc = 0.0, eb_ws = 0.0;
+    auto load_events = [&]() {
+        const uint32_t i = evb + p;
+        eb_step = INT_MAX;
+        if (i < nev) {
+            const int2 r = events[i];
+            eb_step = r.x;
+            eb_fl = r.y;
+            eb_cc = sg.evd[(size_t)i * 4 * n + cs];
+            eb_ws = sg.evd[((size_t)i * 4 + 1) * n + cs];
+        }
+    };
+    load_events();
+    int64_t next_ev = INT64_MAX;
+    int ev_fl = 0;
+    double ev_cc = 0.0, ev_ws = 0.0;
+    auto fetch_event = [&]() {   // event `ev` out of the buffer
+        if (ev - evb >= 16) {
+            evb = ev;
+            load_events();
+        }
+        const int src = row0 | (int)(ev - evb);
+        const int es = __builtin_amdgcn_ds_bpermute(src << 2, eb_step);
+        next_ev = es == INT_MAX ? INT64_MAX : (int64_t)es;
+        ev_fl = __builtin_amdgcn_ds_bpermute(src << 2, eb_fl);
+        ev_cc = bperm_f64(src, eb_cc);
+        ev_ws = bperm_f64(src, eb_ws);
+    };
+    fetch_event();
+    const uint32_t ncall0 = st.ncalls[cs];
+    uint32_t ncall = ncall0;
+    auto cand_at = [&](uint32_t k) { return k < sg.kcap ? sg.cand[(size_t)k * n + cs] : -1.0; };
+    uint32_t kb = 0;                                     // candidate buffer: lane p = calls kb + p, kb + 16 + p
+    double cb_a = cand_at(p), cb_b = cand_at(16 + p);
+    const WinClock wck = win_clock(ck, W0);
+    bool active = live && status == 0;
+#ifdef TMH_DIAG_P1   // diagnostic build only: cycles per section of the walk (s_memtime)
+    uint64_t dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t dt = __builtin_amdgcn_s_memtime();
+#define DSTAMP(i)                                        \
+    {                                                    \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+        dg[i] += t_ - dt;                                \
+        dt = t_;                                         \
+    }
+#else
+#define DSTAMP(i)
+#endif
+    for (;;) {
+        const bool run = active && e < W1;
+        if (__builtin_amdgcn_ballot_w64(run) == 0) break;
+        // wave-uniform chunk bound: the loops over register chunks branch on SGPRs only
+        const int Lmax = rows_max(run ? L : 0);
+#ifdef TMH_DIAG_P1
+        dg[7] += 1;
+#endif
+        if (!run) continue;
+        DSTAMP(6)
+        while (next_ev <= e) {   // _next_day / _next_hour at steps <= e
+            if (ev_fl & FL_DAY) {
+                wsb = wsa;
+                wsa = ev_ws;
+            }
+            if (ev_fl & FL_HOUR) {
+                ccb = cca;
+                cca = ev_cc;
+            }
+            ++ev;
+            fetch_event();
+        }
+        double hf, df;
+        fractions_at(wck, (int32_t)(e - W0), hf, df);
+        DSTAMP(0)
+        const double hh = interp(ccb, cca, hf);
+        const double h = 0.95 < hh ? 0.95 : hh;   // update_parameters
+        const double ws = interp(wsb, wsa, df);
+        const double f = 1.0 / h - 1.0;
+        const uint32_t rel = ncall - ncall0;
+        if (rel - kb >= 32) {   // refill once per 32 calls (its latency is exposed once)
+            kb += 32;
+            cb_a = cand_at(kb + p);
+            cb_b = cand_at(kb + 16 + p);
+        }
+        const uint32_t slot = rel - kb;
+        const double x0 = bperm_f64(row0 | (int)(slot & 15), slot < 16 ? cb_a : cb_b);
+        DSTAMP(1)
+        // ---- next_cloud: tries (cloud_cover_binary.py:82-98)
+        int tries = 0, last = -1;
+        double ncl = 0.0;
+        for (;;) {
+            double x;
+            if (tries == 0 && x0 >= 0.0) x = x0;
+            else x = pow_d(dp.alpha + dp.delta * keyed_u(dp.seed, chain, ncall, TAG_CLOUD, (uint32_t)(tries >> 1),
+                                                        tries & 1),
+                           dp.expo);
+            ncl = x / ws;
+            double bd = INFINITY;
+            int bk = INT_MAX;
+            auto scan = [&](int k, double sc, double sl) {   // :83-88, branch-free
+                const double nsc = ncl + sc;
+                const double nsl = f * nsc;
+                const double tot = nsc + nsl;
+                const bool ok = (k < L) & (nsl - sl > 0.0) & (tot < 5400.0);
+                const double d = ok ? fabs(tot - 3600.0) : INFINITY;
+                const bool take = d < bd;   // ascending k: ties keep the lower k
+                bd = take ? d : bd;
+                bk = take ? k : bk;
+            };
+            // chunks 0..3 straight-line (independent chains overlap: latency, not
+            // issue, bounds this loop); 4..7 only when some row has L > 64
+#pragma unroll
+            for (int ch = 0; ch < RCH_FIXED; ++ch) scan(ch * 16 + p, vc[ch], vl[ch]);
+            if (Lmax > 16 * RCH_FIXED) {
+#pragma unroll
+                for (int ch = RCH_FIXED; ch < RCH; ++ch) scan(ch * 16 + p, vc[ch], vl[ch]);
+            }
+            for (int ch = RCH; ch * 16 < L; ++ch) {   // rare: entries 128..
+                const int k = ch * 16 + p;
+                if (k < L) scan(k, gsc[k], gsl[k]);
+            }
+            const double dmin = row_min_f64(bd);
+            if (dmin < INFINITY) {
+                last = row_min_i32(bd == dmin ? bk : INT_MAX);
+                break;
+            }
+            ++tries;
+            if (tries == 20) {   // reset_sigma (cloud_cover_binary.py:76-78); 300 (k+1) is exact
+                const int nl = (int)(h * 12);
+                vc[0] = 300.0 * (p + 1);
+                vl[0] = f * vc[0];
+                L = nl;
+            }
+            if (tries == 40) break;
+        }
+        ++ncall;
+        DSTAMP(2)
+        if (last < 0) {   // assert not recurse (:91)
+            status = TMH_CHAIN_ASSERT_BINARY;
+            fault = (int32_t)(e - W0);
+            active = false;
+            continue;
+        }
+        if (last + 2 > CAP) {
+            status = TMH_CHAIN_SIGMA_OVERFLOW;
+            fault = (int32_t)(e - W0);
+            active = false;
+            continue;
+        }
+        DSTAMP(3)
+        // sigma_cloud = r_[cl, nsc[:last+1]], sigma_clear = r_[clr, nsl[:last+1]] (:101-105)
+        const int lc = last >> 4, src = row0 | (last & 15);
+        const int top = (last + 1) >> 4;   // highest chunk written
+        const int topmax = rows_max(top);
+        double sc_last = 0.0, sl_last = 0.0;
+        {   // select chunk lc in registers first (one bpermute pair instead of one per chunk)
+            double a = vc[0], b = vl[0];
+#pragma unroll
+            for (int ch = 1; ch < RCH_FIXED; ++ch) {
+                a = lc == ch ? vc[ch] : a;
+                b = lc == ch ? vl[ch] : b;
+            }
+            if (topmax >= RCH_FIXED) {
+#pragma unroll
+                for (int ch = RCH_FIXED; ch < RCH; ++ch) {
+                    a = lc == ch ? vc[ch] : a;
+                    b = lc == ch ? vl[ch] : b;
+                }
+            }
+            sc_last = bperm_f64(src, a);
+            sl_last = bperm_f64(src, b);
+        }
+        if (lc >= RCH) {
+            sc_last = gsc[last];
+            sl_last = gsl[last];
+        }
+        const double nclr = f * (ncl + sc_last) - sl_last;
+        for (int ch = top; ch >= RCH; --ch) {   // rare, descending: reads before writes
+            const int k = ch * 16 + p;
+            const double prev = (ch == RCH && p == 0) ? dpp_row_f64<0x121>(0.0, vc[RCH - 1]) : gsc[k - 1];
+            const double nsc = ncl + prev;
+            gsc[k] = nsc;
+            gsl[k] = f * nsc;
+        }
+        // rows with a lower top rewrite entries >= their new L: harmless
+        if (topmax >= RCH_FIXED) {
+#pragma unroll
+            for (int ch = RCH - 1; ch >= RCH_FIXED; --ch) {
+                const double sh = dpp_row_f64<0x111>(0.0, vc[ch]);
+                const double carry = dpp_row_f64<0x121>(0.0, vc[ch - 1]);
+                const double prev = p == 0 ? carry : sh;
+                const double nsc = ncl + prev;
+                vc[ch] = nsc;
+                vl[ch] = f * nsc;
+            }
+        }
+#pragma unroll
+        for (int ch = RCH_FIXED - 1; ch >= 0; --ch) {
+            {
+                const double sh = dpp_row_f64<0x111>(0.0, vc[ch]);                       // row_shr:1
+                const double carry = ch > 0 ? dpp_row_f64<0x121>(0.0, vc[ch > 0 ? ch - 1 : 0]) : 0.0;   // row_ror:1
+                const double prev = p == 0 ? carry : sh;
+                const double nsc = ncl + prev;
+                const bool first = ch == 0 && p == 0;
+                vc[ch] = first ? ncl : nsc;
+                vl[ch] = first ? nclr : f * nsc;
+            }
+        }
+        DSTAMP(4)
+        L = last + 2;
+        cl = ncl;
+        clr = nclr;
+        s_start = e;
+        e = s_start + ceil_thr(cl + clr) - 1;
+        if (nrec >= sg.cap) {
+            status = TMH_CHAIN_SEGMENT_OVERFLOW;
+            fault = (int32_t)(s_start - W0);
+            active = false;
+            continue;
+        }
+        put_rec(nrec, (int)(s_start + ceil_thr(cl) - 1), (int)e);
+        ++nrec;
+        DSTAMP(5)
+    }
+#ifdef TMH_DIAG_P1
+    if (lane == 0) {
+        const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+        for (int i = 0; i < 8; ++i) g_p1diag[w * 8 + i] = dg[i];
+    }
+#endif
+    if (live && (uint32_t)p < nrec - rbase) rec[rbase + p] = make_int2(rb_x, rb_y);   // partial record group
+    if (!live) return;
     if (status == 0) {
-        double cl = st.cl[c], clr = st.clr[c];
-        int L = st.L[c];
-        const int32_t sec = st.sec[c];
-        double vc[NCH], vl[NCH];
-        double* gsc = sig_c(st, c);
-        double* gsl = sig_l(st, c);
-#pragma unroll
-        for (int ch = 0; ch < NCH; ++ch) {
-            const int k = ch * 64 + lane;
-            vc[ch] = k < L ? gsc[k] : 0.0;
-            vl[ch] = k < L ? gsl[k] : 0.0;
+        while (next_ev <= W1 - 1) {   // remaining boundaries of the window
+            if (ev_fl & FL_DAY) {
+                wsb = wsa;
+                wsa = ev_ws;
+            }
+            if (ev_fl & FL_HOUR) {
+                ccb = cca;
+                cca = ev_cc;
+            }
+            ++ev;
+            fetch_event();
         }
-        int64_t s_start = W0 - sec;   // step at which sec was 1
-        int32_t t1 = ceil_thr(cl), t2 = ceil_thr(cl + clr);
-        int64_t e = s_start + t2 - 1;
-        int2* rec = sg.rec + (size_t)c * sg.cap;
-        if (lane == 0) rec[0] = make_int2((int)(s_start + t1 - 1), (int)e);
-        nrec = 1;
-        const uint32_t nev = min(*n_events, ev_cap_dev(nsteps));
-        uint32_t ev = 0;
-        // the next boundary event and its draws, loaded one event ahead of use
-        int64_t next_ev = INT64_MAX;
-        int ev_fl = 0;
-        double ev_cc = 0.0, ev_ws = 0.0;
-        auto fetch_event = [&]() {
-            if (ev < nev) {
-                const int2 r = events[ev];
-                next_ev = r.x;
-                ev_fl = r.y;
-                ev_cc = sg.evd[(size_t)ev * 4 * n + c];
-                ev_ws = sg.evd[((size_t)ev * 4 + 1) * n + c];
-            } else {
-                next_ev = INT64_MAX;
-            }
-        };
-        fetch_event();
-        auto apply_events = [&](int64_t upto) {   // _next_day / _next_hour at steps <= upto
-            while (next_ev <= upto) {
-                if (ev_fl & FL_DAY) {
-                    wsb = wsa;
-                    wsa = ev_ws;
-                }
-                if (ev_fl & FL_HOUR) {
-                    ccb = cca;
-                    cca = ev_cc;
-                }
-                ++ev;
-                fetch_event();
-            }
-        };
-        // try-0 candidates of the next 64 calls (keyed by call number, so they
-        // can be drawn before the calls' steps are known)
-        uint32_t ncall = st.ncalls[c], kb = ncall;
-        double cand_x, cand_u;
-        cloud_candidates(dp, chain, kb, lane, cand_x, cand_u);
-        const WinClock wck = win_clock(ck, W0);
-        while (e < W1) {
-            apply_events(e);
-            double hf, df;
-            fractions_at(wck, (int32_t)(e - W0), hf, df);
-            const double hh = interp(ccb, cca, hf);
-            const double h = 0.95 < hh ? 0.95 : hh;   // update_parameters
-            const double ws = interp(wsb, wsa, df);
-            if (ncall - kb >= 64u) {
-                kb = ncall;
-                cloud_candidates(dp, chain, kb, lane, cand_x, cand_u);
-            }
-            const int slot = (int)(ncall - kb);
-            const double x0 = readlane_f64(cand_x, slot);
-            double ncl = x0 / ws, nclr = 0.0;
-            uint32_t f = 0;
-            if (!next_cloud_fast(vc, vl, L, ncl, 1.0 / h - 1.0, lane, nclr))
-                f = next_cloud_regs(dp, vc, vl, gsc, gsl, L, h, ws, chain, ncall, x0, readlane_f64(cand_u, slot), lane,
-                                    ncl, nclr);
-            ++ncall;
-            if (f) {
-                status = f;
-                fault = (int32_t)(e - W0);
-                break;
-            }
-            cl = ncl;
-            clr = nclr;
-            t1 = ceil_thr(cl);
-            t2 = ceil_thr(cl + clr);
-            s_start = e;
-            e = s_start + t2 - 1;
-            if (nrec >= sg.cap) {
-                status = TMH_CHAIN_SEGMENT_OVERFLOW;
-                fault = (int32_t)(s_start - W0);
-                break;
-            }
-            if (lane == 0) rec[nrec] = make_int2((int)(s_start + t1 - 1), (int)e);
-            ++nrec;
-        }
-        if (status == 0) apply_events(W1 - 1);   // remaining boundaries of the window
 #pragma unroll
-        for (int ch = 0; ch < NCH; ++ch) {   // register chunks back to the state row
-            const int k = ch * 64 + lane;
+        for (int ch = 0; ch < RCH; ++ch) {   // register chunks back to the state row
+            const int k = ch * 16 + p;
             if (k < L) {
                 gsc[k] = vc[ch];
                 gsl[k] = vl[ch];
             }
         }
-        if (lane == 0) {
+        if (p == 0) {
             st.sec[c] = (int32_t)(W1 - s_start);   // sec after step W1 - 1
             st.cl[c] = cl;
             st.clr[c] = clr;
@@ -721,7 +981,7 @@ __global__ __launch_bounds__(256) void segments_kernel(DrawParams dp, StateView 
             st.ncalls[c] = ncall;
         }
     }
-    if (lane == 0) {
+    if (p == 0) {
         sg.count[c] = nrec;
         sg.fault[c] = fault;
         sg.status[c] = status;
@@ -737,10 +997,12 @@ __global__ __launch_bounds__(256) void segments_kernel(DrawParams dp, StateView 
 // from the draw tables, so the per-second loop holds only the R copies of the
 // sampler pairs and does no fp64 work in fp32 mode.
 template <typename R, int OUT>
-__global__ __launch_bounds__(256) void expand_kernel(KParams kp, StateView st, uint64_t chain0, uint32_t n,
-                                                     int64_t W0, uint32_t nsteps, int64_t utc0,
+__global__ __launch_bounds__(256) void expand_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0,
+                                                     uint32_t n, int64_t W0, uint32_t nsteps, int64_t utc0,
                                                      const double* __restrict__ tab64,
                                                      const float* __restrict__ tab32,
+                                                     const int2* __restrict__ events,
+                                                     const uint32_t* __restrict__ n_events,
                                                      const BlockDesc* __restrict__ desc, SegView sg, TraceView tr,
                                                      StatsView sv)
 {
@@ -762,6 +1024,8 @@ __global__ __launch_bounds__(256) void expand_kernel(KParams kp, StateView st, u
     const int2* rec = sg.rec + (size_t)(live ? c : 0) * sg.cap;
     uint32_t jr = 0, evi = 0;
     FSamp<R> fs;
+    double ccb = 0.0, cca = 0.0;   // fp64 cloud-cover pair: the scale of the minute draws
+    const MinuteCtx mc{dp, chain, W0, fm, events, (int)min(*n_events, ev_cap_dev(nsteps)), tab64};
     if (live) {
         alive = st.status[c] == 0;
         fault = sg.fault[c];
@@ -773,7 +1037,9 @@ __global__ __launch_bounds__(256) void expand_kernel(KParams kp, StateView st, u
         }
         const BlockDesc d = desc[b];
         evi = (uint32_t)d.evi;
-        if (alive && b > 0) samplers_at(d, sg, n, c, s);
+        if (alive && b > 0) samplers_at<R>(d, sg, n, c, s, mc, st);
+        ccb = s.b[S_CC];
+        cca = s.a[S_CC];
         to_real(fs, s);
     }
     if (alive) {   // segment containing the block start: first record with next-call step > start
@@ -788,7 +1054,6 @@ __global__ __launch_bounds__(256) void expand_kernel(KParams kp, StateView st, u
         seg = rec[jr];
     }
     const double* evd = sg.evd + c;
-    const double* mind = sg.mind + c;
     U4 pair{0, 0, 0, 0};
     bool have_pair = false;
     for (uint32_t j = j0; j < j1; ++j) {
@@ -809,18 +1074,21 @@ __global__ __launch_bounds__(256) void expand_kernel(KParams kp, StateView st, u
                     fs.a[S_CLEAR_DAY] = (R)evd[eo + 2 * (size_t)n];
                 }
                 if (fl & FL_HOUR) {
+                    ccb = cca;
+                    cca = evd[eo];
                     fs.b[S_CC] = fs.a[S_CC];
-                    fs.a[S_CC] = (R)evd[eo];
+                    fs.a[S_CC] = (R)cca;
                     fs.b[S_CLEAR_DAY] = fs.a[S_CLEAR_DAY];
                     fs.a[S_CLEAR_DAY] = (R)evd[eo + 3 * (size_t)n];
                 }
             }
-            if (fl & FL_MIN) {                         // _next_min
-                const size_t q = (size_t)((j - fm) / 60);
+            if (fl & FL_MIN) {                         // _next_min, drawn here from its key
+                double cloudy, clear;
+                minute_draws<R>(dp, chain, step, interp(ccb, cca, tab64[(size_t)j * ROW + G_HOURF]), cloudy, clear);
                 fs.b[S_CLOUDY_NOISE] = fs.a[S_CLOUDY_NOISE];
-                fs.a[S_CLOUDY_NOISE] = (R)mind[q * 2 * n];
+                fs.a[S_CLOUDY_NOISE] = (R)cloudy;
                 fs.b[S_CLEAR_NOISE] = fs.a[S_CLEAR_NOISE];
-                fs.a[S_CLEAR_NOISE] = (R)mind[(q * 2 + 1) * n];
+                fs.a[S_CLEAR_NOISE] = (R)clear;
             }
             while (step >= (int64_t)seg.y) seg = rec[++jr];   // next_cloud happened at seg.y
             const bool covered = step < (int64_t)seg.x;
@@ -862,7 +1130,9 @@ __global__ __launch_bounds__(256) void expand_kernel(KParams kp, StateView st, u
 
 // Stats partials -> per-chain accumulators (fixed order: deterministic), then
 // the window-end state of P1/P2 -> chain state.
-__global__ __launch_bounds__(256) void commit_kernel(StateView st, uint32_t n, SegView sg, StatsView sv,
+template <typename R>
+__global__ __launch_bounds__(256) void commit_kernel(StateView st, uint32_t n, SegView sg, StatsView sv, MinuteCtx mc0,
+                                                     const uint32_t* __restrict__ n_events,
                                                      const BlockDesc* __restrict__ desc_end)
 {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -891,7 +1161,10 @@ __global__ __launch_bounds__(256) void commit_kernel(StateView st, uint32_t n, S
         sp.b[k] = st.sb[k][c];
         sp.a[k] = st.sa[k][c];
     }
-    samplers_at(*desc_end, sg, n, c, sp);
+    MinuteCtx mc = mc0;
+    mc.chain += c;
+    mc.ne = (int)min(*n_events, sg.evcap);
+    samplers_at<R>(*desc_end, sg, n, c, sp, mc, st);
 #pragma unroll
     for (int k = 0; k < 5; ++k) {   // cc, clear_day, cloudy_hour (unchanged), noises
         st.sb[k][c] = sp.b[k];
@@ -993,6 +1266,9 @@ StateView make_view(void* base, uint32_t n)
 // plan: tab64 | tab32 | events | n_events | block descriptors
 uint32_t ev_cap(uint32_t n_steps) { return n_steps / 1800 + 64; }
 uint32_t nblk_of(uint32_t n_steps) { return (n_steps + BLOCK_STEPS - 1) / BLOCK_STEPS; }
+// next_cloud calls a chain makes per window: ~0.0045 / s on average, < 0.0085 / s
+// on the busiest chains (windy days); calls past the table are drawn in the walk
+uint32_t cand_cap(uint32_t n_steps) { return n_steps / 100 + 128; }
 
 struct PlanView {
     double* tab64;
@@ -1044,15 +1320,18 @@ size_t scratch_layout(uint32_t n, uint32_t n_steps, void* base, SegView* v)
     o += align_up((size_t)n * 6 * 8);
     if (v) v->part = (double*)(b + o);
     o += align_up((size_t)n * nblk * 4 * 8);
-    const uint32_t evc = ev_cap(n_steps), nmin = n_steps / 60 + 2;
+    const uint32_t evc = ev_cap(n_steps);
     if (v) {
         v->evcap = evc;
-        v->nmin = nmin;
         v->evd = (double*)(b + o);
     }
     o += align_up((size_t)n * evc * 4 * 8);
-    if (v) v->mind = (double*)(b + o);
-    o += align_up((size_t)n * nmin * 2 * 8);
+    const uint32_t kc = cand_cap(n_steps);
+    if (v) {
+        v->kcap = kc;
+        v->cand = (double*)(b + o);
+    }
+    o += align_up((size_t)n * kc * 8);
     return o;
 }
 
@@ -1064,10 +1343,6 @@ struct tmh_engine {
     GParams gp;
     int device;
     int path;   // resolved kernel path: 1 sequential, 2 time-parallel
-    // side stream: the minute draws run beside the segment walk (both need only
-    // the event draws); created on first use, never holds device memory
-    hipStream_t aux = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // kernel timing (tmh_profile_*): event pairs per kernel, read and recycled
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[TMH_K_COUNT];
@@ -1106,9 +1381,6 @@ struct tmh_engine {
                 (void)hipEventDestroy(p.second);
             }
         for (hipEvent_t e : pool) (void)hipEventDestroy(e);
-        if (ev_fork) (void)hipEventDestroy(ev_fork);
-        if (ev_join) (void)hipEventDestroy(ev_join);
-        if (aux) (void)hipStreamDestroy(aux);
     }
 };
 
@@ -1224,6 +1496,13 @@ int tmh_engine_destroy(struct tmh_engine* eng)
 }
 
 int tmh_engine_path(const struct tmh_engine* eng) { return eng ? eng->path : TMH_E_INVAL; }
+
+#ifdef TMH_DIAG_P1
+int tmh_diag_p1(uint64_t* out, uint32_t n)   // diagnostic build only
+{
+    return hip_check(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_p1diag), (size_t)n * 8), "diag copy");
+}
+#endif
 
 int tmh_profile_enable(struct tmh_engine* eng, int on)
 {
@@ -1350,29 +1629,16 @@ int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
     scratch_layout(n_chains, n_steps, scratch, &sg);
     const uint32_t cb = (n_chains + 255) / 256;
     const int64_t utc0 = eng->gp.clock.utc0;
-    if (!eng->aux) {
-        if (int rc = hip_check(hipStreamCreateWithFlags(&eng->aux, hipStreamNonBlocking), "hipStreamCreate")) return rc;
-        if (int rc = hip_check(hipEventCreateWithFlags(&eng->ev_fork, hipEventDisableTiming), "hipEventCreate"))
-            return rc;
-        if (int rc = hip_check(hipEventCreateWithFlags(&eng->ev_join, hipEventDisableTiming), "hipEventCreate"))
-            return rc;
-    }
     hipEvent_t t_step = eng->mark(s);
     hipLaunchKernelGGL(event_draws_kernel, dim3(sg.evcap, cb), dim3(256), 0, s, eng->dp, chain0, n_chains, n_steps,
                        pv.events, pv.n_events, sg.evd);
-    // fork: minute draws on the side stream, segment walk on `s`; join before P2
-    if (int rc = hip_check(hipEventRecord(eng->ev_fork, s), "hipEventRecord")) return rc;
-    if (int rc = hip_check(hipStreamWaitEvent(eng->aux, eng->ev_fork, 0), "hipStreamWaitEvent")) return rc;
-    hipEvent_t t_min = eng->mark(eng->aux);
-    hipLaunchKernelGGL(minute_draws_kernel, dim3(sg.nmin, cb), dim3(256), 0, eng->aux, eng->dp, v, chain0, n_chains,
-                       step0, n_steps, utc0, pv.tab64, pv.events, pv.n_events, sg.evd, sg.mind);
-    eng->close(TMH_K_MINUTE_DRAWS, t_min, eng->aux);
-    if (int rc = hip_check(hipEventRecord(eng->ev_join, eng->aux), "hipEventRecord")) return rc;
+    hipEvent_t t_cand = eng->mark(s);
+    hipLaunchKernelGGL(candidates_kernel, dim3(cb, sg.kcap), dim3(256), 0, s, eng->dp, v, chain0, n_chains, sg);
+    eng->close(TMH_K_CANDIDATES, t_cand, s);
     hipEvent_t t_seg = eng->mark(s);
-    hipLaunchKernelGGL(segments_kernel, dim3((n_chains + 3) / 4), dim3(256), 0, s, eng->dp, v, chain0, n_chains,
+    hipLaunchKernelGGL(segments_kernel, dim3((n_chains + 15) / 16), dim3(256), 0, s, eng->dp, v, chain0, n_chains,
                        step0, n_steps, eng->gp.clock, pv.events, pv.n_events, sg);
     eng->close(TMH_K_SEGMENTS, t_seg, s);
-    if (int rc = hip_check(hipStreamWaitEvent(s, eng->ev_join, 0), "hipStreamWaitEvent")) return rc;
     if (int rc = hip_check(hipGetLastError(), "draws/segments kernels launch")) return rc;
     hipEvent_t t_exp = eng->mark(s);
     dim3 grid2(nblk_of(n_steps), cb);
@@ -1381,8 +1647,8 @@ int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
                     : (!tv.pv && !tv.meter && !tv.residual && !tv.csi && !tv.covered) ? OUT_STATS
                                                                                       : OUT_ANY;
 #define LAUNCH(R, O)                                                                                                 \
-    hipLaunchKernelGGL((expand_kernel<R, O>), grid2, dim3(256), lds, s, eng->kp, v, chain0, n_chains, step0, n_steps, \
-                       utc0, pv.tab64, pv.tab32, pv.desc, sg, tv, sv)
+    hipLaunchKernelGGL((expand_kernel<R, O>), grid2, dim3(256), lds, s, eng->kp, eng->dp, v, chain0, n_chains, step0, \
+                       n_steps, utc0, pv.tab64, pv.tab32, pv.events, pv.n_events, pv.desc, sg, tv, sv)
     if (f64) {
         if (out == OUT_TRACE3) LAUNCH(double, OUT_TRACE3);
         else if (out == OUT_STATS) LAUNCH(double, OUT_STATS);
@@ -1395,7 +1661,13 @@ int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
 #undef LAUNCH
     eng->close(TMH_K_EXPAND, t_exp, s);
     if (int rc = hip_check(hipGetLastError(), "expand_kernel launch")) return rc;
-    hipLaunchKernelGGL(commit_kernel, dim3(cb), dim3(256), 0, s, v, n_chains, sg, sv, pv.desc + nblk_of(n_steps));
+    const MinuteCtx mc{eng->dp, chain0, step0, first_minute_host(utc0, step0), pv.events, 0, pv.tab64};
+    if (f64)
+        hipLaunchKernelGGL(commit_kernel<double>, dim3(cb), dim3(256), 0, s, v, n_chains, sg, sv, mc, pv.n_events,
+                           pv.desc + nblk_of(n_steps));
+    else
+        hipLaunchKernelGGL(commit_kernel<float>, dim3(cb), dim3(256), 0, s, v, n_chains, sg, sv, mc, pv.n_events,
+                           pv.desc + nblk_of(n_steps));
     eng->close(TMH_K_STEP, t_step, s);
     return hip_check(hipGetLastError(), "commit_kernel launch");
 }

@@ -150,6 +150,21 @@ __device__ __forceinline__ double scaled_noise(const KParams& kp, double u, doub
     return normal(u, 1.0, kp.sqrt09 * (s0 + s1 * 8 * cc));
 }
 
+// _next_min noise draw (clearskyindexmodel.py:86-88, 109-111): the reference's
+// fp64 formula in fp64 mode; in fp32 mode the quantile and the affine map run in
+// fp32 (the scale is formed in fp64 and rounded), the value is kept exactly as a
+// double.  Shared by every kernel path so the paths agree bit for bit.
+template <typename R>
+__device__ __forceinline__ double minute_noise(double u, double s0, double s1, double cc, double sqrt09)
+{
+    if constexpr (sizeof(R) == 8) {
+        return normal(u, 1.0, sqrt09 * (s0 + s1 * 8 * cc));
+    } else {
+        const float sc = (float)(sqrt09 * (s0 + s1 * 8 * cc));
+        return (double)(ndtri_f(u) * sc + 1.0f);
+    }
+}
+
 // hourly cloud cover: next(get_cloud_cover(distributions)) (cloud_cover_hourly.py:309-316);
 // faithful = a fresh generator per draw, i.e. state 1.0 (clearskyindexmodel.py:61-63)
 __device__ __forceinline__ double draw_cc_from(const KParams& kp, double state, double u)
