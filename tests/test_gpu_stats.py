@@ -1,0 +1,37 @@
+"""Statistical equivalence on the GPU: the product path (time-parallel kernels,
+fp32, keyed Philox) against the reference's own seeded runs
+(tests/golden/stats_seeded.npz), with the chain-level statistics and KS bar of
+tests/test_stats_cpu.py.  One day, 1,024 chains, Munich, 2019-09-05."""
+import numpy as np
+import pytest
+
+from stats_util import P_MIN, SEGMENT_KEYS, ks, load_reference, summarize, summarize_trace
+from test_stats_cpu import csi_chain_stats
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def test_keyed_gpu_matches_reference_statistics():
+    from tmhpvsim_amd.engine import BatchedSim
+    from tmhpvsim_amd.params import ModelParams
+    n = 1024
+    sim = BatchedSim(n, "2019-09-05 00:00:00", tz="Europe/Berlin", params=ModelParams(with_pv=False, seed=0xC0FFEE),
+                     precision="fp32", chain0=77_000, device="cuda:0", horizon=86400)
+    assert sim.path == "time_parallel"
+    out = sim.run(86400, trace=("csi", "covered"))
+    torch.cuda.synchronize()
+    assert (sim.status() == 0).all()
+    cov = out["covered"].cpu().numpy()
+    csi = out["csi"].cpu().numpy().astype(np.float64)
+    assert (csi > 0).all() and (csi < 2).all()          # tests/test_clearskyindexmodel.py:13
+    ref = load_reference()
+    got, exp = summarize_trace(cov), summarize(ref["first"], ref["runs"])
+    for key in SEGMENT_KEYS:
+        p = ks(got[key], exp[key])
+        assert p > P_MIN, f"{key}: KS p = {p:.2e} ({np.nanmean(got[key]):.4g} vs {np.nanmean(exp[key]):.4g})"
+    g, e = csi_chain_stats(csi[30::60].T), csi_chain_stats(ref["csi_min"])
+    for key in g:
+        p = ks(g[key], e[key])
+        assert p > P_MIN, f"csi {key}: KS p = {p:.2e}"

@@ -533,13 +533,17 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
                 // the meter is its own process in the reference: always keyed
                 const U4 pb = keyed_block(kp.seed, chain, (uint64_t)step >> 1, TAG_STEP2, 0);
                 const bool odd = step & 1;
-                double ue = u32d(odd ? pb.z : pb.x);
-                const double um = u32d(odd ? pb.w : pb.y);
-                if constexpr (RNG == TMH_RNG_INJECTED) ue = dr.one(ch, step, TAG_STEP, 0, 0);
+                R z = noise_z<R>(odd ? pb.z : pb.x);
+                const R mtr = meter_w<R>(odd ? pb.w : pb.y);
+                if constexpr (RNG == TMH_RNG_INJECTED) {
+                    const double ue = dr.one(ch, step, TAG_STEP, 0, 0);
+                    if constexpr (sizeof(R) == 8) z = ndtri(ue);
+                    else z = ndtri_f(ue);
+                }
                 if (ch.status == 0) {
                     const bool covered = ch.sec < ch.t1;
                     cov = covered ? 1 : 0;
-                    second_body<R>(kp, row, fl, fs, covered, ue, um, csi, pv, meter, res);
+                    second_body<R>(kp, row, fl, fs, covered, z, mtr, csi, pv, meter, res);
                     ok = true;
                 }
             }
@@ -1020,7 +1024,7 @@ __global__ __launch_bounds__(256) void expand_kernel(KParams kp, DrawParams dp, 
     Acc acc{0.0, 0.0, 0.0, -INFINITY};
     bool alive = false;
     int32_t fault = INT_MAX;
-    int2 seg = make_int2(0, 0);
+    int2 seg = make_int2(0, 0), seg_nx = make_int2(0, 0);   // current record and the next, loaded ahead
     const int2* rec = sg.rec + (size_t)(live ? c : 0) * sg.cap;
     uint32_t jr = 0, evi = 0;
     FSamp<R> fs;
@@ -1052,6 +1056,7 @@ __global__ __launch_bounds__(256) void expand_kernel(KParams kp, DrawParams dp, 
         }
         jr = (uint32_t)lo;
         seg = rec[jr];
+        seg_nx = rec[min(jr + 1, sg.cap - 1)];
     }
     const double* evd = sg.evd + c;
     U4 pair{0, 0, 0, 0};
@@ -1090,7 +1095,12 @@ __global__ __launch_bounds__(256) void expand_kernel(KParams kp, DrawParams dp, 
                 fs.b[S_CLEAR_NOISE] = fs.a[S_CLEAR_NOISE];
                 fs.a[S_CLEAR_NOISE] = (R)clear;
             }
-            while (step >= (int64_t)seg.y) seg = rec[++jr];   // next_cloud happened at seg.y
+            if (step >= (int64_t)seg.y) {   // next_cloud happened at seg.y
+                seg = seg_nx;
+                ++jr;
+                while (step >= (int64_t)seg.y) seg = rec[++jr];   // zero-length segments (rare)
+                seg_nx = rec[min(jr + 1, sg.cap - 1)];
+            }
             const bool covered = step < (int64_t)seg.x;
             cov = covered ? 1 : 0;
             if (!(step & 1) || !have_pair) {   // one Philox block per step pair (uniform branch)
@@ -1103,8 +1113,8 @@ __global__ __launch_bounds__(256) void expand_kernel(KParams kp, DrawParams dp, 
                 have_pair = true;
             }
             const bool odd = step & 1;
-            second_body<R>(kp, row, fl, fs, covered, u32d(odd ? pair.z : pair.x), u32d(odd ? pair.w : pair.y), csi, pv,
-                           meter, res);
+            second_body<R>(kp, row, fl, fs, covered, noise_z<R>(odd ? pair.z : pair.x), meter_w<R>(odd ? pair.w : pair.y),
+                           csi, pv, meter, res);
         }
         if (fl & (FL_DAY | FL_HOUR)) ++evi;
 #ifdef TMH_DIAG_NO_STORE
@@ -1466,6 +1476,42 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
     k.temp_air = p->site[6];
     k.wind = p->site[7];
     k.tmod_k = std::exp(k.module[TMH_MOD_TEMP_A] + k.module[TMH_MOD_TEMP_B] * k.wind);   // sapm_celltemp factor
+    {   // fp32 constants of the PV chain (pv_power_f)
+        PVF& f = k.pvf;
+        const float alo[4] = {0.512f, -1.56f, 2.286f, -2.222f}, ahi[4] = {-5.743f, 21.77f, -27.49f, 11.56f};
+        const float blo[2] = {0.37f, 0.962f}, bhi[4] = {41.4f, -118.5f, 66.05f, 31.9f};
+        const float clo[3] = {-0.28f, 0.932f, -2.048f}, chi[4] = {-47.01f, 184.2f, -222.0f, 73.81f};
+        memcpy(f.a_disc_lo, alo, sizeof alo);
+        memcpy(f.a_disc_hi, ahi, sizeof ahi);
+        memcpy(f.b_disc_lo, blo, sizeof blo);
+        memcpy(f.b_disc_hi, bhi, sizeof bhi);
+        memcpy(f.c_disc_lo, clo, sizeof clo);
+        memcpy(f.c_disc_hi, chi, sizeof chi);
+        const double* m = k.module;
+        const double* iv = k.inverter;
+        f.tmod_k = (float)k.tmod_k;
+        f.temp_air = (float)k.temp_air;
+        f.dt_1e3 = (float)(m[TMH_MOD_TEMP_DT] * 1e-3);
+        f.fd = (float)m[TMH_MOD_FD];
+        f.bvmpo = (float)m[TMH_MOD_BVMPO];
+        f.mbvmp = (float)m[TMH_MOD_MBVMP];
+        f.nkq = (float)(m[TMH_MOD_N] * (1.38066e-23 / 1.60218e-19));
+        f.impo_c0 = (float)(m[TMH_MOD_IMPO] * m[TMH_MOD_C0]);
+        f.impo_c1 = (float)(m[TMH_MOD_IMPO] * m[TMH_MOD_C1]);
+        f.aimp = (float)m[TMH_MOD_AIMP];
+        f.vmpo = (float)m[TMH_MOD_VMPO];
+        f.c2ns = (float)(m[TMH_MOD_C2] * m[TMH_MOD_NS]);
+        f.c3ns = (float)(m[TMH_MOD_C3] * m[TMH_MOD_NS]);
+        f.paco = (float)iv[0];
+        f.pdco = (float)iv[1];
+        f.vdco = (float)iv[2];
+        f.pso = (float)iv[3];
+        f.ic0 = (float)iv[4];
+        f.ic1 = (float)iv[5];
+        f.ic2 = (float)iv[6];
+        f.ic3 = (float)iv[7];
+        f.pnt = (float)iv[8];
+    }
     memcpy(e->gp.site, p->site, sizeof e->gp.site);
     memcpy(e->gp.linke, p->linke, sizeof e->gp.linke);
     memcpy(e->gp.module, p->module, sizeof e->gp.module);

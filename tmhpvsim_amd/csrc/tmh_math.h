@@ -126,6 +126,46 @@ __device__ __forceinline__ float ndtri_f(double u)
     return 1.41421356237309505f * (p * x);
 }
 
+// the same quantile straight from a 32-bit Philox word w, u = (w + 1/2) 2^-32,
+// all in fp32: t = min(u, 1 - u) = (min(w, ~w) + 1/2) 2^-32 keeps the tails'
+// relative precision, x = 2u - 1 comes from the signed word (per-second noise
+// of the fp32 path; the fp64 path uses ndtri(u32d(w)))
+__device__ __forceinline__ float ndtri_w(uint32_t w)
+{
+    const uint32_t m = w < 0x80000000u ? w : ~w;
+    const float t = fmaf((float)m, 0x1p-32f, 0x1p-33f);
+    const float x = fmaf((float)(int32_t)(w ^ 0x80000000u), 0x1p-31f, 0x1p-32f);
+    const float w0 = -__logf(fmaf(-4.0f * t, t, 4.0f * t));   // -log((1 - x)(1 + x)) = -log(4 t (1 - t))
+    float p;
+    if (w0 < 5.0f) {
+        const float v = w0 - 2.5f;
+        p = 2.81022636e-08f;
+        p = fmaf(p, v, 3.43273939e-07f);
+        p = fmaf(p, v, -3.5233877e-06f);
+        p = fmaf(p, v, -4.39150654e-06f);
+        p = fmaf(p, v, 0.00021858087f);
+        p = fmaf(p, v, -0.00125372503f);
+        p = fmaf(p, v, -0.00417768164f);
+        p = fmaf(p, v, 0.246640727f);
+        p = fmaf(p, v, 1.50140941f);
+    } else if (w0 < 16.0f) {
+        const float v = sqrtf(w0) - 3.0f;
+        p = -0.000200214257f;
+        p = fmaf(p, v, 0.000100950558f);
+        p = fmaf(p, v, 0.00134934322f);
+        p = fmaf(p, v, -0.00367342844f);
+        p = fmaf(p, v, 0.00573950773f);
+        p = fmaf(p, v, -0.0076224613f);
+        p = fmaf(p, v, 0.00943887047f);
+        p = fmaf(p, v, 1.00167406f);
+        p = fmaf(p, v, 2.83297682f);
+    } else {   // p < 2e-7 per draw
+        const float z = normcdfinvf(t);
+        return w < 0x80000000u ? z : -z;
+    }
+    return 1.41421356237309505f * (p * x);
+}
+
 __device__ __noinline__ void gamma_pq(double a, double x, double lga, double& P, double& Q)
 {
     if (x <= 0.0) {

@@ -14,6 +14,13 @@ namespace tmh {
 #define ROW TMH_GEOM_FIELDS
 
 // ------------------------------------------------------------ parameters
+// fp32 constants of the PV chain (pvmodel.py:53-80), rounded once on the host
+struct PVF {
+    float a_disc_lo[4], a_disc_hi[4], b_disc_lo[2], b_disc_hi[4], c_disc_lo[3], c_disc_hi[4];
+    float tmod_k, temp_air, dt_1e3, fd, bvmpo, mbvmp, nkq, impo_c0, impo_c1, aimp, vmpo, c2ns, c3ns;
+    float paco, pdco, vdco, pso, ic0, ic1, ic2, ic3, pnt;
+};
+
 struct KParams {
     int32_t cc_mode, rng_mode, with_pv, precision;
     uint64_t seed;
@@ -25,6 +32,7 @@ struct KParams {
     double alpha, delta, expo, sqrt09, sqrt6;   // cloud_cover_binary.py:35-40, scales
     double temp_air, wind;                      // sapm_celltemp inputs (pvmodel.py:69-70)
     double tmod_k;                              // exp(a + b * wind): constant for the run (wind fixed at 0)
+    PVF pvf;                                    // fp32 copies for the fp32 chain
 };
 
 struct GParams {
@@ -769,6 +777,54 @@ __device__ __forceinline__ R pv_power(const KParams& kp, const R* g, R csi)
 }
 
 
+// fp32 PV chain: the same model as pv_power<float>, with fused multiply-adds,
+// fp32 constants rounded once on the host (KParams::pvf) and the hardware
+// exp / log; within the fp32 tolerance of the fp64 oracle
+__device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float csi)
+{
+    const float c = fminf(csi, g[G_CSIMAX]);
+    const float ghi = c * g[G_GHICS];
+    const float kt = fminf(fmaxf(ghi * g[G_I0H], 0.0f), 1.0f);
+    // DISC Kn (pvlib irradiance.disc): coefficient sets split at kt = 0.6
+    const bool lo = kt <= 0.6f;
+    const float a = lo ? fmaf(fmaf(fmaf(k.a_disc_lo[3], kt, k.a_disc_lo[2]), kt, k.a_disc_lo[1]), kt, k.a_disc_lo[0])
+                       : fmaf(fmaf(fmaf(k.a_disc_hi[3], kt, k.a_disc_hi[2]), kt, k.a_disc_hi[1]), kt, k.a_disc_hi[0]);
+    const float b = lo ? fmaf(k.b_disc_lo[1], kt, k.b_disc_lo[0])
+                       : fmaf(fmaf(fmaf(k.b_disc_hi[3], kt, k.b_disc_hi[2]), kt, k.b_disc_hi[1]), kt, k.b_disc_hi[0]);
+    const float cc = lo ? fmaf(fmaf(k.c_disc_lo[2], kt, k.c_disc_lo[1]), kt, k.c_disc_lo[0])
+                        : fmaf(fmaf(fmaf(k.c_disc_hi[3], kt, k.c_disc_hi[2]), kt, k.c_disc_hi[1]), kt, k.c_disc_hi[0]);
+    const float dkn = fmaf(b, __expf(cc * g[G_AM]), a);
+    float dni = (g[G_KNC] - dkn) * g[G_I0];
+    dni = (g[G_DISCOK] != 0.0f && ghi >= 0.0f && dni >= 0.0f) ? dni : 0.0f;
+    const float dhi = fmaf(-dni, g[G_COSZ], ghi);
+    const float AI = dni * g[G_DNIEXTRA];
+    const float sky = fmaxf(dhi * fmaf(AI, g[G_RB], (1.0f - AI) * g[G_TERM2]), 0.0f);
+    const float poa_direct = fmaxf(dni * g[G_COSAOI], 0.0f);
+    const float poa_diffuse = fmaf(ghi, g[G_GFAC], sky);
+    const float poa_global = poa_direct + poa_diffuse;
+    const float tcell = fmaf(poa_global, k.dt_1e3, fmaf(poa_global, k.tmod_k, k.temp_air));
+    const float Ee = g[G_F1] * fmaf(poa_direct, g[G_F2], k.fd * poa_diffuse) * 1e-3f;
+    const float Bvmpo = fmaf(k.mbvmp, 1.0f - Ee, k.bvmpo);
+    const float delta = k.nkq * (tcell + 273.15f);
+    const float logEe = Ee > 0.0f ? __logf(Ee) : (Ee == 0.0f ? -INFINITY : NAN);
+    const float dt25 = tcell - 25.0f;
+    const float imp = fmaf(k.impo_c1, Ee, k.impo_c0) * Ee * fmaf(k.aimp, dt25, 1.0f);
+    const float dl = delta * logEe;
+    float vmp = fmaf(Bvmpo, dt25, fmaf(k.c3ns, dl * dl, fmaf(k.c2ns, dl, k.vmpo)));
+    vmp = isnan(vmp) ? vmp : fmaxf(vmp, 0.0f);
+    const float pdc = imp * vmp;
+    const float dv = vmp - k.vdco;
+    const float A = k.pdco * fmaf(k.ic1, dv, 1.0f);
+    const float B = k.pso * fmaf(k.ic2, dv, 1.0f);
+    const float C = k.ic0 * fmaf(k.ic3, dv, 1.0f);
+    const float AmB = A - B, pmB = pdc - B;
+    float ac = fmaf(C, pmB * pmB, fmaf(-C, AmB, __fdividef(k.paco, AmB)) * pmB);
+    ac = isnan(ac) ? ac : fminf(ac, k.paco);
+    if (pdc < k.pso) ac = -fabsf(k.pnt);
+    if (isnan(ac)) return 0.0f;   // .fillna(0.)
+    return fmaxf(ac, 0.0f);       // .clip(lower=0.)
+}
+
 // ------------------------------------------------------------ fused per-second body
 template <typename R>
 struct FSamp {
@@ -792,18 +848,31 @@ __device__ __forceinline__ R rinterp(const FSamp<R>& f, int k, R frac)
 }
 
 // clearskyindexmodel.py:146-160 + pvmodel.py:53-80 + metersim.py:51 + pvsim.py:83
+// per-second draws from the step's two Philox words (keyed mode): the noise's
+// standard normal and the meter (metersim.py:51, 9000 u in [0, 9000))
+template <typename R>
+__device__ __forceinline__ R noise_z(uint32_t w)
+{
+#ifdef TMH_DIAG_NO_NDTRI
+    return R((double)w * 0x1p-32 - 0.5);
+#else
+    if constexpr (sizeof(R) == 8) return ndtri(u32d(w));
+    else return ndtri_w(w);
+#endif
+}
+
+template <typename R>
+__device__ __forceinline__ R meter_w(uint32_t w)
+{
+    if constexpr (sizeof(R) == 8) return 9000 * u32d(w);
+    else return fminf(fmaf((float)w, 9000.0f * 0x1p-32f, 9000.0f * 0x1p-33f), 8999.9990234375f);   // largest float < 9000
+}
+
 template <typename R>
 __device__ __forceinline__ void second_body(const KParams& kp, const R* row, uint32_t fl, const FSamp<R>& fs,
-                                            bool covered, double ue, double um, R& csi, R& pv, R& meter, R& res)
+                                            bool covered, R z, R meter_in, R& csi, R& pv, R& meter, R& res)
 {
     const R cloudcover = rinterp(fs, S_CC, row[G_HOURF]);   // == interp() bit for bit when R = double
-    R z;
-#ifdef TMH_DIAG_NO_NDTRI
-    z = R(ue - 0.5);
-#else
-    if constexpr (sizeof(R) == 8) z = ndtri(ue);
-    else z = ndtri_f(ue);
-#endif
     const R eps = z * (R(kp.sqrt6) * (R(0.001) + R(0.0015 * 8) * cloudcover)) + R(0);
     if (covered)
         csi = rinterp(fs, S_CLEAR_DAY, row[G_DAYF]) * (rinterp(fs, S_CLEAR_NOISE, row[G_MINF]) + eps);
@@ -812,10 +881,10 @@ __device__ __forceinline__ void second_body(const KParams& kp, const R* row, uin
 #ifdef TMH_DIAG_NO_PV
     pv = csi * row[G_GHICS];
 #else
-    pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power<R>(kp, row, csi) : R(0);
+    if constexpr (sizeof(R) == 8) pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power<R>(kp, row, csi) : R(0);
+    else pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power_f(kp.pvf, row, csi) : 0.0f;
 #endif
-    if constexpr (sizeof(R) == 8) meter = 9000 * um;
-    else meter = fminf((float)(9000 * um), 8999.9990234375f);   // largest float < 9000: keep [0, 9000)
+    meter = meter_in;
     res = meter - pv;
 }
 
