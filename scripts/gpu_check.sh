@@ -15,11 +15,11 @@ echo "smoke rc=$rc"; tail -3 "$OUT/smoke.log"
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider -rf --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -15 "$OUT/pytest_gpu.log"
 [ $rc -le 1 ] || exit $rc
-timeout -k 10 600 python bench.py --steps 3 --warmup 1 > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err"; rc=$?
+timeout -k 10 600 python bench.py --steps 6 --warmup 2 > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err"; rc=$?
 echo "bench rc=$rc"; cat "$OUT/bench_$TAG.json"; tail -3 "$OUT/bench_$TAG.err"
 [ $rc -eq 0 ] || exit $rc
 cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- \
-    python "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/prof_$TAG.log" 2>&1; rc=$?
+    python "$ROOT/bench.py" --steps 6 --warmup 2 --no-cpu-baseline > "$OUT/prof_$TAG.log" 2>&1; rc=$?
 echo "rocprof rc=$rc"; find "$OUT/prof_$TAG" -name "*stats*"
 exit $rc
