@@ -61,7 +61,7 @@ extern "C" {
 #define TMH_FP64 1         /* everything in fp64 */
 #define TMH_PATH_AUTO 0          /* time-parallel when possible (keyed + faithful), else sequential */
 #define TMH_PATH_SEQUENTIAL 1    /* one work-item per chain, seconds in order */
-#define TMH_PATH_TIME_PARALLEL 2 /* segment pass + (chain x 256 s block) expansion */
+#define TMH_PATH_TIME_PARALLEL 2 /* segment pass + (chain x 128 s block) expansion */
 
 #define TMH_SIGMA_CAP 512  /* capacity of sigma_cloud / sigma_clear per chain (max seen: 132) */
 #define TMH_GEOM_FIELDS 20 /* doubles per step in the clock/geometry table */

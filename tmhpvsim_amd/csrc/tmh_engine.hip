@@ -43,7 +43,10 @@ using namespace tmh;
 
 namespace {
 
-constexpr int BLOCK_STEPS = 256;   // seconds per P2 work-item
+#ifndef TMH_BLOCK_STEPS
+#define TMH_BLOCK_STEPS 128
+#endif
+constexpr int BLOCK_STEPS = TMH_BLOCK_STEPS;   // seconds per P2 work-item
 
 struct BlockDesc {                 // as of the step before the block start; -1 = none in the window
     int32_t q0, q1;                // minute-draw indices of the last two minute boundaries
@@ -1000,8 +1003,14 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
 // One work-item per (chain, block of 256 seconds).  The boundary draws come
 // from the draw tables, so the per-second loop holds only the R copies of the
 // sampler pairs and does no fp64 work in fp32 mode.
+#ifndef TMH_ROW_PREFETCH
+#define TMH_ROW_PREFETCH 0
+#endif
+#ifndef TMH_EXP_WAVES
+#define TMH_EXP_WAVES 1
+#endif
 template <typename R, int OUT>
-__global__ __launch_bounds__(256) void expand_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0,
+__global__ __launch_bounds__(256, TMH_EXP_WAVES) void expand_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0,
                                                      uint32_t n, int64_t W0, uint32_t nsteps, int64_t utc0,
                                                      const double* __restrict__ tab64,
                                                      const float* __restrict__ tab32,
@@ -1061,13 +1070,28 @@ __global__ __launch_bounds__(256) void expand_kernel(KParams kp, DrawParams dp, 
     const double* evd = sg.evd + c;
     U4 pair{0, 0, 0, 0};
     bool have_pair = false;
+    // the step's geometry row (wave-uniform, scalar loads) is fetched one step
+    // ahead, so its latency hides behind the previous step's arithmetic
+    auto load_row = [&](uint32_t j, R* r) {
+#pragma unroll
+        for (int i = 0; i < ROW; ++i)
+            r[i] = sizeof(R) == 8 ? (R)tab64[(size_t)j * ROW + i] : (R)tab32[(size_t)j * ROW + i];
+    };
+#if TMH_ROW_PREFETCH
+    R row_nx[ROW];
+    load_row(j0, row_nx);
+#endif
     for (uint32_t j = j0; j < j1; ++j) {
         const int64_t step = W0 + j;
-        const float* r32 = tab32 + (size_t)j * ROW;
-        const uint32_t fl = __float_as_uint(r32[G_FLAGS]);
         R row[ROW];
+#if TMH_ROW_PREFETCH
 #pragma unroll
-        for (int i = 0; i < ROW; ++i) row[i] = sizeof(R) == 8 ? (R)tab64[(size_t)j * ROW + i] : (R)r32[i];
+        for (int i = 0; i < ROW; ++i) row[i] = row_nx[i];
+        if (j + 1 < j1) load_row(j + 1, row_nx);
+#else
+        load_row(j, row);
+#endif
+        const uint32_t fl = sizeof(R) == 8 ? (uint32_t)tab64[(size_t)j * ROW + G_FLAGS] : __float_as_uint(row[G_FLAGS]);
         R csi = R(NAN), pv = R(NAN), meter = R(NAN), res = R(NAN);
         uint8_t cov = 255;
         const bool ok = alive && (int32_t)j < fault;
@@ -1478,15 +1502,6 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
     k.tmod_k = std::exp(k.module[TMH_MOD_TEMP_A] + k.module[TMH_MOD_TEMP_B] * k.wind);   // sapm_celltemp factor
     {   // fp32 constants of the PV chain (pv_power_f)
         PVF& f = k.pvf;
-        const float alo[4] = {0.512f, -1.56f, 2.286f, -2.222f}, ahi[4] = {-5.743f, 21.77f, -27.49f, 11.56f};
-        const float blo[2] = {0.37f, 0.962f}, bhi[4] = {41.4f, -118.5f, 66.05f, 31.9f};
-        const float clo[3] = {-0.28f, 0.932f, -2.048f}, chi[4] = {-47.01f, 184.2f, -222.0f, 73.81f};
-        memcpy(f.a_disc_lo, alo, sizeof alo);
-        memcpy(f.a_disc_hi, ahi, sizeof ahi);
-        memcpy(f.b_disc_lo, blo, sizeof blo);
-        memcpy(f.b_disc_hi, bhi, sizeof bhi);
-        memcpy(f.c_disc_lo, clo, sizeof clo);
-        memcpy(f.c_disc_hi, chi, sizeof chi);
         const double* m = k.module;
         const double* iv = k.inverter;
         f.tmod_k = (float)k.tmod_k;

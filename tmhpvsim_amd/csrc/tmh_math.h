@@ -19,15 +19,23 @@ struct U4 {
     uint32_t x, y, z, w;
 };
 
+// Key schedule bump on the scalar unit (keys are the seed: wave-uniform).  The
+// asm is volatile so the compiler cannot hoist the twenty round keys of a
+// loop-invariant seed out of a kernel's main loop: held across the loop they
+// spill into VGPR lanes and every round pays a v_readlane (seen in expand_kernel).
+__device__ __forceinline__ void key_bump(uint32_t& k0, uint32_t& k1)
+{
+    asm volatile("s_add_u32 %0, %0, 0x9e3779b9\n\ts_add_u32 %1, %1, 0xbb67ae85" : "+s"(k0), "+s"(k1) : : "scc");
+}
+
 __device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                             uint32_t k0, uint32_t k1)
 {
+    k0 = __builtin_amdgcn_readfirstlane(k0);
+    k1 = __builtin_amdgcn_readfirstlane(k1);
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        if (r) {
-            k0 += 0x9E3779B9u;
-            k1 += 0xBB67AE85u;
-        }
+        if (r) key_bump(k0, k1);
         // one v_mad_u64_u32 per product (both halves) instead of mul_lo + mul_hi:
         // about 25 % less issue time per block on gfx950 (scripts/micro/philox_bench.hip)
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
@@ -135,7 +143,8 @@ __device__ __forceinline__ float ndtri_w(uint32_t w)
     const uint32_t m = w < 0x80000000u ? w : ~w;
     const float t = fmaf((float)m, 0x1p-32f, 0x1p-33f);
     const float x = fmaf((float)(int32_t)(w ^ 0x80000000u), 0x1p-31f, 0x1p-32f);
-    const float w0 = -__logf(fmaf(-4.0f * t, t, 4.0f * t));   // -log((1 - x)(1 + x)) = -log(4 t (1 - t))
+    // -log((1 - x)(1 + x)) = -log(4 t (1 - t)); the argument is >= 2^-31: no denormal path needed
+    const float w0 = -0.693147180559945309f * __builtin_amdgcn_logf(fmaf(-4.0f * t, t, 4.0f * t));
     float p;
     if (w0 < 5.0f) {
         const float v = w0 - 2.5f;

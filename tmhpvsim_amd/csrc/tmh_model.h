@@ -16,7 +16,6 @@ namespace tmh {
 // ------------------------------------------------------------ parameters
 // fp32 constants of the PV chain (pvmodel.py:53-80), rounded once on the host
 struct PVF {
-    float a_disc_lo[4], a_disc_hi[4], b_disc_lo[2], b_disc_hi[4], c_disc_lo[3], c_disc_hi[4];
     float tmod_k, temp_air, dt_1e3, fd, bvmpo, mbvmp, nkq, impo_c0, impo_c1, aimp, vmpo, c2ns, c3ns;
     float paco, pdco, vdco, pso, ic0, ic1, ic2, ic3, pnt;
 };
@@ -786,14 +785,17 @@ __device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float 
     const float ghi = c * g[G_GHICS];
     const float kt = fminf(fmaxf(ghi * g[G_I0H], 0.0f), 1.0f);
     // DISC Kn (pvlib irradiance.disc): coefficient sets split at kt = 0.6
+    // (the model's literal coefficients: compile-time constants, no SGPRs)
     const bool lo = kt <= 0.6f;
-    const float a = lo ? fmaf(fmaf(fmaf(k.a_disc_lo[3], kt, k.a_disc_lo[2]), kt, k.a_disc_lo[1]), kt, k.a_disc_lo[0])
-                       : fmaf(fmaf(fmaf(k.a_disc_hi[3], kt, k.a_disc_hi[2]), kt, k.a_disc_hi[1]), kt, k.a_disc_hi[0]);
-    const float b = lo ? fmaf(k.b_disc_lo[1], kt, k.b_disc_lo[0])
-                       : fmaf(fmaf(fmaf(k.b_disc_hi[3], kt, k.b_disc_hi[2]), kt, k.b_disc_hi[1]), kt, k.b_disc_hi[0]);
-    const float cc = lo ? fmaf(fmaf(k.c_disc_lo[2], kt, k.c_disc_lo[1]), kt, k.c_disc_lo[0])
-                        : fmaf(fmaf(fmaf(k.c_disc_hi[3], kt, k.c_disc_hi[2]), kt, k.c_disc_hi[1]), kt, k.c_disc_hi[0]);
-    const float dkn = fmaf(b, __expf(cc * g[G_AM]), a);
+    const float a3 = lo ? -2.222f : 11.56f, a2 = lo ? 2.286f : -27.49f, a1 = lo ? -1.56f : 21.77f,
+                a0 = lo ? 0.512f : -5.743f;
+    const float b3 = lo ? 0.0f : 31.9f, b2 = lo ? 0.0f : 66.05f, b1 = lo ? 0.962f : -118.5f, b0 = lo ? 0.37f : 41.4f;
+    const float c3 = lo ? 0.0f : 73.81f, c2 = lo ? -2.048f : -222.0f, c1 = lo ? 0.932f : 184.2f,
+                c0 = lo ? -0.28f : -47.01f;
+    const float a = fmaf(fmaf(fmaf(a3, kt, a2), kt, a1), kt, a0);
+    const float b = fmaf(fmaf(fmaf(b3, kt, b2), kt, b1), kt, b0);
+    const float cc = fmaf(fmaf(fmaf(c3, kt, c2), kt, c1), kt, c0);
+    const float dkn = fmaf(b, __builtin_amdgcn_exp2f(cc * g[G_AM] * 1.44269504088896341f), a);
     float dni = (g[G_KNC] - dkn) * g[G_I0];
     dni = (g[G_DISCOK] != 0.0f && ghi >= 0.0f && dni >= 0.0f) ? dni : 0.0f;
     const float dhi = fmaf(-dni, g[G_COSZ], ghi);
@@ -806,7 +808,7 @@ __device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float 
     const float Ee = g[G_F1] * fmaf(poa_direct, g[G_F2], k.fd * poa_diffuse) * 1e-3f;
     const float Bvmpo = fmaf(k.mbvmp, 1.0f - Ee, k.bvmpo);
     const float delta = k.nkq * (tcell + 273.15f);
-    const float logEe = Ee > 0.0f ? __logf(Ee) : (Ee == 0.0f ? -INFINITY : NAN);
+    const float logEe = Ee > 0.0f ? __builtin_amdgcn_logf(Ee) * 0.693147180559945309f : (Ee == 0.0f ? -INFINITY : NAN);
     const float dt25 = tcell - 25.0f;
     const float imp = fmaf(k.impo_c1, Ee, k.impo_c0) * Ee * fmaf(k.aimp, dt25, 1.0f);
     const float dl = delta * logEe;
@@ -818,7 +820,7 @@ __device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float 
     const float B = k.pso * fmaf(k.ic2, dv, 1.0f);
     const float C = k.ic0 * fmaf(k.ic3, dv, 1.0f);
     const float AmB = A - B, pmB = pdc - B;
-    float ac = fmaf(C, pmB * pmB, fmaf(-C, AmB, __fdividef(k.paco, AmB)) * pmB);
+    float ac = fmaf(C, pmB * pmB, fmaf(-C, AmB, k.paco * __builtin_amdgcn_rcpf(AmB)) * pmB);
     ac = isnan(ac) ? ac : fminf(ac, k.paco);
     if (pdc < k.pso) ac = -fabsf(k.pnt);
     if (isnan(ac)) return 0.0f;   // .fillna(0.)
