@@ -1119,13 +1119,14 @@ __global__ __launch_bounds__(256, TMH_EXP_WAVES) void expand_kernel(KParams kp, 
                 fs.b[S_CLEAR_NOISE] = fs.a[S_CLEAR_NOISE];
                 fs.a[S_CLEAR_NOISE] = (R)clear;
             }
-            if (step >= (int64_t)seg.y) {   // next_cloud happened at seg.y
+            const int32_t stepi = (int32_t)step;   // steps < 2^31 (tmh_step checks the window)
+            if (stepi >= seg.y) {   // next_cloud happened at seg.y
                 seg = seg_nx;
                 ++jr;
-                while (step >= (int64_t)seg.y) seg = rec[++jr];   // zero-length segments (rare)
+                while (stepi >= seg.y) seg = rec[++jr];   // zero-length segments (rare)
                 seg_nx = rec[min(jr + 1, sg.cap - 1)];
             }
-            const bool covered = step < (int64_t)seg.x;
+            const bool covered = stepi < seg.x;
             cov = covered ? 1 : 0;
             if (!(step & 1) || !have_pair) {   // one Philox block per step pair (uniform branch)
 #ifdef TMH_DIAG_NO_RNG   // diagnostic builds only (scripts/diag_variants.sh): cost breakdown
@@ -1145,7 +1146,16 @@ __global__ __launch_bounds__(256, TMH_EXP_WAVES) void expand_kernel(KParams kp, 
         if (live && csi == R(-12345))
             emit<R, OUT>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok);
 #else
-        if (live) emit<R, OUT>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok);
+        if constexpr (OUT == OUT_TRACE3) {   // row pointers are wave-uniform: 32-bit lane offsets only
+            if (live) {
+                const size_t ro = (size_t)j * tr.ld;
+                __builtin_nontemporal_store(pv, reinterpret_cast<R*>(tr.pv) + ro + c);
+                __builtin_nontemporal_store(meter, reinterpret_cast<R*>(tr.meter) + ro + c);
+                __builtin_nontemporal_store(res, reinterpret_cast<R*>(tr.residual) + ro + c);
+            }
+        } else if (live) {
+            emit<R, OUT>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok);
+        }
 #endif
     }
     if (live && sv.acc) {
