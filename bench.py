@@ -40,8 +40,8 @@ TRACE_BYTES = 12               # meter + pv + residual, fp32
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--chains", type=int, default=4096, help="chains per GPU")
     ap.add_argument("--seconds", type=int, default=86400)
     ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64"])
@@ -50,9 +50,9 @@ def parse():
     ap.add_argument("--cpu-sample-chains", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--path", default="auto", choices=["auto", "sequential", "time_parallel"])
-    ap.add_argument("--pipeline", type=int, default=2,
-                    help="batches in flight on separate HIP streams (1 = no overlap): batch k+1's segment "
-                         "walk (latency-bound, one wave per SIMD) runs beside batch k's expansion")
+    ap.add_argument("--pipeline", type=int, default=3,
+                    help="batches in flight on separate HIP streams (1 = no overlap): the segment walks of the "
+                         "next batches (latency-bound, one wave per SIMD) run beside this batch's expansion")
     return ap.parse_args()
 
 
@@ -213,6 +213,8 @@ def main():
                       "kernel": "expand_kernel (P2, " + sim.path + ")", "kernel_ms": kmean,
                       "note": "stats mode stores no trace; VALU counters under profiles/"}),
         "phases_ms": phases,
+        # whole-pipeline rate: trace bytes of all batches / wall time (kernels overlap across batches)
+        "effective_trace_gbs": (TRACE_BYTES * n * secs / (elapsed / args.steps) / 1e9) if args.mode == "trace" else None,
         "faulted_chains": bad,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
