@@ -156,6 +156,19 @@ int tmh_engine_destroy(struct tmh_engine* eng);
 /* the kernel path the engine resolved (TMH_PATH_SEQUENTIAL or TMH_PATH_TIME_PARALLEL) */
 int tmh_engine_path(const struct tmh_engine* eng);
 
+/* Per-chain hourly cloud-cover shape tables (a lat/lon sweep with one table per
+ * site).  Replaces, for every chain, the single table of
+ * tmh_params.shapes / shape_is_t that get_distributions_from_shapes_file loads
+ * (cloud_cover_hourly.py:269-288) and get_cloud_cover draws from (:290-316);
+ * the bin edges stay tmh_params.edges.  shapes: device [n_chains][6][4] fp64
+ * (loc, scale, kappa, df per bin), is_t: device [n_chains][6] int32 or NULL
+ * (then tmh_params.shape_is_t).  Row i serves the chain at index i of the
+ * tmh_init / tmh_run batch (chain0 + i), so n_chains must cover the batch.
+ * The buffers are read by every later launch and must outlive them; shapes ==
+ * NULL restores the single table.  Both cc modes and both kernel paths. */
+int tmh_set_shape_tables(struct tmh_engine* eng, const double* shapes, const int32_t* is_t,
+                         uint32_t n_chains);
+
 /* ClearskyindexModel.__init__ for chains [chain0, chain0 + n_chains): the 14+
  * constructor draws and CloudCoverBinary's first cloud.  `inj` may be NULL
  * (keyed mode). */

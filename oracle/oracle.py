@@ -57,6 +57,7 @@ def lib():
         L.orc_run.restype = C.c_int
         L.orc_run.argtypes = [p, C.c_uint64, C.c_uint32, C.c_uint32, p, p, p, C.c_uint64,
                               p, p, p, p, p, p, p, p]
+        L.orc_set_tables.argtypes = [p, p, C.c_uint32]
         _lib = L
     return _lib
 
@@ -105,8 +106,11 @@ def _ptr(a):
 
 
 def run(mp, chain0, n_chains, n_steps, start, tz=None, inj=None, n_threads=1,
-        outputs=("csi", "covered", "pv", "meter", "residual", "pos")):
-    """Run the oracle; returns dict of time-major [n_steps, n_chains] arrays + status/init."""
+        outputs=("csi", "covered", "pv", "meter", "residual", "pos"), tables=None):
+    """Run the oracle; returns dict of time-major [n_steps, n_chains] arrays + status/init.
+
+    tables: optional per-chain shape tables (shapes [n_chains, 6, 4] float64,
+    is_t [n_chains, 6] int32); chain c draws its hourly cloud cover from row c."""
     P = make_params(mp, n_threads)
     cal, utc = calendar(start, n_steps, tz)
     out = {}
@@ -121,9 +125,18 @@ def run(mp, chain0, n_chains, n_steps, start, tz=None, inj=None, n_threads=1,
         inj = np.ascontiguousarray(inj, dtype=np.float64)
         assert inj.shape[0] == n_chains
         stride = inj.shape[1]
-    rc = lib().orc_run(C.byref(P), chain0, n_chains, n_steps, _ptr(cal), _ptr(utc), _ptr(inj), stride,
-                       _ptr(out["csi"]), _ptr(out["covered"]), _ptr(out["pv"]), _ptr(out["meter"]),
-                       _ptr(out["residual"]), _ptr(out["pos"]), _ptr(status), _ptr(init))
+    if tables is not None:
+        tsh = np.ascontiguousarray(tables[0], dtype=np.float64)
+        tit = np.ascontiguousarray(tables[1], dtype=np.int32)
+        assert tsh.shape == (n_chains, 6, 4) and tit.shape == (n_chains, 6)
+        lib().orc_set_tables(_ptr(tsh), _ptr(tit), n_chains)
+    try:
+        rc = lib().orc_run(C.byref(P), chain0, n_chains, n_steps, _ptr(cal), _ptr(utc), _ptr(inj), stride,
+                           _ptr(out["csi"]), _ptr(out["covered"]), _ptr(out["pv"]), _ptr(out["meter"]),
+                           _ptr(out["residual"]), _ptr(out["pos"]), _ptr(status), _ptr(init))
+    finally:
+        if tables is not None:
+            lib().orc_set_tables(None, None, 0)
     if rc != 0:
         raise RuntimeError(f"orc_run failed: {rc}")
     res = {k: v for k, v in out.items() if v is not None}

@@ -310,6 +310,8 @@ typedef struct {
     double sc[ORC_SIGMA_CAP], sl[ORC_SIGMA_CAP];
     double mstate;                /* markov-mode persistent hourly state */
     uint64_t ncalls;              /* next_cloud calls so far (keyed counter of CLOUD draws) */
+    const double* tab;            /* per-chain shape table [6][4] (NULL: orc_params.shapes) */
+    const int32_t* tab_t;
     int status;
     /* rng */
     uint64_t chain;
@@ -338,16 +340,30 @@ static void push(double s[2], double v) { s[0] = s[1]; s[1] = v; }
 
 /* hourly cloud cover draw: get_cloud_cover(distributions) (cloud_cover_hourly.py:309-316).
  * faithful: a fresh generator per call -> state 1.0 (clearskyindexmodel.py:61-63). */
+/* optional per-chain shape tables (a lat/lon sweep, C5): chain c (index within
+ * the orc_run call) draws from g_tab[c] when set, else from orc_params.shapes */
+static const double* g_tab;
+static const int32_t* g_tab_t;
+static uint32_t g_tab_n;
+void orc_set_tables(const double* shapes /* [n][6][4] */, const int32_t* is_t /* [n][6] */, uint32_t n)
+{
+    g_tab = shapes;
+    g_tab_t = is_t;
+    g_tab_n = n;
+}
+
 static double draw_cc(const ctx_t* X, chain_t* ch, double u)
 {
     const orc_params* P = X->P;
     double state = P->cc_mode == 1 ? ch->mstate : 1.0;
     int bin = 0;
     while (bin < 5 && P->edges[bin] < state) ++bin;        /* searchsorted(bins, state), side=left */
+    const double* sh = ch->tab ? ch->tab + 4 * bin : P->shapes[bin];
+    const int is_t = ch->tab ? ch->tab_t[bin] : P->shape_is_t[bin];
     double v;
-    if (P->shape_is_t[bin]) v = orc_stdtrit(P->shapes[bin][3], u);
-    else v = orc_al_ppf(u, P->shapes[bin][2]);
-    v = v * P->shapes[bin][1] + P->shapes[bin][0];       /* scipy rvs: vals * scale + loc */
+    if (is_t) v = orc_stdtrit(sh[3], u);
+    else v = orc_al_ppf(u, sh[2]);
+    v = v * sh[1] + sh[0];                               /* scipy rvs: vals * scale + loc */
     double x = state + v;
     x = x < 0.0 ? 0.0 : (x > 1.0 ? 1.0 : x);              /* np.clip(., 0, 1) */
     if (P->cc_mode == 1) ch->mstate = x;
@@ -726,6 +742,10 @@ int orc_run(const orc_params* P, uint64_t chain0, uint32_t n_chains, uint32_t n_
     for (uint32_t c = 0; c < n_chains; ++c) {
         chain_t* ch = (chain_t*)calloc(1, sizeof(chain_t));
         ch->chain = chain0 + c;
+        if (g_tab && c < g_tab_n) {
+            ch->tab = g_tab + 24 * (size_t)c;
+            ch->tab_t = g_tab_t + 6 * (size_t)c;
+        }
         if (inj) { ch->inj = inj + (uint64_t)c * inj_stride; ch->inj_len = inj_stride; }
         fields_t t0 = {cal[0], cal[1], cal[2], cal[3]};
         chain_init(&X, ch, &t0);

@@ -20,10 +20,11 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-def _sim(n, start, tz=None, mp=None, prec="fp64", chain0=0, inj=None, horizon=None, kernel_path="auto"):
+def _sim(n, start, tz=None, mp=None, prec="fp64", chain0=0, inj=None, horizon=None, kernel_path="auto", tables=None):
     from tmhpvsim_amd.engine import BatchedSim
     return BatchedSim(n, start, tz=tz, params=mp or ModelParams(), precision=prec, chain0=chain0,
-                      device="cuda:0", injected=inj, horizon=horizon or 400 * 86400, kernel_path=kernel_path)
+                      device="cuda:0", injected=inj, horizon=horizon or 400 * 86400, kernel_path=kernel_path,
+                      shape_tables=tables)
 
 
 def _np(t):
@@ -117,11 +118,13 @@ def test_keyed_vs_oracle(start, tz, steps, variant, prec):
             assert err.max() <= tol, (f, _where(err, tol), got["pv"][np.unravel_index(np.argmax(err), err.shape)])
 
 
-def test_markov_keyed_vs_oracle():
+@pytest.mark.parametrize("path", ["sequential", "time_parallel"])
+def test_markov_keyed_vs_oracle(path):
     mp = ModelParams(cc_mode=CC_MARKOV, seed=77)
     n, steps, start = 128, 43200, "2019-09-05 06:00:00"
     ref = O.run(mp, 0, n, steps, start, tz="Europe/Berlin", n_threads=8)
-    sim = _sim(n, start, tz="Europe/Berlin", mp=mp, horizon=steps)
+    sim = _sim(n, start, tz="Europe/Berlin", mp=mp, horizon=steps, kernel_path=path)
+    assert sim.path == path
     out = sim.run(steps)
     np.testing.assert_array_equal(sim.status(), ref["status"])
     ok = ref["status"] == 0
@@ -131,6 +134,38 @@ def test_markov_keyed_vs_oracle():
     for f in ("csi", "pv", "residual"):
         err = _err(f, got, rf)
         assert err.max() <= 1e-12, (f, _where(err, 1e-12), got["pv"][np.unravel_index(np.argmax(err), err.shape)])
+
+
+@pytest.mark.parametrize("path", ["sequential", "time_parallel"])
+@pytest.mark.parametrize("markov", [True, False])
+def test_site_tables_vs_oracle(markov, path):
+    """Per-chain shape tables (C5's lat/lon sweep: one mc_dist_shapes table x U(0.9, 1.1) per
+    site) through tmh_set_shape_tables, both cc modes and both kernel paths, against the oracle
+    with the same tables; chains > n_tab are refused."""
+    from tmhpvsim_amd.params import site_shape_tables
+    mp = ModelParams(cc_mode=CC_MARKOV if markov else 0, seed=0x7AB1E + 1)
+    n, steps, start = 128, 30000, "2019-09-05 04:00:00"
+    tab = site_shape_tables(n, site0=3000)
+    ref = O.run(mp, 3000, n, steps, start, tz="Europe/Berlin", n_threads=8, tables=tab)
+    sim = _sim(n, start, tz="Europe/Berlin", mp=mp, chain0=3000, horizon=steps, kernel_path=path, tables=tab)
+    out = sim.run(steps, window=10000)
+    np.testing.assert_array_equal(sim.status(), ref["status"])
+    ok = ref["status"] == 0
+    np.testing.assert_array_equal(_np(out["covered"])[:, ok], ref["covered"][:, ok])
+    got = {f: _np(out[f])[:, ok] for f in ("csi", "pv", "meter", "residual")}
+    rf = {f: ref[f][:, ok] for f in ("csi", "pv", "meter", "residual")}
+    for f in ("csi", "pv", "residual"):
+        err = _err(f, got, rf)
+        assert err.max() <= 1e-12, (f, _where(err, 1e-12))
+    plain = O.run(mp, 3000, n, steps, start, tz="Europe/Berlin", n_threads=8, outputs=("covered",))
+    assert (plain["covered"][:, ok] != ref["covered"][:, ok]).any()    # the tables are in effect
+    rc = sim.L.tmh_init(sim._eng, _ptr_of(sim.state), 0, n + 1, None, sim._stream())   # batch > tables
+    assert rc != 0 and b"shape tables" in sim.L.tmh_last_error()
+
+
+def _ptr_of(t):
+    import ctypes as C
+    return C.c_void_p(t.data_ptr())
 
 
 def test_geometry_table_vs_oracle():
@@ -177,26 +212,32 @@ def test_window_and_partition_invariance():
         assert _same(ra[f], torch.cat([r0[f], r1[f]], dim=1)), f
 
 
-@pytest.mark.parametrize("prec", ["fp32", "fp64"])
-def test_time_parallel_equals_sequential(prec):
-    """P1 segments + P2 (chain x 256 s) expansion == one-lane-per-chain sequential kernel, bit for bit,
-    over uneven windows crossing midnight and the DST fall-back (state carried between windows)."""
+@pytest.mark.parametrize("prec,markov", [("fp32", False), ("fp64", False), ("fp32", True)])
+def test_time_parallel_equals_sequential(prec, markov):
+    """P1 segments + P2 (chain x 128 s) expansion == one-lane-per-chain sequential kernel, bit for bit,
+    over uneven windows crossing midnight and the DST fall-back (state carried between windows);
+    markov: the hourly Markov cc (markov_cc_kernel) with per-site tables."""
+    from tmhpvsim_amd.params import site_shape_tables
     start, n = "2019-10-26 21:00:00", 192
     windows = [7001, 30000, 1, 20000]
     steps = sum(windows)
-    a = _sim(n, start, tz="Europe/Berlin", prec=prec, horizon=steps, kernel_path="time_parallel")
-    b = _sim(n, start, tz="Europe/Berlin", prec=prec, horizon=steps, kernel_path="sequential")
+    mp = ModelParams(cc_mode=CC_MARKOV) if markov else None
+    tab = site_shape_tables(n) if markov else None
+    a = _sim(n, start, tz="Europe/Berlin", mp=mp, prec=prec, horizon=steps, kernel_path="time_parallel", tables=tab)
+    b = _sim(n, start, tz="Europe/Berlin", mp=mp, prec=prec, horizon=steps, kernel_path="sequential", tables=tab)
     assert a.path == "time_parallel" and b.path == "sequential"
     for w in windows:
         ra, rb = a.run(w, window=w), b.run(w, window=w)
         for f in ("csi", "covered", "pv", "meter", "residual"):
             assert _same(ra[f], rb[f]), (w, f)
     np.testing.assert_array_equal(a.status(), b.status())
+    ok = torch.as_tensor(a.status() == 0, device="cuda:0")   # a faulted chain's state is frozen, not defined
     for f in ("sb_cc", "sa_cc", "sb_clear_day", "sa_clear_day", "sb_cloudy_noise", "sa_clear_noise", "sa_ws",
-              "cloud_length", "clear_length", "sec", "sigma_len"):
-        assert _same(a.state_field(f), b.state_field(f)), f
+              "cloud_length", "clear_length", "sec", "sigma_len", "markov_state"):
+        assert _same(a.state_field(f)[ok], b.state_field(f)[ok]), f
     L = a.state_field("sigma_len").long()
     live = torch.arange(a.state_field("sigma_cloud").shape[1], device="cuda:0")[None, :] < L[:, None]
+    live &= ok[:, None]
     for f in ("sigma_cloud", "sigma_clear"):   # entries past len(sigma) are dead storage
         assert torch.equal(a.state_field(f)[live], b.state_field(f)[live]), f
 

@@ -1,0 +1,59 @@
+"""Per-site shape tables on the CPU: the host-side table generator
+(tmhpvsim_amd.params.site_shape_tables) and the oracle's per-chain table path
+that the GPU parity tests (test_gpu_parity.py::test_site_tables_vs_oracle)
+compare against."""
+import numpy as np
+
+from oracle import oracle as O
+from oracle import philox as P
+from tmhpvsim_amd.params import CC_MARKOV, SHAPES, SHAPE_IS_T, ModelParams, _philox4x32_10, site_shape_tables
+
+
+def test_host_philox_matches_known_answers():
+    ctr = np.array([[0, 0, 0, 0], [0xFFFFFFFF] * 4, [0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344]],
+                   dtype=np.uint32)
+    key = np.array([[0, 0], [0xFFFFFFFF] * 2, [0xA4093822, 0x299F31D0]], dtype=np.uint32)
+    np.testing.assert_array_equal(_philox4x32_10(ctr, key), P.philox4x32_10(ctr, key))
+    # Random123 kat_vectors philox4x32_10
+    assert [int(x) for x in _philox4x32_10(ctr[1:2], key[1:2])[0]] == [0x408F276D, 0x41C83B0E, 0xA20BC7C6,
+                                                                        0x6D5451FD]
+
+
+def test_site_tables_shape_range_and_partition():
+    tab, is_t = site_shape_tables(1000, site0=0)
+    base = np.array(SHAPES)
+    f = tab / base[None]
+    fin = np.isfinite(base)
+    assert np.isnan(tab[:, ~fin]).all()
+    assert (f[:, fin] >= 0.9).all() and (f[:, fin] <= 1.1).all()
+    assert abs(f[:, fin].mean() - 1.0) < 3e-3 and f[:, fin].std() > 0.05
+    np.testing.assert_array_equal(is_t, np.broadcast_to(SHAPE_IS_T, (1000, 6)))
+    part, _ = site_shape_tables(300, site0=700)                 # global site id keyed
+    np.testing.assert_array_equal(part, tab[700:])
+    assert (tab[:, 1, 1] > 0).all() and (tab[:, 2, 3] > 0).all()   # scale, Student-t df stay positive
+
+
+def test_oracle_tables_equal_to_default_change_nothing():
+    mp = ModelParams(cc_mode=CC_MARKOV, seed=5, with_pv=False)
+    n, steps, start = 16, 7200, "2019-09-05 08:00:00"
+    same = (np.broadcast_to(np.array(SHAPES), (n, 6, 4)).copy(), np.broadcast_to(SHAPE_IS_T, (n, 6)).astype(np.int32))
+    a = O.run(mp, 0, n, steps, start, tz="Europe/Berlin", outputs=("csi", "covered"))
+    b = O.run(mp, 0, n, steps, start, tz="Europe/Berlin", outputs=("csi", "covered"), tables=same)
+    np.testing.assert_array_equal(a["covered"], b["covered"])
+    np.testing.assert_array_equal(a["csi"], b["csi"])
+
+
+def test_oracle_tables_are_per_chain():
+    """Chain c with table row c == the single-table run of chain c with params.shapes = row c."""
+    n, steps, start = 6, 7200, "2019-09-05 08:00:00"
+    for markov in (True, False):
+        mp = ModelParams(cc_mode=CC_MARKOV if markov else 0, seed=9, with_pv=False)
+        tab, is_t = site_shape_tables(n, site0=40)
+        r = O.run(mp, 40, n, steps, start, tz="Europe/Berlin", outputs=("csi", "covered"), tables=(tab, is_t))
+        for c in (0, 3, 5):
+            mc = ModelParams(cc_mode=mp.cc_mode, seed=9, with_pv=False, shapes=tab[c].copy())
+            one = O.run(mc, 40 + c, 1, steps, start, tz="Europe/Berlin", outputs=("csi", "covered"))
+            np.testing.assert_array_equal(one["covered"][:, 0], r["covered"][:, c])
+            np.testing.assert_array_equal(one["csi"][:, 0], r["csi"][:, c])
+        plain = O.run(mp, 40, n, steps, start, tz="Europe/Berlin", outputs=("csi",))
+        assert not np.array_equal(plain["csi"], r["csi"])

@@ -137,8 +137,8 @@ __global__ __launch_bounds__(256) void init_kernel(KParams kp, StateView st, uin
     }
     double u[12];
     for (int d = 0; d < 12; ++d) u[d] = dr.one(ch, 0, TAG_INIT, (uint32_t)(d >> 1), d & 1);
-    ch.s.b[S_CC] = draw_cc(kp, ch, u[0]);
-    ch.s.a[S_CC] = draw_cc(kp, ch, u[1]);
+    ch.s.b[S_CC] = draw_cc(kp, c, ch, u[0]);
+    ch.s.a[S_CC] = draw_cc(kp, c, ch, u[1]);
     ch.s.b[S_CLEAR_DAY] = normal(u[2], 0.99, 0.08);
     ch.s.a[S_CLEAR_DAY] = normal(u[3], 0.99, 0.08);
     bool name_error = false;
@@ -380,8 +380,32 @@ __global__ __launch_bounds__(256) void event_draws_kernel(DrawParams dp, uint64_
     }
     if (fl & FL_HOUR) {
         const U4 u = keyed_block(dp.seed, chain, step, TAG_BOUNDARY, 1);
-        o[0] = cc_faithful(dp, u52(u.x, u.y));
+        if (!dp.markov) o[0] = cc_faithful(dp, c, u52(u.x, u.y));
         o[3 * (size_t)n] = normal(u52(u.z, u.w), 0.99, 0.08);
+    }
+}
+
+// markov-mode hourly cloud cover (cloud_cover_hourly.py:309-316 as one long-lived
+// generator per chain): the only sequential dependence in the window is the
+// hour-to-hour cc state, 24 draws a day, so one lane per chain walks the
+// window's hour events in order and fills evd[e][0] for the time-parallel
+// kernels.  The state is the last drawn cc, i.e. sa[S_CC] (init and every
+// _next_hour push the markov state), so nothing extra is carried over.
+__global__ __launch_bounds__(256) void markov_cc_kernel(KParams kp, StateView st, uint64_t chain0, uint32_t n,
+                                                        uint32_t nsteps, const int2* __restrict__ events,
+                                                        const uint32_t* __restrict__ n_events, double* evd)
+{
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const uint64_t chain = chain0 + c;
+    const uint32_t ne = min(*n_events, ev_cap_dev(nsteps));
+    double state = st.mstate[c];
+    for (uint32_t e = 0; e < ne; ++e) {
+        const int2 ev = events[e];
+        if (!(ev.y & FL_HOUR)) continue;
+        const U4 u = keyed_block(kp.seed, chain, (uint64_t)ev.x, TAG_BOUNDARY, 1);
+        state = draw_cc_from(kp, c, state, u52(u.x, u.y));
+        evd[(size_t)e * 4 * n + c] = state;
     }
 }
 
@@ -511,7 +535,7 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
                 }
                 if (fl & FL_HOUR) {                    // _next_hour (advances clear_day)
                     dr.two(ch, step, TAG_BOUNDARY, 1, u0, u1);
-                    push(ch.s, S_CC, draw_cc(kp, ch, u0));
+                    push(ch.s, S_CC, draw_cc(kp, c, ch, u0));
                     push(ch.s, S_CLEAR_DAY, normal(u1, 0.99, 0.08));
                 }
                 if (fl & FL_MIN) {                     // _next_min
@@ -1177,7 +1201,7 @@ __global__ __launch_bounds__(256, TMH_EXP_WAVES) void expand_kernel(KParams kp, 
 template <typename R>
 __global__ __launch_bounds__(256) void commit_kernel(StateView st, uint32_t n, SegView sg, StatsView sv, MinuteCtx mc0,
                                                      const uint32_t* __restrict__ n_events,
-                                                     const BlockDesc* __restrict__ desc_end)
+                                                     const BlockDesc* __restrict__ desc_end, int markov)
 {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n) return;
@@ -1216,6 +1240,7 @@ __global__ __launch_bounds__(256) void commit_kernel(StateView st, uint32_t n, S
     }
     st.sb[S_WS][c] = sg.end_p1[2 * (size_t)n + c];
     st.sa[S_WS][c] = sg.end_p1[3 * (size_t)n + c];
+    if (markov) st.mstate[c] = sp.a[S_CC];   // the markov state is the last hourly draw
 }
 
 __global__ void probe_kernel(int fn, double a, const double* x, double* out, uint32_t n)
@@ -1386,7 +1411,8 @@ struct tmh_engine {
     DrawParams dp;
     GParams gp;
     int device;
-    int path;   // resolved kernel path: 1 sequential, 2 time-parallel
+    int path;          // resolved kernel path: 1 sequential, 2 time-parallel
+    uint32_t n_tab = 0;   // rows of the per-chain shape tables (0: none)
     // kernel timing (tmh_profile_*): event pairs per kernel, read and recycled
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[TMH_K_COUNT];
@@ -1478,11 +1504,11 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
     // memoryless (faithful) hourly draw, and whole-minute UTC offsets
     bool minutes = ((clock->local0 - clock->utc0) % 60) == 0;
     for (int i = 0; i < clock->n_shifts; ++i) minutes = minutes && (clock->shift_delta[i] % 60) == 0;
-    const bool tp_ok = p->rng_mode == TMH_RNG_KEYED && p->cc_mode == TMH_CC_FAITHFUL && minutes;
+    const bool tp_ok = p->rng_mode == TMH_RNG_KEYED && minutes;
     int path = p->kernel_path == TMH_PATH_AUTO ? (tp_ok ? TMH_PATH_TIME_PARALLEL : TMH_PATH_SEQUENTIAL)
                                                : p->kernel_path;
     if (path == TMH_PATH_TIME_PARALLEL && !tp_ok)
-        return fail(TMH_E_INVAL, "kernel_path time-parallel needs keyed rng, faithful cc mode, whole-minute offsets");
+        return fail(TMH_E_INVAL, "kernel_path time-parallel needs keyed rng and whole-minute offsets");
     int ndev = 0;
     if (int rc = hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount")) return rc;
     if (device < 0 || device >= ndev) return fail(TMH_E_INVAL, "device %d out of range (%d devices)", device, ndev);
@@ -1554,6 +1580,8 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
     d.fb_k = d.fb_is_t ? p->shapes[fb][3] : p->shapes[fb][2];
     d.fb_scale = p->shapes[fb][1];
     d.fb_loc = p->shapes[fb][0];
+    d.fb_bin = fb;
+    d.markov = p->cc_mode == TMH_CC_MARKOV;
     e->device = device;
     e->path = path;
     *out = e;
@@ -1567,6 +1595,23 @@ int tmh_engine_destroy(struct tmh_engine* eng)
 }
 
 int tmh_engine_path(const struct tmh_engine* eng) { return eng ? eng->path : TMH_E_INVAL; }
+
+int tmh_set_shape_tables(struct tmh_engine* eng, const double* shapes, const int32_t* is_t, uint32_t n_chains)
+{
+    if (!eng) return fail(TMH_E_INVAL, "NULL engine");
+    if (shapes && n_chains == 0) return fail(TMH_E_INVAL, "per-chain shape tables with n_chains 0");
+    eng->kp.tab = eng->dp.tab = shapes;
+    eng->kp.tab_t = eng->dp.tab_t = shapes ? is_t : nullptr;
+    eng->n_tab = shapes ? n_chains : 0;
+    return TMH_OK;
+}
+
+static int check_tables(const tmh_engine* eng, uint32_t n_chains)
+{
+    if (eng->kp.tab && n_chains > eng->n_tab)
+        return fail(TMH_E_INVAL, "batch of %u chains exceeds the %u per-chain shape tables", n_chains, eng->n_tab);
+    return TMH_OK;
+}
 
 #ifdef TMH_DIAG_P1
 int tmh_diag_p1(uint64_t* out, uint32_t n)   // diagnostic build only
@@ -1610,6 +1655,7 @@ int tmh_init(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
     if (n_chains == 0) return TMH_OK;
     if (eng->kp.rng_mode == TMH_RNG_INJECTED && (!inj || !inj->u || inj->stride < inj->len))
         return fail(TMH_E_INVAL, "injected mode needs a stream with stride >= len");
+    if (int rc = check_tables(eng, n_chains)) return rc;
     if (int rc = hip_check(hipSetDevice(eng->device), "hipSetDevice")) return rc;
     const tmh_clock& ck = eng->gp.clock;
     int64_t sod = ck.local0 % 86400;
@@ -1662,6 +1708,7 @@ int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
         return fail(TMH_E_INVAL, "trace ld %llu < n_chains %u", (unsigned long long)trace->ld, n_chains);
     if (stats && stats->hist && (stats->n_bins == 0 || stats->n_bins > 16384 || !(stats->hi > stats->lo)))
         return fail(TMH_E_INVAL, "bad histogram spec (n_bins %u in [1,16384], hi > lo)", stats->n_bins);
+    if (int rc = check_tables(eng, n_chains)) return rc;
     const bool tp = eng->path == TMH_PATH_TIME_PARALLEL;
     if (tp && (!scratch || scratch_bytes < tmh_scratch_bytes(n_chains, n_steps)))
         return fail(TMH_E_INVAL, "scratch too small: %zu < %zu", scratch_bytes, tmh_scratch_bytes(n_chains, n_steps));
@@ -1703,6 +1750,9 @@ int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
     hipEvent_t t_step = eng->mark(s);
     hipLaunchKernelGGL(event_draws_kernel, dim3(sg.evcap, cb), dim3(256), 0, s, eng->dp, chain0, n_chains, n_steps,
                        pv.events, pv.n_events, sg.evd);
+    if (eng->dp.markov)
+        hipLaunchKernelGGL(markov_cc_kernel, dim3(cb), dim3(256), 0, s, eng->kp, v, chain0, n_chains, n_steps,
+                           pv.events, pv.n_events, sg.evd);
     hipEvent_t t_cand = eng->mark(s);
     hipLaunchKernelGGL(candidates_kernel, dim3(cb, sg.kcap), dim3(256), 0, s, eng->dp, v, chain0, n_chains, sg);
     eng->close(TMH_K_CANDIDATES, t_cand, s);
@@ -1735,10 +1785,10 @@ int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
     const MinuteCtx mc{eng->dp, chain0, step0, first_minute_host(utc0, step0), pv.events, 0, pv.tab64};
     if (f64)
         hipLaunchKernelGGL(commit_kernel<double>, dim3(cb), dim3(256), 0, s, v, n_chains, sg, sv, mc, pv.n_events,
-                           pv.desc + nblk_of(n_steps));
+                           pv.desc + nblk_of(n_steps), eng->dp.markov);
     else
         hipLaunchKernelGGL(commit_kernel<float>, dim3(cb), dim3(256), 0, s, v, n_chains, sg, sv, mc, pv.n_events,
-                           pv.desc + nblk_of(n_steps));
+                           pv.desc + nblk_of(n_steps), eng->dp.markov);
     eng->close(TMH_K_STEP, t_step, s);
     return hip_check(hipGetLastError(), "commit_kernel launch");
 }

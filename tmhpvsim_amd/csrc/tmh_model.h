@@ -32,6 +32,8 @@ struct KParams {
     double temp_air, wind;                      // sapm_celltemp inputs (pvmodel.py:69-70)
     double tmod_k;                              // exp(a + b * wind): constant for the run (wind fixed at 0)
     PVF pvf;                                    // fp32 copies for the fp32 chain
+    const double* tab;                          // per-chain shape tables [n][6][4] (NULL: shapes)
+    const int32_t* tab_t;                       // per-chain Student-t flags [n][6] (NULL: is_t)
 };
 
 struct GParams {
@@ -173,21 +175,39 @@ __device__ __forceinline__ double minute_noise(double u, double s0, double s1, d
 }
 
 // hourly cloud cover: next(get_cloud_cover(distributions)) (cloud_cover_hourly.py:309-316);
-// faithful = a fresh generator per draw, i.e. state 1.0 (clearskyindexmodel.py:61-63)
-__device__ __forceinline__ double draw_cc_from(const KParams& kp, double state, double u)
+// faithful = a fresh generator per draw, i.e. state 1.0 (clearskyindexmodel.py:61-63).
+// Chain c (index within the launch) draws from its own table when per-chain
+// tables are set (tmh_set_shape_tables: a lat/lon sweep, C5).
+__device__ __forceinline__ double draw_cc_from(const KParams& kp, uint32_t c, double state, double u)
 {
     int bin = 0;
     while (bin < 5 && kp.edges[bin] < state) ++bin;   // np.searchsorted(bins, state)
-    double v = kp.is_t[bin] ? stdtrit(kp.shapes[bin][3], u) : al_ppf(u, kp.shapes[bin][2]);
-    v = v * kp.shapes[bin][1] + kp.shapes[bin][0];   // scipy rvs: vals * scale + loc
+    double loc, scale, kappa, df;
+    int is_t;
+    if (kp.tab) {
+        const double* sh = kp.tab + (size_t)c * 24 + 4 * bin;
+        loc = sh[0];
+        scale = sh[1];
+        kappa = sh[2];
+        df = sh[3];
+        is_t = kp.tab_t ? kp.tab_t[(size_t)c * 6 + bin] : kp.is_t[bin];
+    } else {
+        loc = kp.shapes[bin][0];
+        scale = kp.shapes[bin][1];
+        kappa = kp.shapes[bin][2];
+        df = kp.shapes[bin][3];
+        is_t = kp.is_t[bin];
+    }
+    double v = is_t ? stdtrit(df, u) : al_ppf(u, kappa);
+    v = v * scale + loc;                              // scipy rvs: vals * scale + loc
     const double x = state + v;
     return x < 0.0 ? 0.0 : (x > 1.0 ? 1.0 : x);      // np.clip(., 0, 1)
 }
 
-__device__ __forceinline__ double draw_cc(const KParams& kp, Chain& ch, double u)
+__device__ __forceinline__ double draw_cc(const KParams& kp, uint32_t c, Chain& ch, double u)
 {
     const double state = kp.cc_mode == TMH_CC_MARKOV ? ch.mstate : 1.0;
-    const double x = draw_cc_from(kp, state, u);
+    const double x = draw_cc_from(kp, c, state, u);
     if (kp.cc_mode == TMH_CC_MARKOV) ch.mstate = x;
     return x;
 }
@@ -275,14 +295,26 @@ struct DrawParams {
     uint64_t seed;
     double alpha, delta, expo, sqrt09;
     double fb_k, fb_scale, fb_loc;   // the bin a fresh generator (state 1.0) draws from
-    int32_t fb_is_t, pad;
+    int32_t fb_is_t, fb_bin;
+    const double* tab;               // per-chain shape tables (KParams::tab)
+    const int32_t* tab_t;
+    int32_t markov, pad;             // cc_mode markov: hourly draws come from markov_cc_kernel
 };
 
 // faithful hourly cloud cover: a fresh get_cloud_cover generator (state 1.0) per draw
-__device__ __forceinline__ double cc_faithful(const DrawParams& dp, double u)
+__device__ __forceinline__ double cc_faithful(const DrawParams& dp, uint32_t c, double u)
 {
-    double v = dp.fb_is_t ? stdtrit(dp.fb_k, u) : al_ppf(u, dp.fb_k);
-    v = v * dp.fb_scale + dp.fb_loc;
+    double k = dp.fb_k, scale = dp.fb_scale, loc = dp.fb_loc;
+    int is_t = dp.fb_is_t;
+    if (dp.tab) {
+        const double* sh = dp.tab + (size_t)c * 24 + 4 * dp.fb_bin;
+        if (dp.tab_t) is_t = dp.tab_t[(size_t)c * 6 + dp.fb_bin];
+        k = is_t ? sh[3] : sh[2];
+        scale = sh[1];
+        loc = sh[0];
+    }
+    double v = is_t ? stdtrit(k, u) : al_ppf(u, k);
+    v = v * scale + loc;
     const double x = 1.0 + v;
     return x < 0.0 ? 0.0 : (x > 1.0 ? 1.0 : x);
 }

@@ -42,10 +42,14 @@ class BatchedSim:
     chain0 : global id of the first chain (keyed RNG -> partition-independent results)
     injected : optional device tensor [n_chains, L] of uniforms (RNG_INJECTED mode)
     horizon : maximum number of steps this object will run (sizes the DST table)
+    shape_tables : optional per-chain hourly cloud-cover tables (shapes [n, 6, 4],
+        is_t [n, 6]; e.g. params.site_shape_tables) in place of params.shapes —
+        one table per site of a lat/lon sweep (tmh_set_shape_tables)
     """
 
     def __init__(self, n_chains, start, tz=None, params: ModelParams | None = None, precision="fp32",
-                 chain0=0, device=None, injected=None, horizon=400 * 86400, kernel_path="auto"):
+                 chain0=0, device=None, injected=None, horizon=400 * 86400, kernel_path="auto",
+                 shape_tables=None):
         torch = _torch()
         L = _lib.load()
         self.L = L
@@ -79,6 +83,20 @@ class BatchedSim:
                 raise ValueError("injected must have one row per chain")
             self.injected = inj
             self._us = _lib.UStream(inj.data_ptr(), inj.shape[1], inj.shape[1])
+        self.tables = None
+        if shape_tables is not None:
+            sh, it = shape_tables if isinstance(shape_tables, tuple) else (shape_tables, None)
+            sh = torch.as_tensor(np.asarray(sh, dtype=np.float64) if not torch.is_tensor(sh) else sh,
+                                 dtype=torch.float64, device=self.device).contiguous()
+            if tuple(sh.shape) != (self.n, 6, 4):
+                raise ValueError(f"shape_tables must be [n_chains, 6, 4], got {tuple(sh.shape)}")
+            if it is not None:
+                it = torch.as_tensor(np.asarray(it) if not torch.is_tensor(it) else it,
+                                     dtype=torch.int32, device=self.device).contiguous()
+                if tuple(it.shape) != (self.n, 6):
+                    raise ValueError(f"shape_tables is_t must be [n_chains, 6], got {tuple(it.shape)}")
+            self.tables = (sh, it)   # the engine reads them on every launch: keep them alive
+            _lib.check(L.tmh_set_shape_tables(self._eng, _ptr(sh), _ptr(it) if it is not None else None, self.n))
         self.step = 0
         self.hist = None
         self.chain_acc = None

@@ -135,3 +135,41 @@ def load_shapes_csv(path):
         else:
             raise NotImplementedError(f"distribution {row['dist']!r} is not implemented")
     return shapes, is_t, edges
+
+
+def _philox4x32_10(ctr, key):
+    """Philox4x32-10 (Random123) on uint32 arrays ctr (..., 4), key (..., 2); host-side
+    table generation only (the kernels' Philox is tmhpvsim_amd/csrc/tmh_math.h)."""
+    M0, M1, W0, W1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57), np.uint32(0x9E3779B9), np.uint32(0xBB67AE85)
+    c = [ctr[..., i].astype(np.uint32) for i in range(4)]
+    k0, k1 = key[..., 0].astype(np.uint32), key[..., 1].astype(np.uint32)
+    lo32 = np.uint64(0xFFFFFFFF)
+    for r in range(10):
+        p0 = c[0].astype(np.uint64) * M0
+        p1 = c[2].astype(np.uint64) * M1
+        c = [((p1 >> np.uint64(32)).astype(np.uint32) ^ c[1] ^ k0), (p1 & lo32).astype(np.uint32),
+             ((p0 >> np.uint64(32)).astype(np.uint32) ^ c[3] ^ k1), (p0 & lo32).astype(np.uint32)]
+        if r < 9:
+            k0 = k0 + W0
+            k1 = k1 + W1
+    return np.stack(c, axis=-1)
+
+
+def site_shape_tables(n_sites, site0=0, shapes=SHAPES, shape_is_t=SHAPE_IS_T, seed=0x7AB1E, spread=0.1):
+    """Per-site hourly cloud-cover tables for a lat/lon sweep: every
+    parameter of the mc_dist_shapes.csv table (cloud_cover_hourly.py:282-288)
+    times U(1 - spread, 1 + spread), drawn per (site, entry) from Philox4x32-10
+    keyed by (seed, global site id), so a site's table does not depend on how
+    the sweep is partitioned.  Returns shapes [n, 6, 4] fp64 (NaN entries stay
+    NaN) and is_t [n, 6] int32, ready for BatchedSim(shape_tables=...)."""
+    sid = np.arange(site0, site0 + n_sites, dtype=np.uint64)
+    ctr = np.zeros((n_sites, 6, 4), dtype=np.uint32)
+    ctr[..., 0] = np.arange(6, dtype=np.uint32)[None, :]
+    ctr[..., 1] = (sid >> np.uint64(32)).astype(np.uint32)[:, None]
+    key = np.zeros((n_sites, 6, 2), dtype=np.uint32)
+    key[..., 0] = np.uint32(seed & 0xFFFFFFFF)
+    key[..., 1] = (sid & np.uint64(0xFFFFFFFF)).astype(np.uint32)[:, None]
+    u = (_philox4x32_10(ctr, key).astype(np.float64) + 0.5) * 2.0 ** -32
+    tab = np.asarray(shapes, dtype=np.float64)[None] * (1.0 - spread + 2.0 * spread * u)
+    is_t = np.broadcast_to(np.asarray(shape_is_t, dtype=np.int32), (n_sites, 6)).copy()
+    return np.ascontiguousarray(tab), is_t
