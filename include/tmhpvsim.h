@@ -169,6 +169,18 @@ int tmh_engine_path(const struct tmh_engine* eng);
 int tmh_set_shape_tables(struct tmh_engine* eng, const double* shapes, const int32_t* is_t,
                          uint32_t n_chains);
 
+/* Per-chain PV sites (the lat/lon sweep of SURVEY C5; the reference builds one
+ * PVModel per site, pvmodel.py:19-30).  sites: device [n_chains][8] fp64 rows in
+ * tmh_params.site order; columns 0-5 (latitude, longitude, altitude, tilt,
+ * surface azimuth, albedo) are per chain, temp_air and wind stay tmh_params'
+ * (pvmodel.py:69-70 fixes them).  linke: device [n_chains][12] monthly Linke
+ * turbidity or NULL (tmh_params.linke).  The clock, the boundary schedule and
+ * the sun's place stay in the shared plan; solar position, clear-sky GHI,
+ * DISC, POA and the SAPM factors are then evaluated per chain-second.  Row i
+ * serves the chain at index i of the batch; buffers must outlive the
+ * launches; sites == NULL restores the engine's single site. */
+int tmh_set_sites(struct tmh_engine* eng, const double* sites, const double* linke, uint32_t n_chains);
+
 /* ClearskyindexModel.__init__ for chains [chain0, chain0 + n_chains): the 14+
  * constructor draws and CloudCoverBinary's first cloud.  `inj` may be NULL
  * (keyed mode). */

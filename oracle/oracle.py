@@ -58,6 +58,7 @@ def lib():
         L.orc_run.argtypes = [p, C.c_uint64, C.c_uint32, C.c_uint32, p, p, p, C.c_uint64,
                               p, p, p, p, p, p, p, p]
         L.orc_set_tables.argtypes = [p, p, C.c_uint32]
+        L.orc_set_sites.argtypes = [p, p, C.c_uint32]
         _lib = L
     return _lib
 
@@ -106,11 +107,12 @@ def _ptr(a):
 
 
 def run(mp, chain0, n_chains, n_steps, start, tz=None, inj=None, n_threads=1,
-        outputs=("csi", "covered", "pv", "meter", "residual", "pos"), tables=None):
+        outputs=("csi", "covered", "pv", "meter", "residual", "pos"), tables=None, sites=None):
     """Run the oracle; returns dict of time-major [n_steps, n_chains] arrays + status/init.
 
     tables: optional per-chain shape tables (shapes [n_chains, 6, 4] float64,
-    is_t [n_chains, 6] int32); chain c draws its hourly cloud cover from row c."""
+    is_t [n_chains, 6] int32); chain c draws its hourly cloud cover from row c.
+    sites: optional per-chain PV sites [n_chains, 8] (or (sites, linke [n_chains, 12]))."""
     P = make_params(mp, n_threads)
     cal, utc = calendar(start, n_steps, tz)
     out = {}
@@ -130,6 +132,14 @@ def run(mp, chain0, n_chains, n_steps, start, tz=None, inj=None, n_threads=1,
         tit = np.ascontiguousarray(tables[1], dtype=np.int32)
         assert tsh.shape == (n_chains, 6, 4) and tit.shape == (n_chains, 6)
         lib().orc_set_tables(_ptr(tsh), _ptr(tit), n_chains)
+    if sites is not None:
+        ssi, sli = sites if isinstance(sites, tuple) else (sites, None)
+        ssi = np.ascontiguousarray(ssi, dtype=np.float64)
+        assert ssi.shape == (n_chains, 8)
+        if sli is not None:
+            sli = np.ascontiguousarray(sli, dtype=np.float64)
+            assert sli.shape == (n_chains, 12)
+        lib().orc_set_sites(_ptr(ssi), _ptr(sli), n_chains)
     try:
         rc = lib().orc_run(C.byref(P), chain0, n_chains, n_steps, _ptr(cal), _ptr(utc), _ptr(inj), stride,
                            _ptr(out["csi"]), _ptr(out["covered"]), _ptr(out["pv"]), _ptr(out["meter"]),
@@ -137,6 +147,8 @@ def run(mp, chain0, n_chains, n_steps, start, tz=None, inj=None, n_threads=1,
     finally:
         if tables is not None:
             lib().orc_set_tables(None, None, 0)
+        if sites is not None:
+            lib().orc_set_sites(None, None, 0)
     if rc != 0:
         raise RuntimeError(f"orc_run failed: {rc}")
     res = {k: v for k, v in out.items() if v is not None}

@@ -710,6 +710,20 @@ double orc_pv(const orc_params* P, int64_t utc, int doy, int leap, double csi)
     return pv_power(P, &g, csi);
 }
 
+/* optional per-chain PV sites (C5): chain c (index within the orc_run call)
+ * uses site columns 0-5 of g_sites[c] (temp_air and wind stay P's) and, when
+ * set, the monthly Linke turbidity g_site_linke[c]; its geometry is then
+ * evaluated per chain-step */
+static const double* g_sites;
+static const double* g_site_linke;
+static uint32_t g_sites_n;
+void orc_set_sites(const double* sites /* [n][8] */, const double* linke /* [n][12] or NULL */, uint32_t n)
+{
+    g_sites = sites;
+    g_site_linke = linke;
+    g_sites_n = n;
+}
+
 /* -------------------------------------------------------------------- run */
 /* cal: n_steps x 6 int32 = (day of month, hour, minute, second, day of year, leap) local fields.
  * Outputs time-major [step][chain]; any pointer may be NULL.
@@ -742,6 +756,14 @@ int orc_run(const orc_params* P, uint64_t chain0, uint32_t n_chains, uint32_t n_
     for (uint32_t c = 0; c < n_chains; ++c) {
         chain_t* ch = (chain_t*)calloc(1, sizeof(chain_t));
         ch->chain = chain0 + c;
+        orc_params Pc;
+        const orc_params* Ps = P;   /* the chain's PV site */
+        if (g_sites && c < g_sites_n) {
+            Pc = *P;
+            memcpy(Pc.site, g_sites + 8 * (size_t)c, 6 * sizeof(double));
+            if (g_site_linke) memcpy(Pc.linke, g_site_linke + 12 * (size_t)c, 12 * sizeof(double));
+            Ps = &Pc;
+        }
         if (g_tab && c < g_tab_n) {
             ch->tab = g_tab + 24 * (size_t)c;
             ch->tab_t = g_tab_t + 6 * (size_t)c;
@@ -807,7 +829,13 @@ int orc_run(const orc_params* P, uint64_t chain0, uint32_t n_chains, uint32_t n_
             if (pos_out) pos_out[o] = (uint32_t)ch->pos;
             double pv = NAN, meter = NAN;
             if (!ch->status) {
-                pv = P->with_pv ? pv_power(P, &G[s], csi) : 0.0;
+                if (P->with_pv && Ps != P) {
+                    geom_t gs;
+                    geometry(Ps, utc[s], cal[6 * s + 4], cal[6 * s + 5], &gs);
+                    pv = pv_power(Ps, &gs, csi);
+                } else {
+                    pv = P->with_pv ? pv_power(P, &G[s], csi) : 0.0;
+                }
                 double ue_unused, um;
                 step_u(P->seed, ch->chain, s, &ue_unused, &um);
                 meter = 9000 * um;

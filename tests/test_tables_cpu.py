@@ -57,3 +57,28 @@ def test_oracle_tables_are_per_chain():
             np.testing.assert_array_equal(one["csi"][:, 0], r["csi"][:, c])
         plain = O.run(mp, 40, n, steps, start, tz="Europe/Berlin", outputs=("csi",))
         assert not np.array_equal(plain["csi"], r["csi"])
+
+
+def test_site_grid_layout():
+    from tmhpvsim_amd.params import Site, site_grid
+    g = site_grid(256, 256)
+    assert g.shape == (65536, 8)
+    assert g[0, 0] == 35.0 and g[-1, 0] == 60.0 and g[0, 1] == -10.0 and g[-1, 1] == 30.0
+    np.testing.assert_array_equal(g[:, 3], g[:, 0])                  # tilt = latitude (pvmodel.py:25)
+    assert (g[:, 4] == 180.0).all() and (g[:, 6] == Site().temp_air).all()
+    assert g[1, 0] == 35.0 and g[256, 0] > 35.0                       # latitude-major
+
+
+def test_oracle_sites_equal_to_default_change_nothing():
+    mp = ModelParams(seed=21)
+    n, steps, start = 8, 3600, "2019-09-05 11:00:00"
+    sites = np.broadcast_to(mp.site.as_array(), (n, 8)).copy()
+    a = O.run(mp, 0, n, steps, start, tz="Europe/Berlin")
+    b = O.run(mp, 0, n, steps, start, tz="Europe/Berlin", sites=sites)
+    for k in ("csi", "pv", "residual"):
+        np.testing.assert_array_equal(a[k], b[k])
+    far = sites.copy()
+    far[:, 1] += 30.0                                                   # 2 h of solar time east
+    c = O.run(mp, 0, n, steps, start, tz="Europe/Berlin", sites=far)
+    np.testing.assert_array_equal(a["csi"], c["csi"])
+    assert not np.allclose(a["pv"], c["pv"])

@@ -184,7 +184,7 @@ __global__ __launch_bounds__(256) void init_kernel(KParams kp, StateView st, uin
 
 // ------------------------------------------------------------ plan kernels
 __global__ __launch_bounds__(256) void geom_kernel(GParams gp, int64_t step0, uint32_t n, double* tab64,
-                                                   float* tab32)
+                                                   float* tab32, double* sun)
 {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
@@ -203,56 +203,12 @@ __global__ __launch_bounds__(256) void geom_kernel(GParams gp, int64_t step0, ui
     if (hour != hourp) fl |= FL_HOUR;     // :123
     if (minute != minutep) fl |= FL_MIN;  // :125
     // ---- PV geometry (pvmodel.py:50-76; pvlib 0.6.3 model choices) ----
-    const double lat = gp.site[0], lon = gp.site[1], alt = gp.site[2], tilt = gp.site[3], saz = gp.site[4],
-                 albedo = gp.site[5];
     int doy, leap;
     civil_doy(dn, doy, leap);
-    const double pres = 100.0 * pow((44331.514 - alt) / 11880.516, 1.0 / 0.1902632);   // alt2pres
-    double zen, azen, az;
-    solpos(ck.utc0 + s, lat, lon, pres, 12.0, zen, azen, az);
-    const double ct = cos(rad(zen));
-    g[G_COSZ] = ct;
-    g[G_CSIMAX] = 27.21 * exp(-114 * ct) + 1.665 * exp(-4.494 * ct) + 1.08;
-    const double dni_extra = extra_rad(doy, 1366.1);
-    const double am_rel =
-        azen <= 90.0 ? 1.0 / (cos(rad(azen)) + 0.50572 * pow(6.07995 + (90.0 - azen), -1.6364)) : NAN;
-    const double am_abs = am_rel * pres / 101325.0;
-    const double tl = linke_at(gp.linke, doy, leap);
-    const double fh1 = exp(-alt / 8000.0), fh2 = exp(-alt / 1250.0);
-    const double cg1 = 5.09e-05 * alt + 0.868, cg2 = 3.92e-05 * alt + 0.0387;
-    double cz = cosd(azen);
-    cz = cz > 0.0 ? cz : 0.0;
-    const double gexp = exp(-cg2 * am_abs * (fh1 + fh2 * (tl - 1.0)));
-    const double gmax = isnan(gexp) ? 0.0 : (gexp > 0.0 ? gexp : 0.0);
-    g[G_GHICS] = cg1 * dni_extra * cz * tl / tl * gmax;
-    const double I0 = extra_rad(doy, 1370.0);
-    const double czd = cosd(zen);
-    g[G_I0] = I0;
-    g[G_I0H] = I0 * (czd > 0.065 ? czd : 0.065);
-    double amd = zen <= 90.0 ? 1.0 / (cos(rad(zen)) + 0.15 * pow(93.885 - zen, -1.253)) : NAN;
-    amd = amd * 101325.0 / 101325.0;
-    amd = amd < 12.0 ? amd : (isnan(amd) ? amd : 12.0);
-    g[G_AM] = amd;
-    g[G_KNC] = 0.866 - 0.122 * amd + 0.0121 * (amd * amd) - 0.000653 * pow(amd, 3.0) + 0.000014 * pow(amd, 4.0);
-    g[G_DISCOK] = zen > 87.0 ? 0.0 : 1.0;
-    double proj = cosd(tilt) * cosd(azen) + sind(tilt) * sind(azen) * cosd(az - saz);
-    proj = proj > 1.0 ? 1.0 : (proj < -1.0 ? -1.0 : proj);
-    const double cos_tt = proj > 0.0 ? proj : 0.0;
-    const double czs = cosd(azen);
-    g[G_RB] = cos_tt / (czs > 0.01745 ? czs : 0.01745);
-    g[G_DNIEXTRA] = dni_extra;
-    g[G_TERM2] = 0.5 * (1.0 + cosd(tilt));
-    g[G_GFAC] = albedo * (1.0 - cos(rad(tilt))) * 0.5;
-    const double aoi = deg(acos(proj));
-    g[G_COSAOI] = cos(rad(aoi));
-    const double* m = gp.module;
-    double f1 = (((m[4] * am_abs + m[3]) * am_abs + m[2]) * am_abs + m[1]) * am_abs + m[0];
-    f1 = isnan(f1) ? 0.0 : f1;
-    g[G_F1] = f1 > 0.0 ? f1 : 0.0;
-    double f2 = ((((m[10] * aoi + m[9]) * aoi + m[8]) * aoi + m[7]) * aoi + m[6]) * aoi + m[5];
-    f2 = f2 > 0.0 ? f2 : 0.0;
-    if (aoi < 0.0) f2 = 0.0;
-    g[G_F2] = f2;
+    double sn[SUN_W];
+    sun_at(ck.utc0 + s, doy, leap, gp.linke, sn);
+    for (int i = 0; i < SUN_W; ++i) sun[(size_t)j * SUN_W + i] = sn[i];
+    site_geom<true>(site_k(gp.site), sn, sn[SUN_TL], gp.module, g);
     if (g[G_GHICS] == 0.0) fl |= FL_NIGHT;   // ghi_cs = 0 -> pv = 0 whatever the csi
     g[G_FLAGS] = (double)fl;
     double* o64 = tab64 + (size_t)j * ROW;
@@ -486,7 +442,8 @@ template <typename R, int RNG>
 __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, uint64_t chain0, uint32_t n,
                                                     int64_t step0, uint32_t nsteps,
                                                     const double* __restrict__ tab64,
-                                                    const float* __restrict__ tab32, InjView inj, TraceView tr,
+                                                    const float* __restrict__ tab32,
+                                                    const double* __restrict__ sun, InjView inj, TraceView tr,
                                                     StatsView sv)
 {
     extern __shared__ uint32_t lds_hist[];
@@ -513,6 +470,12 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
     FSamp<R> fs;
     to_real(fs, ch.s);
     Acc acc{0.0, 0.0, 0.0, -INFINITY};
+    LaneSite ls{};   // per-chain sites (tmh_set_sites)
+    if (kp.sites) {
+        ls.k = site_k(kp.sites + (size_t)(live ? c : 0) * 8);
+        ls.linke = kp.site_linke ? kp.site_linke + (size_t)(live ? c : 0) * 12 : nullptr;
+        ls.tl_doy = -1;
+    }
     for (uint32_t j = 0; j < nsteps; ++j) {
         const uint64_t step = (uint64_t)(step0 + j);
         const float* r32 = tab32 + (size_t)j * ROW;
@@ -570,7 +533,12 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
                 if (ch.status == 0) {
                     const bool covered = ch.sec < ch.t1;
                     cov = covered ? 1 : 0;
-                    second_body<R>(kp, row, fl, fs, covered, z, mtr, csi, pv, meter, res);
+                    uint32_t flp = fl;
+                    if (kp.sites) {   // this chain's own site
+                        const bool night = lane_row<R>(ls, sun + (size_t)j * SUN_W, kp.module, row);
+                        flp = night ? (fl | FL_NIGHT) : (fl & ~(uint32_t)FL_NIGHT);
+                    }
+                    second_body<R>(kp, row, flp, fs, covered, z, mtr, csi, pv, meter, res);
                     ok = true;
                 }
             }
@@ -1033,11 +1001,12 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
 #ifndef TMH_EXP_WAVES
 #define TMH_EXP_WAVES 1
 #endif
-template <typename R, int OUT>
+template <typename R, int OUT, bool SITES>
 __global__ __launch_bounds__(256, TMH_EXP_WAVES) void expand_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0,
                                                      uint32_t n, int64_t W0, uint32_t nsteps, int64_t utc0,
                                                      const double* __restrict__ tab64,
                                                      const float* __restrict__ tab32,
+                                                     const double* __restrict__ sun,
                                                      const int2* __restrict__ events,
                                                      const uint32_t* __restrict__ n_events,
                                                      const BlockDesc* __restrict__ desc, SegView sg, TraceView tr,
@@ -1063,6 +1032,12 @@ __global__ __launch_bounds__(256, TMH_EXP_WAVES) void expand_kernel(KParams kp, 
     FSamp<R> fs;
     double ccb = 0.0, cca = 0.0;   // fp64 cloud-cover pair: the scale of the minute draws
     const MinuteCtx mc{dp, chain, W0, fm, events, (int)min(*n_events, ev_cap_dev(nsteps)), tab64};
+    LaneSite ls{};   // per-chain sites (C5): this chain's site constants
+    if constexpr (SITES) {
+        ls.k = site_k(kp.sites + (size_t)(live ? c : 0) * 8);
+        ls.linke = kp.site_linke ? kp.site_linke + (size_t)(live ? c : 0) * 12 : nullptr;
+        ls.tl_doy = -1;
+    }
     if (live) {
         alive = st.status[c] == 0;
         fault = sg.fault[c];
@@ -1162,7 +1137,12 @@ __global__ __launch_bounds__(256, TMH_EXP_WAVES) void expand_kernel(KParams kp, 
                 have_pair = true;
             }
             const bool odd = step & 1;
-            second_body<R>(kp, row, fl, fs, covered, noise_z<R>(odd ? pair.z : pair.x), meter_w<R>(odd ? pair.w : pair.y),
+            uint32_t flp = fl;
+            if constexpr (SITES) {   // this chain's own site: geometry per chain-second
+                const bool night = lane_row<R>(ls, sun + (size_t)j * SUN_W, kp.module, row);
+                flp = night ? (fl | FL_NIGHT) : (fl & ~(uint32_t)FL_NIGHT);
+            }
+            second_body<R>(kp, row, flp, fs, covered, noise_z<R>(odd ? pair.z : pair.x), meter_w<R>(odd ? pair.w : pair.y),
                            csi, pv, meter, res);
         }
         if (fl & (FL_DAY | FL_HOUR)) ++evi;
@@ -1345,6 +1325,7 @@ struct PlanView {
     int2* events;
     uint32_t* n_events;
     BlockDesc* desc;
+    double* sun;   // [n_steps][SUN_W]: the sun's place per step (per-chain sites)
 };
 
 size_t plan_layout(uint32_t n_steps, void* base, PlanView* v)
@@ -1361,6 +1342,8 @@ size_t plan_layout(uint32_t n_steps, void* base, PlanView* v)
     o += ALIGN;
     if (v) v->desc = (BlockDesc*)(b + o);
     o += align_up((size_t)(nblk_of(n_steps) + 1) * sizeof(BlockDesc));
+    if (v) v->sun = (double*)(b + o);
+    o += align_up((size_t)n_steps * SUN_W * 8);
     return o;
 }
 
@@ -1412,7 +1395,8 @@ struct tmh_engine {
     GParams gp;
     int device;
     int path;          // resolved kernel path: 1 sequential, 2 time-parallel
-    uint32_t n_tab = 0;   // rows of the per-chain shape tables (0: none)
+    uint32_t n_tab = 0;     // rows of the per-chain shape tables (0: none)
+    uint32_t n_sites = 0;   // rows of the per-chain sites (0: the engine's one site)
     // kernel timing (tmh_profile_*): event pairs per kernel, read and recycled
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[TMH_K_COUNT];
@@ -1606,10 +1590,22 @@ int tmh_set_shape_tables(struct tmh_engine* eng, const double* shapes, const int
     return TMH_OK;
 }
 
+int tmh_set_sites(struct tmh_engine* eng, const double* sites, const double* linke, uint32_t n_chains)
+{
+    if (!eng) return fail(TMH_E_INVAL, "NULL engine");
+    if (sites && n_chains == 0) return fail(TMH_E_INVAL, "per-chain sites with n_chains 0");
+    eng->kp.sites = sites;
+    eng->kp.site_linke = sites ? linke : nullptr;
+    eng->n_sites = sites ? n_chains : 0;
+    return TMH_OK;
+}
+
 static int check_tables(const tmh_engine* eng, uint32_t n_chains)
 {
     if (eng->kp.tab && n_chains > eng->n_tab)
         return fail(TMH_E_INVAL, "batch of %u chains exceeds the %u per-chain shape tables", n_chains, eng->n_tab);
+    if (eng->kp.sites && n_chains > eng->n_sites)
+        return fail(TMH_E_INVAL, "batch of %u chains exceeds the %u per-chain sites", n_chains, eng->n_sites);
     return TMH_OK;
 }
 
@@ -1683,7 +1679,7 @@ int tmh_plan(struct tmh_engine* eng, int64_t step0, uint32_t n_steps, void* plan
     plan_layout(n_steps, plan, &pv);
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(geom_kernel, dim3((n_steps + 255) / 256), dim3(256), 0, s, eng->gp, step0, n_steps, pv.tab64,
-                       pv.tab32);
+                       pv.tab32, pv.sun);
     hipLaunchKernelGGL(events_kernel, dim3(1), dim3(1024), 0, s, pv.tab32, step0, n_steps, eng->gp.clock.utc0,
                        pv.events, ev_cap(n_steps), pv.n_events);
     const uint32_t nb = nblk_of(n_steps);
@@ -1735,7 +1731,7 @@ int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
         dim3 grid((n_chains + 255) / 256), block(256);
 #define LAUNCH(R, M)                                                                                                 \
     hipLaunchKernelGGL((chain_kernel<R, M>), grid, block, lds, s, eng->kp, v, chain0, n_chains, step0, n_steps,      \
-                       pv.tab64, pv.tab32, iv, tv, sv)
+                       pv.tab64, pv.tab32, pv.sun, iv, tv, sv)
         if (f64 && keyed) LAUNCH(double, TMH_RNG_KEYED);
         else if (f64) LAUNCH(double, TMH_RNG_INJECTED);
         else if (keyed) LAUNCH(float, TMH_RNG_KEYED);
@@ -1767,17 +1763,20 @@ int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
     const int out = (no_stats && tv.pv && tv.meter && tv.residual && !tv.csi && !tv.covered) ? OUT_TRACE3
                     : (!tv.pv && !tv.meter && !tv.residual && !tv.csi && !tv.covered) ? OUT_STATS
                                                                                       : OUT_ANY;
-#define LAUNCH(R, O)                                                                                                 \
-    hipLaunchKernelGGL((expand_kernel<R, O>), grid2, dim3(256), lds, s, eng->kp, eng->dp, v, chain0, n_chains, step0, \
-                       n_steps, utc0, pv.tab64, pv.tab32, pv.events, pv.n_events, pv.desc, sg, tv, sv)
-    if (f64) {
-        if (out == OUT_TRACE3) LAUNCH(double, OUT_TRACE3);
-        else if (out == OUT_STATS) LAUNCH(double, OUT_STATS);
-        else LAUNCH(double, OUT_ANY);
+#define LAUNCH(R, O, S)                                                                                              \
+    hipLaunchKernelGGL((expand_kernel<R, O, S>), grid2, dim3(256), lds, s, eng->kp, eng->dp, v, chain0, n_chains,      \
+                       step0, n_steps, utc0, pv.tab64, pv.tab32, pv.sun, pv.events, pv.n_events, pv.desc, sg, tv, sv)
+    if (eng->kp.sites) {   // per-chain sites: one instantiation per precision, any output
+        if (f64) LAUNCH(double, OUT_ANY, true);
+        else LAUNCH(float, OUT_ANY, true);
+    } else if (f64) {
+        if (out == OUT_TRACE3) LAUNCH(double, OUT_TRACE3, false);
+        else if (out == OUT_STATS) LAUNCH(double, OUT_STATS, false);
+        else LAUNCH(double, OUT_ANY, false);
     } else {
-        if (out == OUT_TRACE3) LAUNCH(float, OUT_TRACE3);
-        else if (out == OUT_STATS) LAUNCH(float, OUT_STATS);
-        else LAUNCH(float, OUT_ANY);
+        if (out == OUT_TRACE3) LAUNCH(float, OUT_TRACE3, false);
+        else if (out == OUT_STATS) LAUNCH(float, OUT_STATS, false);
+        else LAUNCH(float, OUT_ANY, false);
     }
 #undef LAUNCH
     eng->close(TMH_K_EXPAND, t_exp, s);

@@ -34,6 +34,8 @@ struct KParams {
     PVF pvf;                                    // fp32 copies for the fp32 chain
     const double* tab;                          // per-chain shape tables [n][6][4] (NULL: shapes)
     const int32_t* tab_t;                       // per-chain Student-t flags [n][6] (NULL: is_t)
+    const double* sites;                        // per-chain PV sites [n][8] (NULL: the plan's site)
+    const double* site_linke;                   // per-chain monthly Linke turbidity [n][12] (NULL: params)
 };
 
 struct GParams {
@@ -660,45 +662,6 @@ __device__ void civil_doy(int64_t z, int& doy, int& leap)
     doy = cum[m - 1] + (int)d + ((leap && m > 2) ? 1 : 0);
 }
 
-__device__ void solpos(int64_t utc, double lat, double lon, double pressure_pa, double temp_c, double& zen,
-                       double& azen, double& az)
-{   // NOAA / Meeus low-precision sun + SPA refraction (same restatement as the oracle)
-    const double jd = (double)utc / 86400.0 + 2440587.5;
-    const double T = (jd - 2451545.0) / 36525.0;
-    const double L0 = fmod(280.46646 + T * (36000.76983 + T * 0.0003032), 360.0);
-    const double M = 357.52911 + T * (35999.05029 - 0.0001537 * T);
-    const double e = 0.016708634 - T * (0.000042037 + 0.0000001267 * T);
-    const double Mr = rad(M);
-    const double C = sin(Mr) * (1.914602 - T * (0.004817 + 0.000014 * T)) +
-                     sin(2.0 * Mr) * (0.019993 - 0.000101 * T) + sin(3.0 * Mr) * 0.000289;
-    const double omega = 125.04 - 1934.136 * T;
-    const double lam = L0 + C - 0.00569 - 0.00478 * sin(rad(omega));
-    const double eps0 = 23.0 + (26.0 + (21.448 - T * (46.815 + T * (0.00059 - T * 0.001813))) / 60.0) / 60.0;
-    const double eps = eps0 + 0.00256 * cos(rad(omega));
-    const double decl = asin(sin(rad(eps)) * sin(rad(lam)));
-    double y = tan(rad(eps) / 2.0);
-    y *= y;
-    const double L0r = rad(L0);
-    const double eot = 4.0 * deg(y * sin(2.0 * L0r) - 2.0 * e * sin(Mr) + 4.0 * e * y * sin(Mr) * cos(2.0 * L0r) -
-                                 0.5 * y * y * sin(4.0 * L0r) - 1.25 * e * e * sin(2.0 * Mr));
-    int64_t sod = utc % 86400;
-    if (sod < 0) sod += 86400;
-    double tst = fmod((double)sod / 60.0 + eot + 4.0 * lon, 1440.0);
-    if (tst < 0) tst += 1440.0;
-    const double ha = rad(tst / 4.0 - 180.0);
-    const double latr = rad(lat);
-    double cz = sin(latr) * sin(decl) + cos(latr) * cos(decl) * cos(ha);
-    cz = cz > 1.0 ? 1.0 : (cz < -1.0 ? -1.0 : cz);
-    zen = deg(acos(cz));
-    az = deg(atan2(sin(ha), cos(ha) * sin(latr) - tan(decl) * cos(latr))) + 180.0;
-    const double e0 = 90.0 - zen;
-    double de = 0.0;
-    if (e0 >= -1.0 * (0.26667 + 0.5667))
-        de = (pressure_pa / 100.0 / 1010.0) * (283.0 / (273.0 + temp_c)) * 1.02 /
-             (60.0 * tan(rad(e0 + 10.3 / (e0 + 5.11))));
-    azen = 90.0 - (e0 + de);
-}
-
 __device__ __forceinline__ double extra_rad(int doy, double s0)
 {
     const double B = (2.0 * 3.14159265358979323846 / 365.0) * (doy - 1);
@@ -725,6 +688,173 @@ __device__ double linke_at(const double* lts, int doy, int leap)
         y0 = y1;
     }
     return lts[0];
+}
+
+// ---- solar geometry, split by what it depends on (pvmodel.py:50-76, pvlib 0.6.3
+// model choices; NOAA / Meeus low-precision sun + SPA refraction, the oracle's
+// restatement).  The sun's place depends on the instant only: one plan row per
+// step (sun_at).  The site part runs once per site and step in geom_kernel, or
+// per chain-second when every chain has its own site (tmh_set_sites, C5).
+enum { SUN_SIND = 0, SUN_COSD, SUN_TAND, SUN_EOT, SUN_MIN, SUN_DNIX, SUN_I0, SUN_TL, SUN_DOY, SUN_LEAP, SUN_W = 12 };
+
+__device__ void sun_at(int64_t utc, int doy, int leap, const double* linke, double* o)
+{
+    const double jd = (double)utc / 86400.0 + 2440587.5;
+    const double T = (jd - 2451545.0) / 36525.0;
+    const double L0 = fmod(280.46646 + T * (36000.76983 + T * 0.0003032), 360.0);
+    const double M = 357.52911 + T * (35999.05029 - 0.0001537 * T);
+    const double e = 0.016708634 - T * (0.000042037 + 0.0000001267 * T);
+    const double Mr = rad(M);
+    const double C = sin(Mr) * (1.914602 - T * (0.004817 + 0.000014 * T)) +
+                     sin(2.0 * Mr) * (0.019993 - 0.000101 * T) + sin(3.0 * Mr) * 0.000289;
+    const double omega = 125.04 - 1934.136 * T;
+    const double lam = L0 + C - 0.00569 - 0.00478 * sin(rad(omega));
+    const double eps0 = 23.0 + (26.0 + (21.448 - T * (46.815 + T * (0.00059 - T * 0.001813))) / 60.0) / 60.0;
+    const double eps = eps0 + 0.00256 * cos(rad(omega));
+    const double decl = asin(sin(rad(eps)) * sin(rad(lam)));
+    double y = tan(rad(eps) / 2.0);
+    y *= y;
+    const double L0r = rad(L0);
+    const double eot = 4.0 * deg(y * sin(2.0 * L0r) - 2.0 * e * sin(Mr) + 4.0 * e * y * sin(Mr) * cos(2.0 * L0r) -
+                                 0.5 * y * y * sin(4.0 * L0r) - 1.25 * e * e * sin(2.0 * Mr));
+    int64_t sod = utc % 86400;
+    if (sod < 0) sod += 86400;
+    o[SUN_SIND] = sin(decl);
+    o[SUN_COSD] = cos(decl);
+    o[SUN_TAND] = tan(decl);
+    o[SUN_EOT] = eot;
+    o[SUN_MIN] = (double)sod / 60.0;
+    o[SUN_DNIX] = extra_rad(doy, 1366.1);   // ineichen dni_extra
+    o[SUN_I0] = extra_rad(doy, 1370.0);     // disc I0
+    o[SUN_TL] = linke ? linke_at(linke, doy, leap) : 0.0;
+    o[SUN_DOY] = doy;
+    o[SUN_LEAP] = leap;
+}
+
+// per-site constants of the geometry (site row: lat, lon, altitude, tilt, azimuth, albedo)
+struct SiteK {
+    double lon, slat, clat, pres, refr, alt, fh1, fh2, cg1, cg2, ctilt, stilt, saz, term2, gfac;
+};
+
+__device__ __forceinline__ SiteK site_k(const double* site)
+{
+    SiteK k;
+    const double lat = site[0], alt = site[2], tilt = site[3], albedo = site[5];
+    k.lon = site[1];
+    k.saz = site[4];
+    k.alt = alt;
+    const double latr = rad(lat);
+    k.slat = sin(latr);
+    k.clat = cos(latr);
+    k.pres = 100.0 * pow((44331.514 - alt) / 11880.516, 1.0 / 0.1902632);   // alt2pres
+    k.refr = (k.pres / 100.0 / 1010.0) * (283.0 / (273.0 + 12.0)) * 1.02;    // SPA refraction at 12 C
+    k.fh1 = exp(-alt / 8000.0);
+    k.fh2 = exp(-alt / 1250.0);
+    k.cg1 = 5.09e-05 * alt + 0.868;
+    k.cg2 = 3.92e-05 * alt + 0.0387;
+    k.ctilt = cosd(tilt);
+    k.stilt = sind(tilt);
+    k.term2 = 0.5 * (1.0 + cosd(tilt));
+    k.gfac = albedo * (1.0 - cos(rad(tilt))) * 0.5;
+    return k;
+}
+
+// geometry row fields G_COSZ..G_F2 of one site and step (fp64); returns true
+// when the clear-sky GHI is 0 (pv = 0 whatever the csi).  FULL = false stops
+// there at night (the per-chain-second path); FULL fills every field.
+template <bool FULL>
+__device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, double tl, const double* m, double* g)
+{
+    double tst = fmod(sun[SUN_MIN] + sun[SUN_EOT] + 4.0 * k.lon, 1440.0);
+    if (tst < 0) tst += 1440.0;
+    const double ha = rad(tst / 4.0 - 180.0);
+    const double cha = cos(ha);
+    double czr = k.slat * sun[SUN_SIND] + k.clat * sun[SUN_COSD] * cha;
+    czr = czr > 1.0 ? 1.0 : (czr < -1.0 ? -1.0 : czr);
+    const double zen = deg(acos(czr));
+    const double e0 = 90.0 - zen;
+    double de = 0.0;
+    if (e0 >= -1.0 * (0.26667 + 0.5667)) de = k.refr / (60.0 * tan(rad(e0 + 10.3 / (e0 + 5.11))));
+    const double azen = 90.0 - (e0 + de);
+    const double czs = cosd(azen);
+    if (!FULL && !(czs > 0.0)) return true;   // ghi_cs = cg1 * .. * max(cos(apparent zenith), 0) = 0
+    const double az = deg(atan2(sin(ha), cha * k.slat - sun[SUN_TAND] * k.clat)) + 180.0;
+    const double ct = cos(rad(zen));
+    g[G_COSZ] = ct;
+    g[G_CSIMAX] = 27.21 * exp(-114 * ct) + 1.665 * exp(-4.494 * ct) + 1.08;   // pvmodel.py:52-58
+    const double dni_extra = sun[SUN_DNIX];
+    const double am_rel = azen <= 90.0 ? 1.0 / (czs + 0.50572 * pow(6.07995 + (90.0 - azen), -1.6364)) : NAN;
+    const double am_abs = am_rel * k.pres / 101325.0;
+    const double cz = czs > 0.0 ? czs : 0.0;
+    const double gexp = exp(-k.cg2 * am_abs * (k.fh1 + k.fh2 * (tl - 1.0)));
+    const double gmax = isnan(gexp) ? 0.0 : (gexp > 0.0 ? gexp : 0.0);
+    g[G_GHICS] = k.cg1 * dni_extra * cz * tl / tl * gmax;                     // ineichen (pvmodel.py:60)
+    const double I0 = sun[SUN_I0];
+    g[G_I0] = I0;                                                              // disc (pvmodel.py:63)
+    g[G_I0H] = I0 * (ct > 0.065 ? ct : 0.065);
+    double amd = zen <= 90.0 ? 1.0 / (ct + 0.15 * pow(93.885 - zen, -1.253)) : NAN;
+    amd = amd * 101325.0 / 101325.0;
+    amd = amd < 12.0 ? amd : (isnan(amd) ? amd : 12.0);
+    g[G_AM] = amd;
+    g[G_KNC] = 0.866 - 0.122 * amd + 0.0121 * (amd * amd) - 0.000653 * pow(amd, 3.0) + 0.000014 * pow(amd, 4.0);
+    g[G_DISCOK] = zen > 87.0 ? 0.0 : 1.0;
+    double proj = k.ctilt * czs + k.stilt * sind(azen) * cosd(az - k.saz);    // haydavies / aoi (pvmodel.py:66-72)
+    proj = proj > 1.0 ? 1.0 : (proj < -1.0 ? -1.0 : proj);
+    const double cos_tt = proj > 0.0 ? proj : 0.0;
+    g[G_RB] = cos_tt / (czs > 0.01745 ? czs : 0.01745);
+    g[G_DNIEXTRA] = dni_extra;
+    g[G_TERM2] = k.term2;
+    g[G_GFAC] = k.gfac;
+    const double aoi = deg(acos(proj));
+    g[G_COSAOI] = cos(rad(aoi));
+    double f1 = (((m[4] * am_abs + m[3]) * am_abs + m[2]) * am_abs + m[1]) * am_abs + m[0];   // sapm spectral
+    f1 = isnan(f1) ? 0.0 : f1;
+    g[G_F1] = f1 > 0.0 ? f1 : 0.0;
+    double f2 = ((((m[10] * aoi + m[9]) * aoi + m[8]) * aoi + m[7]) * aoi + m[6]) * aoi + m[5];   // sapm aoi loss
+    f2 = f2 > 0.0 ? f2 : 0.0;
+    if (aoi < 0.0) f2 = 0.0;
+    g[G_F2] = f2;
+    return g[G_GHICS] == 0.0;
+}
+
+// the kernels' row of one chain's own site (fp32 rows carry the reciprocals
+// of I0h and dni_extra, like geom_kernel's fp32 table)
+template <typename R>
+__device__ __forceinline__ void site_row(const double* g, R* row)
+{
+#pragma unroll
+    for (int i = G_COSZ; i <= G_F2; ++i) row[i] = (R)g[i];
+    if constexpr (sizeof(R) == 4) {
+        row[G_I0H] = (float)(1.0 / g[G_I0H]);
+        row[G_DNIEXTRA] = (float)(1.0 / g[G_DNIEXTRA]);
+    }
+}
+
+// per-chain site state of a kernel lane: constants + the day's Linke turbidity
+struct LaneSite {
+    SiteK k;
+    const double* linke;   // the chain's 12 monthly values, or NULL (the plan's per-step value)
+    int tl_doy;
+    double tl;
+};
+
+// the geometry of lane site `ls` at the plan's sun row; true = night
+template <typename R>
+__device__ __forceinline__ bool lane_row(LaneSite& ls, const double* sun, const double* module, R* row)
+{
+    double tl = sun[SUN_TL];
+    if (ls.linke) {
+        const int doy = (int)sun[SUN_DOY];
+        if (doy != ls.tl_doy) {
+            ls.tl_doy = doy;
+            ls.tl = linke_at(ls.linke, doy, (int)sun[SUN_LEAP]);
+        }
+        tl = ls.tl;
+    }
+    double g[ROW];
+    if (site_geom<false>(ls.k, sun, tl, module, g)) return true;
+    site_row<R>(g, row);
+    return g[G_GHICS] == 0.0;
 }
 
 

@@ -45,11 +45,14 @@ class BatchedSim:
     shape_tables : optional per-chain hourly cloud-cover tables (shapes [n, 6, 4],
         is_t [n, 6]; e.g. params.site_shape_tables) in place of params.shapes —
         one table per site of a lat/lon sweep (tmh_set_shape_tables)
+    sites : optional per-chain PV sites [n, 8] in Site.as_array() order (e.g.
+        params.site_grid), or (sites, linke [n, 12]); columns 0-5 vary per chain,
+        temp_air and wind stay params.site's (tmh_set_sites)
     """
 
     def __init__(self, n_chains, start, tz=None, params: ModelParams | None = None, precision="fp32",
                  chain0=0, device=None, injected=None, horizon=400 * 86400, kernel_path="auto",
-                 shape_tables=None):
+                 shape_tables=None, sites=None):
         torch = _torch()
         L = _lib.load()
         self.L = L
@@ -97,6 +100,20 @@ class BatchedSim:
                     raise ValueError(f"shape_tables is_t must be [n_chains, 6], got {tuple(it.shape)}")
             self.tables = (sh, it)   # the engine reads them on every launch: keep them alive
             _lib.check(L.tmh_set_shape_tables(self._eng, _ptr(sh), _ptr(it) if it is not None else None, self.n))
+        self.sites = None
+        if sites is not None:
+            si, li = sites if isinstance(sites, tuple) else (sites, None)
+            si = torch.as_tensor(np.asarray(si, dtype=np.float64) if not torch.is_tensor(si) else si,
+                                 dtype=torch.float64, device=self.device).contiguous()
+            if tuple(si.shape) != (self.n, 8):
+                raise ValueError(f"sites must be [n_chains, 8], got {tuple(si.shape)}")
+            if li is not None:
+                li = torch.as_tensor(np.asarray(li, dtype=np.float64) if not torch.is_tensor(li) else li,
+                                     dtype=torch.float64, device=self.device).contiguous()
+                if tuple(li.shape) != (self.n, 12):
+                    raise ValueError(f"sites linke must be [n_chains, 12], got {tuple(li.shape)}")
+            self.sites = (si, li)
+            _lib.check(L.tmh_set_sites(self._eng, _ptr(si), _ptr(li) if li is not None else None, self.n))
         self.step = 0
         self.hist = None
         self.chain_acc = None

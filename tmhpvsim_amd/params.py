@@ -173,3 +173,24 @@ def site_shape_tables(n_sites, site0=0, shapes=SHAPES, shape_is_t=SHAPE_IS_T, se
     tab = np.asarray(shapes, dtype=np.float64)[None] * (1.0 - spread + 2.0 * spread * u)
     is_t = np.broadcast_to(np.asarray(shape_is_t, dtype=np.int32), (n_sites, 6)).copy()
     return np.ascontiguousarray(tab), is_t
+
+
+def site_grid(n_lat=256, n_lon=256, lat=(35.0, 60.0), lon=(-10.0, 30.0), base: Site | None = None):
+    """PV sites on a regular lat/lon grid (256 x 256 over 35-60 N,
+    10 W-30 E), latitude-major: [n_lat * n_lon, 8] rows in tmh_params.site order.
+    Every site is the reference's system (pvmodel.py:19-30) moved: tilt =
+    latitude, facing south, the base site's altitude, albedo, air temperature
+    and wind.  Ready for BatchedSim(sites=...) (slice rows for a chain range)."""
+    b = base or Site()
+    la = np.linspace(lat[0], lat[1], n_lat)
+    lo = np.linspace(lon[0], lon[1], n_lon)
+    g = np.empty((n_lat, n_lon, 8), dtype=np.float64)
+    g[..., 0] = la[:, None]
+    g[..., 1] = lo[None, :]
+    g[..., 2] = b.altitude
+    g[..., 3] = la[:, None]
+    g[..., 4] = b.surface_azimuth
+    g[..., 5] = b.albedo
+    g[..., 6] = b.temp_air
+    g[..., 7] = b.wind_speed
+    return g.reshape(-1, 8)
