@@ -39,13 +39,20 @@ TRACE_BYTES = 12               # meter + pv + residual, fp32
 
 def parse():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="c2", choices=["c2", "c5"],
+                    help="c2: the headline (BASELINE.json configs[1]); c5: the lat/lon sweep (65,536 sites x 1 "
+                         "week, markov cc with per-site tables, per-site PV geometry, stats mode, day windows)")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--chains", type=int, default=4096, help="chains per GPU")
-    ap.add_argument("--seconds", type=int, default=86400)
+    ap.add_argument("--chains", type=int, default=None, help="chains per GPU (c2: 4096, c5: 65536)")
+    ap.add_argument("--seconds", type=int, default=None, help="c2: 86400, c5: 604800")
+    ap.add_argument("--window", type=int, default=None, help="steps per tmh_step window (c2: all, c5: 86400)")
+    ap.add_argument("--cc", default=None, choices=["faithful", "markov"],
+                    help="hourly cloud-cover mode (c2: faithful, the reference's; c5: markov, whose low-cover "
+                         "AssertionError (cloud_cover_binary.py:91) ends most chains within days)")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64"])
-    ap.add_argument("--mode", default="trace", choices=["trace", "stats"])
+    ap.add_argument("--mode", default=None, choices=["trace", "stats"], help="c2: trace, c5: stats")
     ap.add_argument("--start", default="2019-09-05 00:00:00")
     ap.add_argument("--cpu-sample-chains", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -53,23 +60,35 @@ def parse():
     ap.add_argument("--pipeline", type=int, default=3,
                     help="batches in flight on separate HIP streams (1 = no overlap): the segment walks of the "
                          "next batches (latency-bound, one wave per SIMD) run beside this batch's expansion")
-    return ap.parse_args()
+    a = ap.parse_args()
+    c5 = a.workload == "c5"
+    a.chains = a.chains or (65536 if c5 else 4096)
+    a.seconds = a.seconds or (604800 if c5 else 86400)
+    a.mode = a.mode or ("stats" if c5 else "trace")
+    a.cc = a.cc or ("markov" if c5 else "faithful")
+    a.window = min(a.window or (86400 if c5 else a.seconds), a.seconds)
+    return a
 
 
-def cpu_baseline(args):
-    """The C oracle on a bounded sample of the same workload (same site/day/modes, fp64)."""
+def cpu_baseline(args, kw):
+    """The C oracle on a bounded sample of the same workload (same site(s)/day/modes, fp64)."""
     from oracle import oracle as O
-    from tmhpvsim_amd.params import ModelParams
+    from tmhpvsim_amd.params import CC_MARKOV, ModelParams
     threads = max(1, min(16, os.cpu_count() or 1))
-    n = args.cpu_sample_chains
-    O.run(ModelParams(), 0, 2, 600, args.start, tz="Europe/Berlin", n_threads=1)   # load + warm
+    c5 = args.workload == "c5"
+    mp = ModelParams(cc_mode=CC_MARKOV if args.cc == "markov" else 0)
+    n = args.cpu_sample_chains if not c5 else min(args.cpu_sample_chains // 16, args.chains)
+    secs = min(args.seconds, 86400)
+    extra = {}
+    if c5:   # the first n sites of the sweep, their tables; geometry per chain-second like the GPU path
+        extra = dict(tables=tuple(x[:n] for x in kw["shape_tables"]), sites=kw["sites"][:n])
+    O.run(mp, 0, 2, 600, args.start, tz="Europe/Berlin", n_threads=1)   # load + warm
     t = time.perf_counter()
-    O.run(ModelParams(), 10 ** 9, n, args.seconds, args.start, tz="Europe/Berlin", n_threads=threads,
-          outputs=("residual",))
+    O.run(mp, 10 ** 9, n, secs, args.start, tz="Europe/Berlin", n_threads=threads, outputs=("residual",), **extra)
     dt = time.perf_counter() - t
-    return {"value": n * args.seconds / dt, "unit": "chain-seconds/s", "cores": threads, "kind": "port",
-            "sample": f"{n} chains x {args.seconds} s (C2 site/day, fp64 C oracle, {threads} OpenMP threads, "
-                      f"{dt:.1f} s wall)"}
+    return {"value": n * secs / dt, "unit": "chain-seconds/s", "cores": threads, "kind": "port",
+"sample": f"{n} chains x {secs} s ({'C5 sites/tables, ' + args.cc if c5 else 'C2 site/day'}, fp64 C oracle, "
+                      f"{threads} OpenMP threads, {dt:.1f} s wall)"}
 
 
 def traffic(args, n, secs):
@@ -103,14 +122,20 @@ def main():
 
     from tmhpvsim_amd import _lib
     from tmhpvsim_amd.engine import BatchedSim
-    from tmhpvsim_amd.params import ModelParams
+    from tmhpvsim_amd.params import CC_MARKOV, ModelParams, site_grid, site_shape_tables
 
     from tmhpvsim_amd.dist import all_reduce_stats
 
     L = _lib.load()
-    n, secs = args.chains, args.seconds
-    sim = BatchedSim(n, args.start, tz="Europe/Berlin", params=ModelParams(), precision=args.precision,
-                     chain0=rank * n, device=dev, horizon=secs, kernel_path=args.path)
+    n, secs, win = args.chains, args.seconds, args.window
+    c5 = args.workload == "c5"
+    kw = {}
+    if c5:   # the grid's sites (rank r takes rows [r n, (r+1) n) of a 256 x 256 x world sweep)
+        grid = site_grid(256 * world, 256) if n == 65536 else site_grid(max(1, n // 256) * world, 256)
+        sl = slice(rank * n, (rank + 1) * n)
+        kw = dict(shape_tables=site_shape_tables(n, site0=rank * n), sites=grid[sl][:n])
+    sim = BatchedSim(n, args.start, tz="Europe/Berlin", params=ModelParams(cc_mode=CC_MARKOV if args.cc == "markov" else 0),
+                     precision=args.precision, chain0=rank * n, device=dev, horizon=secs, kernel_path=args.path, **kw)
     real = sim.real
 
     class Ctx:   # one batch in flight: its own state, plan, scratch, outputs and HIP stream
@@ -118,9 +143,9 @@ def main():
             self.stream = torch.cuda.Stream(dev)
             self.sptr = C.c_void_p(self.stream.cuda_stream)
             self.state = torch.zeros(L.tmh_state_bytes(n), dtype=torch.uint8, device=dev)
-            self.plan = torch.empty(L.tmh_plan_bytes(secs), dtype=torch.uint8, device=dev)
-            self.scratch = torch.empty(L.tmh_scratch_bytes(n, secs), dtype=torch.uint8, device=dev)
-            self.trace = {f: torch.empty(secs, n, dtype=real, device=dev) for f in ("pv", "meter", "residual")} \
+            self.plan = torch.empty(L.tmh_plan_bytes(win), dtype=torch.uint8, device=dev)
+            self.scratch = torch.empty(L.tmh_scratch_bytes(n, win), dtype=torch.uint8, device=dev)
+            self.trace = {f: torch.empty(win, n, dtype=real, device=dev) for f in ("pv", "meter", "residual")} \
                 if args.mode == "trace" else {}
             self.tr = _lib.Trace(None, None, *(self.trace[f].data_ptr() if f in self.trace else None
                                                for f in ("pv", "meter", "residual")), n)
@@ -138,12 +163,14 @@ def main():
     def one_step(k):
         cx = ctxs[k % len(ctxs)]
         chain0 = (rank + k * world) * n                    # fresh global chains every batch
-        _lib.check(L.tmh_plan(sim._eng, 0, secs, C.c_void_p(cx.plan.data_ptr()), cx.sptr))
         _lib.check(L.tmh_init(sim._eng, C.c_void_p(cx.state.data_ptr()), chain0, n, None, cx.sptr))
-        _lib.check(L.tmh_step(sim._eng, C.c_void_p(cx.state.data_ptr()), chain0, n, 0, secs, None,
-                              C.byref(cx.tr), C.byref(cx.st) if cx.st is not None else None,
-                              C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()), cx.scratch.numel(),
-                              cx.sptr))
+        for s0 in range(0, secs, win):   # windows: a trace window is overwritten by the next (C2: one window)
+            w = min(win, secs - s0)
+            _lib.check(L.tmh_plan(sim._eng, s0, w, C.c_void_p(cx.plan.data_ptr()), cx.sptr))
+            _lib.check(L.tmh_step(sim._eng, C.c_void_p(cx.state.data_ptr()), chain0, n, s0, w, None,
+                                  C.byref(cx.tr), C.byref(cx.st) if cx.st is not None else None,
+                                  C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
+                                  cx.scratch.numel(), cx.sptr))
 
     def exchange():
         """stats mode: the one cross-GPU step, an RCCL all-reduce of the aggregate statistics"""
@@ -188,6 +215,10 @@ def main():
     for cx in ctxs:
         sim.state = cx.state
         bad += int((sim.status() != 0).sum())
+    nwin = (secs + win - 1) // win
+    for name in phases:                                    # per batch (all windows)
+        if phases[name] is not None:
+            phases[name] *= nwin
     kmean = phases["expand"] if phases["expand"] else float("nan")
     if world > 1:
         t = torch.tensor([elapsed, kmean], device=dev, dtype=torch.float64)
@@ -201,8 +232,10 @@ def main():
         "value": value, "unit": "chain-seconds/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic (keyed Philox)",
-        "config": {"workload": f"C2: {n} chains/GPU x {secs} s at 1 s, Munich, Europe/Berlin, "
-                               f"{args.start[:10]}, {args.mode} mode ({'meter+pv+residual fp32 trace' if args.mode == 'trace' else 'on-GPU stats'})",
+        "config": {"workload": (f"C2: {n} chains/GPU x {secs} s at 1 s, Munich, Europe/Berlin, " if not c5 else
+                                f"C5: {n} sites/GPU on a lat/lon grid (35-60 N, 10 W-30 E) x {secs} s, {args.cc} cc "
+                                f"with per-site tables, per-site PV geometry, {win} s windows, Europe/Berlin, ")
+                               + f"{args.start[:10]}, {args.mode} mode ({'meter+pv+residual fp32 trace' if args.mode == 'trace' else 'on-GPU stats'})",
                    "chains_per_gpu": n, "seconds": secs, "parallelism": f"chains sharded over {world} GPU(s)",
                    "batches_in_flight": len(ctxs)},
         "roofline": ({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -218,7 +251,7 @@ def main():
         "faulted_chains": bad,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(args)
+        line["cpu_baseline"] = cpu_baseline(args, kw)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
