@@ -655,7 +655,10 @@ __device__ __forceinline__ double bperm_f64(int src_lane, double v)
     return __hiloint2double(hi, lo);
 }
 
-constexpr int RCH = 8;         // register chunks of 16 entries: sigma entries 0..127 (all but ~1e-5 of calls)
+#ifndef TMH_RCH
+#define TMH_RCH 8
+#endif
+constexpr int RCH = TMH_RCH;   // register chunks of 16 entries: sigma entries 0..127 (all but ~1e-5 of calls)
 constexpr int RCH_FIXED = 4;   // chunks always processed (L <= 64 for 99.7 % of calls)
 
 // P1: segment walk.  Four chains per wavefront, one per row of 16 lanes; entry
@@ -998,11 +1001,11 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
 #ifndef TMH_ROW_PREFETCH
 #define TMH_ROW_PREFETCH 0
 #endif
-#ifndef TMH_EXP_WAVES
-#define TMH_EXP_WAVES 1
+#ifndef TMH_EXP_WAVES   // min waves per SIMD of the fp32 single-site expansion: 6 = at most 80 VGPRs (-3.5 % vs 5)
+#define TMH_EXP_WAVES 6
 #endif
 template <typename R, int OUT, bool SITES>
-__global__ __launch_bounds__(256, TMH_EXP_WAVES) void expand_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0,
+__global__ __launch_bounds__(256, (SITES || sizeof(R) == 8) ? 1 : TMH_EXP_WAVES) void expand_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0,
                                                      uint32_t n, int64_t W0, uint32_t nsteps, int64_t utc0,
                                                      const double* __restrict__ tab64,
                                                      const float* __restrict__ tab32,
