@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--cpu-sample-chains", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--path", default="auto", choices=["auto", "sequential", "time_parallel"])
+    ap.add_argument("--no-stagger", dest="stagger", action="store_false",
+                    help="issue each batch as one tmh_step (batches then run in lockstep across streams)")
     ap.add_argument("--pipeline", type=int, default=3,
                     help="batches in flight on separate HIP streams (1 = no overlap): the segment walks of the "
                          "next batches (latency-bound, one wave per SIMD) run beside this batch's expansion")
@@ -160,17 +162,52 @@ def main():
     torch.cuda.synchronize()
     L.tmh_profile_enable(sim._eng, 1)
 
-    def one_step(k):
+    nwin = (secs + win - 1) // win
+
+    def one_step(k):   # a whole batch on its context's stream (multi-window batches)
         cx = ctxs[k % len(ctxs)]
         chain0 = (rank + k * world) * n                    # fresh global chains every batch
         _lib.check(L.tmh_init(sim._eng, C.c_void_p(cx.state.data_ptr()), chain0, n, None, cx.sptr))
-        for s0 in range(0, secs, win):   # windows: a trace window is overwritten by the next (C2: one window)
+        for s0 in range(0, secs, win):   # windows: a trace window is overwritten by the next
             w = min(win, secs - s0)
             _lib.check(L.tmh_plan(sim._eng, s0, w, C.c_void_p(cx.plan.data_ptr()), cx.sptr))
             _lib.check(L.tmh_step(sim._eng, C.c_void_p(cx.state.data_ptr()), chain0, n, s0, w, None,
                                   C.byref(cx.tr), C.byref(cx.st) if cx.st is not None else None,
                                   C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
                                   cx.scratch.numel(), cx.sptr))
+
+    def start(k):      # one-window batch, first half: construction, plan, segment walk (tmh_walk)
+        cx = ctxs[k % len(ctxs)]
+        cx.chain0 = (rank + k * world) * n                 # fresh global chains every batch
+        _lib.check(L.tmh_init(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, None, cx.sptr))
+        _lib.check(L.tmh_plan(sim._eng, 0, secs, C.c_void_p(cx.plan.data_ptr()), cx.sptr))
+        _lib.check(L.tmh_walk(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs,
+                              C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()), cx.scratch.numel(),
+                              cx.sptr))
+
+    def finish(k):     # second half: expansion (trace / stats) and commit (tmh_expand)
+        cx = ctxs[k % len(ctxs)]
+        _lib.check(L.tmh_expand(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs, None,
+                                C.byref(cx.tr), C.byref(cx.st) if cx.st is not None else None,
+                                C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
+                                cx.scratch.numel(), cx.sptr))
+
+    def run_batches(k0, cnt):
+        """Batches k0 .. k0 + cnt - 1.  One-window batches are software-pipelined:
+        the walks of the next (depth - 1) batches are issued ahead of this batch's
+        expansion, on their own streams, so the latency-bound segment walks overlap
+        the expansion instead of running in lockstep with it."""
+        if nwin > 1 or not args.stagger:
+            for k in range(k0, k0 + cnt):
+                one_step(k)
+            return
+        ahead = len(ctxs) - 1
+        for k in range(k0, min(k0 + ahead, k0 + cnt)):
+            start(k)
+        for k in range(k0, k0 + cnt):
+            if k + ahead < k0 + cnt:
+                start(k + ahead)
+            finish(k)
 
     def exchange():
         """stats mode: the one cross-GPU step, an RCCL all-reduce of the aggregate statistics"""
@@ -182,8 +219,7 @@ def main():
                    peak_residual=acc[:, 3].max(), hist=hist)
         return all_reduce_stats(tot)
 
-    for k in range(args.warmup):
-        one_step(k)
+    run_batches(0, args.warmup)
     if args.mode == "stats":
         exchange()                                         # loads torch's reduction kernels outside the timing
         for cx in ctxs:
@@ -197,8 +233,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.warmup, args.warmup + args.steps):
-        one_step(k)
+    run_batches(args.warmup, args.steps)
     if args.mode == "stats":
         exchange()
     torch.cuda.synchronize()
@@ -215,7 +250,6 @@ def main():
     for cx in ctxs:
         sim.state = cx.state
         bad += int((sim.status() != 0).sum())
-    nwin = (secs + win - 1) // win
     for name in phases:                                    # per batch (all windows)
         if phases[name] is not None:
             phases[name] *= nwin
@@ -237,7 +271,7 @@ def main():
                                 f"with per-site tables, per-site PV geometry, {win} s windows, Europe/Berlin, ")
                                + f"{args.start[:10]}, {args.mode} mode ({'meter+pv+residual fp32 trace' if args.mode == 'trace' else 'on-GPU stats'})",
                    "chains_per_gpu": n, "seconds": secs, "parallelism": f"chains sharded over {world} GPU(s)",
-                   "batches_in_flight": len(ctxs)},
+                   "batches_in_flight": len(ctxs), "staggered": bool(args.stagger and nwin == 1)},
         "roofline": ({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": achieved / HBM_PEAK_GBS, "traffic": traffic(args, n, secs),
                       "kernel": "expand_kernel (P2, " + sim.path + ")", "kernel_ms": kmean,

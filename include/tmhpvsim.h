@@ -208,6 +208,20 @@ int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
              const tmh_stats* stats, const void* plan, void* scratch, size_t scratch_bytes,
              void* stream);
 
+/* tmh_step in its two halves, for callers that overlap independent batches
+ * (bench.py: the latency-bound segment walks of the next batches run beside
+ * this batch's expansion).  tmh_walk: boundary draws, candidate cloud lengths
+ * and the P1 segment walk into `scratch`; tmh_expand: the P2 expansion
+ * (traces / statistics) and the state commit from that scratch.  Call them in
+ * this order on the same plan, scratch and state (the same stream, or with the
+ * caller ordering them); tmh_step == tmh_walk + tmh_expand.  On the sequential
+ * path tmh_walk does nothing and tmh_expand runs the whole step. */
+int tmh_walk(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, int64_t step0,
+             uint32_t n_steps, const void* plan, void* scratch, size_t scratch_bytes, void* stream);
+int tmh_expand(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, int64_t step0,
+               uint32_t n_steps, const tmh_ustream* inj, const tmh_trace* trace, const tmh_stats* stats,
+               const void* plan, void* scratch, size_t scratch_bytes, void* stream);
+
 /* Kernel timing (measurement only).  While enabled, tmh_step records HIP
  * events, on the stream each kernel runs on, around the kernels of the
  * time-parallel path; tmh_profile_read waits for them and returns the summed

@@ -8,7 +8,7 @@ cd "$ROOT"
 VARIANTS="${VARIANTS:-base:- norng:-DTMH_DIAG_NO_RNG nondtri:-DTMH_DIAG_NO_NDTRI nopv:-DTMH_DIAG_NO_PV nostore:-DTMH_DIAG_NO_STORE}"
 if [ "${1:-run}" = build ]; then
   for v in $VARIANTS; do
-    name=${v%%:*}; flag=${v#*:}; [ "$flag" = "-" ] && flag=""
+    name=${v%%:*}; flag=${v#*:}; [ "$flag" = "-" ] && flag=""; flag=${flag//+/ }
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off $flag \
       -I include -o tmhpvsim_amd/libtmh_$name.so tmhpvsim_amd/csrc/tmh_engine.hip || exit 1
   done

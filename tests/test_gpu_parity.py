@@ -318,6 +318,36 @@ def test_time_parallel_equals_sequential(prec, markov):
         assert torch.equal(a.state_field(f)[live], b.state_field(f)[live]), f
 
 
+@pytest.mark.parametrize("path", ["time_parallel", "sequential"])
+def test_walk_then_expand_equals_step(path):
+    """tmh_walk + tmh_expand (the split bench.py pipelines) == tmh_run, bit for bit."""
+    import ctypes as C
+    from tmhpvsim_amd import _lib
+    start, steps, n = "2019-09-05 05:00:00", 7000, 96
+    a = _sim(n, start, tz="Europe/Berlin", prec="fp32", horizon=steps, kernel_path=path)
+    b = _sim(n, start, tz="Europe/Berlin", prec="fp32", horizon=steps, kernel_path=path)
+    ra = a.run(steps, window=steps)
+    L = b.L
+    out = {f: torch.empty(steps, n, dtype=torch.float32, device="cuda:0") for f in ("csi", "pv", "meter", "residual")}
+    cov = torch.empty(steps, n, dtype=torch.uint8, device="cuda:0")
+    tr = _lib.Trace(out["csi"].data_ptr(), cov.data_ptr(), out["pv"].data_ptr(), out["meter"].data_ptr(),
+                    out["residual"].data_ptr(), n)
+    plan = torch.empty(L.tmh_plan_bytes(steps), dtype=torch.uint8, device="cuda:0")
+    scr = torch.empty(max(1, L.tmh_scratch_bytes(n, steps)), dtype=torch.uint8, device="cuda:0")
+    p = lambda t: C.c_void_p(t.data_ptr())
+    s = b._stream()
+    _lib.check(L.tmh_plan(b._eng, 0, steps, p(plan), s))
+    _lib.check(L.tmh_walk(b._eng, p(b.state), 0, n, 0, steps, p(plan), p(scr), scr.numel(), s))
+    _lib.check(L.tmh_expand(b._eng, p(b.state), 0, n, 0, steps, None, C.byref(tr), None, p(plan), p(scr),
+                            scr.numel(), s))
+    torch.cuda.synchronize()
+    for f in ("csi", "pv", "meter", "residual"):
+        assert _same(ra[f], out[f]), f
+    assert _same(ra["covered"], cov)
+    np.testing.assert_array_equal(a.status(), b.status())
+    assert _same(a.state_field("sa_cc"), b.state_field("sa_cc"))
+
+
 def test_stats_match_trace():
     start, steps, n = "2019-09-05 00:00:00", 20000, 512
     s = _sim(n, start, tz="Europe/Berlin", prec="fp32", horizon=steps)

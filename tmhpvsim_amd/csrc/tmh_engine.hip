@@ -671,7 +671,10 @@ constexpr int RCH_FIXED = 4;   // chunks always processed (L <= 64 for 99.7 % of
 // the r_[cl, nsc[:last+1]] shift is row_shr:1 / row_ror:1.  Output per chain:
 // segment records (first uncovered step, next call step) and the window-end
 // binary state.
-__global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
+#ifndef TMH_SEG_WAVES
+#define TMH_SEG_WAVES 1
+#endif
+__global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
                                                           int64_t W0, uint32_t nsteps, tmh_clock ck,
                                                           const int2* __restrict__ events,
                                                           const uint32_t* __restrict__ n_events, SegView sg)
@@ -1691,16 +1694,18 @@ int tmh_plan(struct tmh_engine* eng, int64_t step0, uint32_t n_steps, void* plan
     return hip_check(hipGetLastError(), "plan kernels launch");
 }
 
-int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, int64_t step0,
-             uint32_t n_steps, const tmh_ustream* inj, const tmh_trace* trace, const tmh_stats* stats,
-             const void* plan, void* scratch, size_t scratch_bytes, void* stream)
+enum { PH_WALK = 1, PH_EXPAND = 2, PH_ALL = 3 };
+
+static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, int64_t step0,
+                       uint32_t n_steps, const tmh_ustream* inj, const tmh_trace* trace, const tmh_stats* stats,
+                       const void* plan, void* scratch, size_t scratch_bytes, void* stream, int phases)
 {
     if (!eng || !state || !plan) return fail(TMH_E_INVAL, "NULL engine/state/plan");
     if (n_chains == 0 || n_steps == 0) return TMH_OK;
     if (step0 < 0 || step0 + (int64_t)n_steps > (int64_t)INT_MAX - (1 << 20))
         return fail(TMH_E_INVAL, "step window [%lld, +%u) outside [0, 2^31 - 2^20)", (long long)step0, n_steps);
     if ((n_chains + 255) / 256 > 65535) return fail(TMH_E_INVAL, "n_chains %u > 16,776,960 per call", n_chains);
-    if (eng->kp.rng_mode == TMH_RNG_INJECTED && (!inj || !inj->u || inj->stride < inj->len))
+    if ((phases & PH_EXPAND) && eng->kp.rng_mode == TMH_RNG_INJECTED && (!inj || !inj->u || inj->stride < inj->len))
         return fail(TMH_E_INVAL, "injected mode needs a stream with stride >= len");
     if (trace && (trace->csi || trace->pv || trace->meter || trace->residual || trace->covered) &&
         trace->ld < n_chains)
@@ -1730,7 +1735,8 @@ int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
     }
     hipStream_t s = (hipStream_t)stream;
     const bool f64 = eng->kp.precision == TMH_FP64, keyed = eng->kp.rng_mode == TMH_RNG_KEYED;
-    if (!tp) {
+    if (!tp) {   // sequential path: one kernel, run by the expand phase
+        if (!(phases & PH_EXPAND)) return TMH_OK;
         dim3 grid((n_chains + 255) / 256), block(256);
 #define LAUNCH(R, M)                                                                                                 \
     hipLaunchKernelGGL((chain_kernel<R, M>), grid, block, lds, s, eng->kp, v, chain0, n_chains, step0, n_steps,      \
@@ -1746,7 +1752,8 @@ int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
     scratch_layout(n_chains, n_steps, scratch, &sg);
     const uint32_t cb = (n_chains + 255) / 256;
     const int64_t utc0 = eng->gp.clock.utc0;
-    hipEvent_t t_step = eng->mark(s);
+    hipEvent_t t_step = phases == PH_ALL ? eng->mark(s) : nullptr;
+    if (phases & PH_WALK) {
     hipLaunchKernelGGL(event_draws_kernel, dim3(sg.evcap, cb), dim3(256), 0, s, eng->dp, chain0, n_chains, n_steps,
                        pv.events, pv.n_events, sg.evd);
     if (eng->dp.markov)
@@ -1760,6 +1767,8 @@ int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
                        step0, n_steps, eng->gp.clock, pv.events, pv.n_events, sg);
     eng->close(TMH_K_SEGMENTS, t_seg, s);
     if (int rc = hip_check(hipGetLastError(), "draws/segments kernels launch")) return rc;
+    }
+    if (!(phases & PH_EXPAND)) return TMH_OK;
     hipEvent_t t_exp = eng->mark(s);
     dim3 grid2(nblk_of(n_steps), cb);
     const bool no_stats = !sv.hist && !sv.acc;
@@ -1793,6 +1802,29 @@ int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
                            pv.desc + nblk_of(n_steps), eng->dp.markov);
     eng->close(TMH_K_STEP, t_step, s);
     return hip_check(hipGetLastError(), "commit_kernel launch");
+}
+
+int tmh_step(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, int64_t step0,
+             uint32_t n_steps, const tmh_ustream* inj, const tmh_trace* trace, const tmh_stats* stats,
+             const void* plan, void* scratch, size_t scratch_bytes, void* stream)
+{
+    return step_phases(eng, state, chain0, n_chains, step0, n_steps, inj, trace, stats, plan, scratch, scratch_bytes,
+                       stream, PH_ALL);
+}
+
+int tmh_walk(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, int64_t step0,
+             uint32_t n_steps, const void* plan, void* scratch, size_t scratch_bytes, void* stream)
+{
+    return step_phases(eng, state, chain0, n_chains, step0, n_steps, nullptr, nullptr, nullptr, plan, scratch,
+                       scratch_bytes, stream, PH_WALK);
+}
+
+int tmh_expand(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, int64_t step0,
+               uint32_t n_steps, const tmh_ustream* inj, const tmh_trace* trace, const tmh_stats* stats,
+               const void* plan, void* scratch, size_t scratch_bytes, void* stream)
+{
+    return step_phases(eng, state, chain0, n_chains, step0, n_steps, inj, trace, stats, plan, scratch, scratch_bytes,
+                       stream, PH_EXPAND);
 }
 
 int tmh_run(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, int64_t step0,
