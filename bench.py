@@ -246,6 +246,15 @@ def main():
                      ("candidates", _lib.K_CANDIDATES), ("tmh_step", _lib.K_STEP)):
         ms, cnt = _lib.profile_read(sim._eng, kk)
         phases[name] = ms / cnt if cnt else None
+    # the dominant kernel alone: one more batch with nothing beside it (after the timed
+    # region, not part of `value`): its duration without the pipelined walks sharing the CUs
+    one_step(args.warmup + args.steps)
+    torch.cuda.synchronize()
+    alone_ms, alone_n = _lib.profile_read(sim._eng, _lib.K_EXPAND)
+    alone_ms = alone_ms / alone_n if alone_n else float("nan")
+    alone_ms *= 1 if nwin == 1 else nwin
+    for kk in (_lib.K_SEGMENTS, _lib.K_CANDIDATES, _lib.K_STEP):
+        _lib.profile_read(sim._eng, kk)
     bad = 0
     for cx in ctxs:
         sim.state = cx.state
@@ -275,7 +284,11 @@ def main():
         "roofline": ({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": achieved / HBM_PEAK_GBS, "traffic": traffic(args, n, secs),
                       "kernel": "expand_kernel (P2, " + sim.path + ")", "kernel_ms": kmean,
-                      "bytes_per_launch": TRACE_BYTES * n * secs} if args.mode == "trace" else
+                      "bytes_per_launch": TRACE_BYTES * n * secs,
+                      # the same launch with no other batch in flight (one extra batch after the timed region)
+                      "alone": {"kernel_ms": alone_ms, "achieved": TRACE_BYTES * n * secs / (alone_ms / 1e3) / 1e9,
+                                "frac": TRACE_BYTES * n * secs / (alone_ms / 1e3) / 1e9 / HBM_PEAK_GBS}}
+                     if args.mode == "trace" else
                      {"bound": "valu", "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
                       "kernel": "expand_kernel (P2, " + sim.path + ")", "kernel_ms": kmean,
                       "note": "stats mode stores no trace; VALU counters under profiles/"}),
