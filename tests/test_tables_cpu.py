@@ -82,3 +82,29 @@ def test_oracle_sites_equal_to_default_change_nothing():
     c = O.run(mp, 0, n, steps, start, tz="Europe/Berlin", sites=far)
     np.testing.assert_array_equal(a["csi"], c["csi"])
     assert not np.allclose(a["pv"], c["pv"])
+
+
+def test_shapes_csv_round_trip(tmp_path):
+    """Shape-table I/O in the mc_dist_shapes.csv format (cloud_cover_hourly.py:282-288):
+    the default table and per-site tables written by save_shapes_csv load back through
+    load_shapes_csv (pandas' reader, as the reference loads them) with the Student-t bin,
+    the right edges and the parameters.  pandas' default float parser is not correctly
+    rounded: tiny parameters come back up to ~1e-13 relative off, which is
+    why the engine is always given the bits load_shapes_csv returns, i.e. the bits the
+    reference's own loader produces from the same file."""
+    from tmhpvsim_amd.params import EDGES, load_shapes_csv, load_site_tables, save_shapes_csv, save_site_tables
+    tab, is_t = site_shape_tables(3, site0=11)
+    cases = [(np.array(SHAPES), np.array(SHAPE_IS_T))] + [(tab[i], is_t[i]) for i in range(3)]
+    for i, (sh0, it0) in enumerate(cases):
+        f = tmp_path / f"shapes{i}.csv"
+        save_shapes_csv(f, sh0, it0, EDGES)
+        sh, it, ed = load_shapes_csv(f)
+        np.testing.assert_allclose(sh, sh0, rtol=1e-12, atol=0, equal_nan=True)
+        np.testing.assert_array_equal(it, it0)
+        np.testing.assert_array_equal(ed, EDGES)
+    lines = open(tmp_path / "shapes0.csv").read().splitlines()
+    assert lines[0] == ",,loc,scale,kappa,df,dist" and lines[3].endswith(",t") and lines[1].startswith("-0.001,0.1,")
+    save_site_tables(tmp_path / "t.npz", tab, is_t)
+    t2, i2 = load_site_tables(tmp_path / "t.npz")
+    np.testing.assert_array_equal(np.nan_to_num(t2, nan=-1), np.nan_to_num(tab, nan=-1))
+    np.testing.assert_array_equal(i2, is_t)

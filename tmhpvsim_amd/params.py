@@ -137,6 +137,39 @@ def load_shapes_csv(path):
     return shapes, is_t, edges
 
 
+def save_shapes_csv(path, shapes, is_t, edges, lefts=None):
+    """Write a shape table in the reference's mc_dist_shapes.csv format
+    (cloud_cover_hourly.py:282-288 reads it: a two-level (left, right] interval
+    index, then loc, scale, kappa, df, dist with 'al' / 't').  Values are written
+    with Python's shortest round-trip repr; NaN cells stay empty.  `lefts`
+    defaults to (-0.001, then the previous right edge)."""
+    shapes = np.asarray(shapes, dtype=np.float64)
+    edges = np.asarray(edges, dtype=np.float64)
+    if lefts is None:
+        lefts = np.concatenate([[-0.001], edges[:-1]])
+
+    def cell(v):
+        return "" if not np.isfinite(v) else repr(float(v))
+
+    with open(path, "w") as f:
+        f.write(",,loc,scale,kappa,df,dist\n")
+        for i in range(len(edges)):
+            t = bool(is_t[i])
+            f.write(",".join([repr(float(lefts[i])), repr(float(edges[i])), cell(shapes[i, 0]), cell(shapes[i, 1]),
+                              "" if t else cell(shapes[i, 2]), cell(shapes[i, 3]) if t else "",
+                              "t" if t else "al"]) + "\n")
+
+
+def save_site_tables(path, shapes, is_t):
+    """Per-site shape tables ([n, 6, 4] fp64, [n, 6] int32) as an .npz (no pickles)."""
+    np.savez(path, shapes=np.asarray(shapes, dtype=np.float64), is_t=np.asarray(is_t, dtype=np.int32))
+
+
+def load_site_tables(path):
+    d = np.load(path, allow_pickle=False)
+    return d["shapes"], d["is_t"]
+
+
 def _philox4x32_10(ctr, key):
     """Philox4x32-10 (Random123) on uint32 arrays ctr (..., 4), key (..., 2); host-side
     table generation only (the kernels' Philox is tmhpvsim_amd/csrc/tmh_math.h)."""
