@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--path", default="auto", choices=["auto", "sequential", "time_parallel"])
     ap.add_argument("--no-stagger", dest="stagger", action="store_false",
                     help="issue each batch as one tmh_step (batches then run in lockstep across streams)")
+    ap.add_argument("--walk-priority", default="high", choices=["high", "normal"],
+                    help="HIP stream priority of the construction + segment walk (pipelined batches)")
     ap.add_argument("--pipeline", type=int, default=3,
                     help="batches in flight on separate HIP streams (1 = no overlap): the segment walks of the "
                          "next batches (latency-bound, one wave per SIMD) run beside this batch's expansion")
@@ -140,10 +142,18 @@ def main():
                      precision=args.precision, chain0=rank * n, device=dev, horizon=secs, kernel_path=args.path, **kw)
     real = sim.real
 
-    class Ctx:   # one batch in flight: its own state, plan, scratch, outputs and HIP stream
+    prio_lo, prio_hi = torch.cuda.Stream.priority_range()
+
+    class Ctx:   # one batch in flight: its own state, plan, scratch, outputs and HIP streams
         def __init__(self):
             self.stream = torch.cuda.Stream(dev)
             self.sptr = C.c_void_p(self.stream.cuda_stream)
+            # the walk runs on a stream of its own, high priority by default: its
+            # long-lived workgroups take CU slots as the expansion's short ones retire
+            self.wstream = torch.cuda.Stream(dev, priority=prio_hi if args.walk_priority == "high" else prio_lo)
+            self.wptr = C.c_void_p(self.wstream.cuda_stream)
+            self.walked = torch.cuda.Event()
+            self.done = torch.cuda.Event()
             self.state = torch.zeros(L.tmh_state_bytes(n), dtype=torch.uint8, device=dev)
             self.plan = torch.empty(L.tmh_plan_bytes(win), dtype=torch.uint8, device=dev)
             self.scratch = torch.empty(L.tmh_scratch_bytes(n, win), dtype=torch.uint8, device=dev)
@@ -159,6 +169,11 @@ def main():
                 self.st = _lib.Stats(self.hist.data_ptr(), 4096, 0, -300.0, 9000.0, self.acc.data_ptr())
 
     ctxs = [Ctx() for _ in range(max(1, args.pipeline))]
+    # one stream for every batch's expansion: expansions run back to back, in order
+    # (they fill the chip on their own), while the walks of the next batches run on
+    # their contexts' high-priority streams beside them
+    estream = torch.cuda.Stream(dev)
+    eptr = C.c_void_p(estream.cuda_stream)
     torch.cuda.synchronize()
     L.tmh_profile_enable(sim._eng, 1)
 
@@ -176,41 +191,56 @@ def main():
                                   C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
                                   cx.scratch.numel(), cx.sptr))
 
-    def start(k):      # one-window batch, first half: construction, plan, segment walk (tmh_walk)
+    def build(k):      # construction of batch k's chains and its plan, on the expansion stream
+        cx = ctxs[k % len(ctxs)]      # (in order after the expansion that last used this context;
+        cx.chain0 = (rank + k * world) * n   # beside a running expansion these small grids would starve)
+        _lib.check(L.tmh_init(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, None, eptr))
+        _lib.check(L.tmh_plan(sim._eng, 0, secs, C.c_void_p(cx.plan.data_ptr()), eptr))
+        cx.done.record(estream)
+
+    def start(k):      # the segment walk (tmh_walk) of batch k, on its context's walk stream
         cx = ctxs[k % len(ctxs)]
-        cx.chain0 = (rank + k * world) * n                 # fresh global chains every batch
-        _lib.check(L.tmh_init(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, None, cx.sptr))
-        _lib.check(L.tmh_plan(sim._eng, 0, secs, C.c_void_p(cx.plan.data_ptr()), cx.sptr))
+        cx.wstream.wait_event(cx.done)
         _lib.check(L.tmh_walk(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs,
                               C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()), cx.scratch.numel(),
-                              cx.sptr))
+                              cx.wptr))
+        cx.walked.record(cx.wstream)
 
     def finish(k):     # second half: expansion (trace / stats) and commit (tmh_expand)
         cx = ctxs[k % len(ctxs)]
+        estream.wait_event(cx.walked)
         _lib.check(L.tmh_expand(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs, None,
                                 C.byref(cx.tr), C.byref(cx.st) if cx.st is not None else None,
                                 C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
-                                cx.scratch.numel(), cx.sptr))
+                                cx.scratch.numel(), eptr))
 
     def run_batches(k0, cnt):
         """Batches k0 .. k0 + cnt - 1.  One-window batches are software-pipelined:
-        the walks of the next (depth - 1) batches are issued ahead of this batch's
-        expansion, on their own streams, so the latency-bound segment walks overlap
-        the expansion instead of running in lockstep with it."""
+        construction + plan and the expansions run in order on one stream, the
+        segment walks of the next (depth - 1) batches on high-priority streams beside
+        them, so the one-wave-per-SIMD walks overlap the expansion instead of running
+        in lockstep with it (separate per-batch streams drift into lockstep: every
+        expansion then shares the chip with the others and with every walk)."""
         if nwin > 1 or not args.stagger:
             for k in range(k0, k0 + cnt):
                 one_step(k)
             return
-        ahead = len(ctxs) - 1
+        D = len(ctxs)
+        ahead = D - 1
+        for k in range(k0, min(k0 + D, k0 + cnt)):
+            build(k)
         for k in range(k0, min(k0 + ahead, k0 + cnt)):
             start(k)
         for k in range(k0, k0 + cnt):
             if k + ahead < k0 + cnt:
                 start(k + ahead)
             finish(k)
+            if k + D < k0 + cnt:
+                build(k + D)
 
     def exchange():
         """stats mode: the one cross-GPU step, an RCCL all-reduce of the aggregate statistics"""
+        estream.synchronize()
         for cx in ctxs:
             cx.stream.synchronize()
         hist = sum(cx.hist for cx in ctxs)

@@ -1004,6 +1004,9 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
 #ifndef TMH_ROW_PREFETCH
 #define TMH_ROW_PREFETCH 0
 #endif
+#ifndef TMH_DIAG_EXP_LDS   // diagnostic: extra LDS per expand workgroup (caps its occupancy)
+#define TMH_DIAG_EXP_LDS 0
+#endif
 #ifndef TMH_EXP_WAVES   // min waves per SIMD of the fp32 single-site expansion: 6 = at most 80 VGPRs (-3.5 % vs 5)
 #define TMH_EXP_WAVES 6
 #endif
@@ -1776,7 +1779,7 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
                     : (!tv.pv && !tv.meter && !tv.residual && !tv.csi && !tv.covered) ? OUT_STATS
                                                                                       : OUT_ANY;
 #define LAUNCH(R, O, S)                                                                                              \
-    hipLaunchKernelGGL((expand_kernel<R, O, S>), grid2, dim3(256), lds, s, eng->kp, eng->dp, v, chain0, n_chains,      \
+    hipLaunchKernelGGL((expand_kernel<R, O, S>), grid2, dim3(256), lds + TMH_DIAG_EXP_LDS, s, eng->kp, eng->dp, v, chain0, n_chains,      \
                        step0, n_steps, utc0, pv.tab64, pv.tab32, pv.sun, pv.events, pv.n_events, pv.desc, sg, tv, sv)
     if (eng->kp.sites) {   // per-chain sites: one instantiation per precision, any output
         if (f64) LAUNCH(double, OUT_ANY, true);
