@@ -39,8 +39,9 @@ TRACE_BYTES = 12               # meter + pv + residual, fp32
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="c2", choices=["c2", "c5"],
-                    help="c2: the headline (BASELINE.json configs[1]); c5: the lat/lon sweep (65,536 sites x 1 "
+    ap.add_argument("--workload", default="c2", choices=["c2", "c4", "c5"],
+                    help="c2: the headline (BASELINE.json configs[1]); c4: 16,384 chains x the year 2019 "
+                         "(Europe/Berlin wall clock, stats, day windows); c5: the lat/lon sweep (65,536 sites x 1 "
                          "week, markov cc with per-site tables, per-site PV geometry, stats mode, day windows)")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8)
@@ -53,7 +54,7 @@ def parse():
                          "AssertionError (cloud_cover_binary.py:91) ends most chains within days)")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64"])
     ap.add_argument("--mode", default=None, choices=["trace", "stats"], help="c2: trace, c5: stats")
-    ap.add_argument("--start", default="2019-09-05 00:00:00")
+    ap.add_argument("--start", default=None, help="c2/c5: 2019-09-05 00:00:00, c4: 2019-01-01 00:00:00")
     ap.add_argument("--cpu-sample-chains", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--path", default="auto", choices=["auto", "sequential", "time_parallel"])
@@ -65,12 +66,13 @@ def parse():
                     help="batches in flight on separate HIP streams (1 = no overlap): the segment walks of the "
                          "next batches (latency-bound, one wave per SIMD) run beside this batch's expansion")
     a = ap.parse_args()
-    c5 = a.workload == "c5"
-    a.chains = a.chains or (65536 if c5 else 4096)
-    a.seconds = a.seconds or (604800 if c5 else 86400)
-    a.mode = a.mode or ("stats" if c5 else "trace")
+    c5, c4 = a.workload == "c5", a.workload == "c4"
+    a.chains = a.chains or {"c2": 4096, "c4": 16384, "c5": 65536}[a.workload]
+    a.seconds = a.seconds or {"c2": 86400, "c4": 365 * 86400, "c5": 604800}[a.workload]
+    a.mode = a.mode or ("trace" if a.workload == "c2" else "stats")
     a.cc = a.cc or ("markov" if c5 else "faithful")
-    a.window = min(a.window or (86400 if c5 else a.seconds), a.seconds)
+    a.window = min(a.window or (86400 if (c5 or c4) else a.seconds), a.seconds)
+    a.start = a.start or ("2019-01-01 00:00:00" if c4 else "2019-09-05 00:00:00")
     return a
 
 
@@ -142,6 +144,7 @@ def main():
                      precision=args.precision, chain0=rank * n, device=dev, horizon=secs, kernel_path=args.path, **kw)
     real = sim.real
 
+    nwin = (secs + win - 1) // win
     prio_lo, prio_hi = torch.cuda.Stream.priority_range()
 
     class Ctx:   # one batch in flight: its own state, plan, scratch, outputs and HIP streams
@@ -157,6 +160,11 @@ def main():
             self.state = torch.zeros(L.tmh_state_bytes(n), dtype=torch.uint8, device=dev)
             self.plan = torch.empty(L.tmh_plan_bytes(win), dtype=torch.uint8, device=dev)
             self.scratch = torch.empty(L.tmh_scratch_bytes(n, win), dtype=torch.uint8, device=dev)
+            if nwin > 1:   # second plan + scratch: window w+1's walk beside window w's expansion
+                self.plan2 = torch.empty_like(self.plan)
+                self.scratch2 = torch.empty_like(self.scratch)
+                self.wev = [torch.cuda.Event(), torch.cuda.Event()]
+                self.eev = [torch.cuda.Event(), torch.cuda.Event()]
             self.trace = {f: torch.empty(win, n, dtype=real, device=dev) for f in ("pv", "meter", "residual")} \
                 if args.mode == "trace" else {}
             self.tr = _lib.Trace(None, None, *(self.trace[f].data_ptr() if f in self.trace else None
@@ -177,33 +185,73 @@ def main():
     torch.cuda.synchronize()
     L.tmh_profile_enable(sim._eng, 1)
 
-    nwin = (secs + win - 1) // win
-
-    def one_step(k):   # a whole batch on its context's stream (multi-window batches)
+    def one_step(k):   # a whole batch on its context's streams
         cx = ctxs[k % len(ctxs)]
         chain0 = (rank + k * world) * n                    # fresh global chains every batch
         _lib.check(L.tmh_init(sim._eng, C.c_void_p(cx.state.data_ptr()), chain0, n, None, cx.sptr))
-        for s0 in range(0, secs, win):   # windows: a trace window is overwritten by the next
-            w = min(win, secs - s0)
-            _lib.check(L.tmh_plan(sim._eng, s0, w, C.c_void_p(cx.plan.data_ptr()), cx.sptr))
-            _lib.check(L.tmh_step(sim._eng, C.c_void_p(cx.state.data_ptr()), chain0, n, s0, w, None,
-                                  C.byref(cx.tr), C.byref(cx.st) if cx.st is not None else None,
-                                  C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
-                                  cx.scratch.numel(), cx.sptr))
+        if nwin == 1 or sim.path != "time_parallel":
+            for s0 in range(0, secs, win):   # windows: a trace window is overwritten by the next
+                w = min(win, secs - s0)
+                _lib.check(L.tmh_plan(sim._eng, s0, w, C.c_void_p(cx.plan.data_ptr()), cx.sptr))
+                _lib.check(L.tmh_step(sim._eng, C.c_void_p(cx.state.data_ptr()), chain0, n, s0, w, None,
+                                      C.byref(cx.tr), C.byref(cx.st) if cx.st is not None else None,
+                                      C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
+                                      cx.scratch.numel(), cx.sptr))
+            return
+        # multi-window: the segment walk of window w+1 (high-priority stream) beside the
+        # expansion of window w; plans and draws on the expansion's stream (as BatchedSim.run)
+        bufs = [(cx.plan, cx.scratch), (cx.plan2, cx.scratch2)]
+        wins = [(s0, min(win, secs - s0)) for s0 in range(0, secs, win)]
+        sp = C.c_void_p(cx.state.data_ptr())
 
-    def build(k):      # construction of batch k's chains and its plan, on the expansion stream
+        def views(w):
+            return tuple(C.c_void_p(t.data_ptr()) for t in bufs[w & 1])
+
+        def prev_of(w):
+            return (views(w - 1)[1], wins[w - 1][1]) if w > 0 else (None, 0)
+
+        def draws(w):
+            pl, sc = views(w)
+            _lib.check(L.tmh_plan(sim._eng, wins[w][0], wins[w][1], pl, cx.sptr))
+            _lib.check(L.tmh_walk_part(sim._eng, sp, chain0, n, wins[w][0], wins[w][1], pl, sc, cx.scratch.numel(),
+                                       *prev_of(w), _lib.WALK_DRAWS, cx.sptr))
+            cx.wev[w & 1].record(cx.stream)
+
+        def segments(w):
+            pl, sc = views(w)
+            cx.wstream.wait_event(cx.wev[w & 1])
+            _lib.check(L.tmh_walk_part(sim._eng, sp, chain0, n, wins[w][0], wins[w][1], pl, sc, cx.scratch.numel(),
+                                       *prev_of(w), _lib.WALK_SEGMENTS, cx.wptr))
+            cx.eev[w & 1].record(cx.wstream)
+
+        draws(0)
+        segments(0)
+        for w in range(len(wins)):
+            cx.stream.wait_event(cx.eev[w & 1])
+            if w + 1 < len(wins):
+                draws(w + 1)
+                segments(w + 1)
+            pl, sc = views(w)
+            _lib.check(L.tmh_expand(sim._eng, sp, chain0, n, wins[w][0], wins[w][1], None,
+                                    C.byref(cx.tr), C.byref(cx.st) if cx.st is not None else None, pl, sc,
+                                    cx.scratch.numel(), cx.sptr))
+
+    def build(k):      # construction of batch k's chains, its plan and draws, on the expansion stream
         cx = ctxs[k % len(ctxs)]      # (in order after the expansion that last used this context;
         cx.chain0 = (rank + k * world) * n   # beside a running expansion these small grids would starve)
         _lib.check(L.tmh_init(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, None, eptr))
         _lib.check(L.tmh_plan(sim._eng, 0, secs, C.c_void_p(cx.plan.data_ptr()), eptr))
+        _lib.check(L.tmh_walk_part(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs,
+                                   C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
+                                   cx.scratch.numel(), None, 0, _lib.WALK_DRAWS, eptr))
         cx.done.record(estream)
 
-    def start(k):      # the segment walk (tmh_walk) of batch k, on its context's walk stream
+    def start(k):      # the segment walk of batch k, on its context's walk stream
         cx = ctxs[k % len(ctxs)]
         cx.wstream.wait_event(cx.done)
-        _lib.check(L.tmh_walk(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs,
-                              C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()), cx.scratch.numel(),
-                              cx.wptr))
+        _lib.check(L.tmh_walk_part(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs,
+                                   C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
+                                   cx.scratch.numel(), None, 0, _lib.WALK_SEGMENTS, cx.wptr))
         cx.walked.record(cx.wstream)
 
     def finish(k):     # second half: expansion (trace / stats) and commit (tmh_expand)
@@ -305,7 +353,8 @@ def main():
         "value": value, "unit": "chain-seconds/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic (keyed Philox)",
-        "config": {"workload": (f"C2: {n} chains/GPU x {secs} s at 1 s, Munich, Europe/Berlin, " if not c5 else
+        "config": {"workload": (f"{args.workload.upper()}: {n} chains/GPU x {secs} s at 1 s, Munich, Europe/Berlin, "
+                                + (f"{win} s windows, " if nwin > 1 else "") if not c5 else
                                 f"C5: {n} sites/GPU on a lat/lon grid (35-60 N, 10 W-30 E) x {secs} s, {args.cc} cc "
                                 f"with per-site tables, per-site PV geometry, {win} s windows, Europe/Berlin, ")
                                + f"{args.start[:10]}, {args.mode} mode ({'meter+pv+residual fp32 trace' if args.mode == 'trace' else 'on-GPU stats'})",

@@ -222,6 +222,26 @@ int tmh_expand(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_
                uint32_t n_steps, const tmh_ustream* inj, const tmh_trace* trace, const tmh_stats* stats,
                const void* plan, void* scratch, size_t scratch_bytes, void* stream);
 
+/* The walk in parts and across windows (time-parallel path).
+ * parts: TMH_WALK_DRAWS = boundary draws, markov hourly cover and candidate cloud
+ * lengths (many small workgroups); TMH_WALK_SEGMENTS = the P1 segment walk (one
+ * wave per SIMD, long-lived).  Small grids issued beside a running expansion
+ * wait for CU slots, so a pipelining caller puts the draws on the expansion's
+ * stream and only the segment walk on a second, high-priority stream.
+ * prev_scratch (nullable): the scratch (laid out for prev_n_steps) of the previous
+ * window of these chains; the window-start status, cloud-cover and wind pairs then
+ * come from that window's walk instead of the state, so this walk may run while
+ * the previous window's expansion and commit are in flight.  Order: draws(w+1)
+ * after segments(w); segments(w+1) after draws(w+1); expand(w+1) after
+ * segments(w+1) and expand(w); any part of w+2 after expand(w), the last reader
+ * of the buffers w+2 reuses (BatchedSim.run, bench.py).  Same bits as tmh_step
+ * window by window. */
+#define TMH_WALK_DRAWS 1
+#define TMH_WALK_SEGMENTS 2
+int tmh_walk_part(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, int64_t step0,
+                  uint32_t n_steps, const void* plan, void* scratch, size_t scratch_bytes,
+                  const void* prev_scratch, uint32_t prev_n_steps, int parts, void* stream);
+
 /* Kernel timing (measurement only).  While enabled, tmh_step records HIP
  * events, on the stream each kernel runs on, around the kernels of the
  * time-parallel path; tmh_profile_read waits for them and returns the summed

@@ -348,6 +348,30 @@ def test_walk_then_expand_equals_step(path):
     assert _same(a.state_field("sa_cc"), b.state_field("sa_cc"))
 
 
+@pytest.mark.parametrize("markov", [False, True])
+def test_pipelined_windows_equal_one_window(markov):
+    """BatchedSim.run over several windows (walk of window w+1 via tmh_walk_next beside the
+    expansion of window w) == one window: traces bit for bit, state, per-chain statistics."""
+    from tmhpvsim_amd.params import site_shape_tables
+    start, steps, n = "2019-03-30 22:00:00", 3 * 7001, 160
+    mp = ModelParams(cc_mode=CC_MARKOV) if markov else None
+    tab = site_shape_tables(n) if markov else None
+    a = _sim(n, start, tz="Europe/Berlin", mp=mp, prec="fp32", horizon=steps, tables=tab)
+    b = _sim(n, start, tz="Europe/Berlin", mp=mp, prec="fp32", horizon=steps, tables=tab)
+    a.enable_stats()
+    b.enable_stats()
+    ra = a.run(steps, window=steps)
+    rb = b.run(steps, window=3000)            # 8 windows, the last one short
+    for f in ("csi", "covered", "pv", "meter", "residual"):
+        assert _same(ra[f], rb[f]), f
+    np.testing.assert_array_equal(a.status(), b.status())
+    ok = torch.as_tensor(a.status() == 0, device="cuda:0")
+    for f in ("sa_cc", "sb_ws", "sa_clear_noise", "cloud_length", "sec", "sigma_len", "markov_state"):
+        assert _same(a.state_field(f)[ok], b.state_field(f)[ok]), f
+    assert torch.equal(a.hist, b.hist)
+    np.testing.assert_allclose(a.chain_acc[:, ok].cpu().numpy(), b.chain_acc[:, ok].cpu().numpy(), rtol=1e-12)
+
+
 def test_stats_match_trace():
     start, steps, n = "2019-09-05 00:00:00", 20000, 512
     s = _sim(n, start, tz="Europe/Berlin", prec="fp32", horizon=steps)

@@ -63,8 +63,10 @@ class Stats(C.Structure):
 EXPORTS = ["tmh_abi_version", "tmh_last_error", "tmh_state_bytes", "tmh_state_offsets", "tmh_plan_bytes",
            "tmh_scratch_bytes", "tmh_workspace_bytes", "tmh_engine_create", "tmh_engine_destroy", "tmh_engine_path",
            "tmh_init", "tmh_run", "tmh_plan", "tmh_step", "tmh_probe", "tmh_profile_enable", "tmh_profile_read",
-           "tmh_set_shape_tables", "tmh_set_sites", "tmh_walk", "tmh_expand"]
+           "tmh_set_shape_tables", "tmh_set_sites", "tmh_walk", "tmh_expand",
+           "tmh_walk_part"]
 K_EXPAND, K_SEGMENTS, K_CANDIDATES, K_STEP = 0, 1, 2, 3
+WALK_DRAWS, WALK_SEGMENTS = 1, 2
 
 _lib = None
 
@@ -108,6 +110,7 @@ def load():
                            sz, p]
     L.tmh_plan.argtypes = [p, i64, u32, p, p]
     L.tmh_walk.argtypes = [p, p, u64, u32, i64, u32, p, p, sz, p]
+    L.tmh_walk_part.argtypes = [p, p, u64, u32, i64, u32, p, p, sz, p, u32, C.c_int, p]
     L.tmh_expand.argtypes = [p, p, u64, u32, i64, u32, C.POINTER(UStream), C.POINTER(Trace), C.POINTER(Stats), p, p,
                              sz, p]
     L.tmh_probe.argtypes = [C.c_int, C.c_double, p, p, u32, p]
@@ -117,7 +120,7 @@ def load():
     L.tmh_profile_read.argtypes = [p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int)]
     for name in ("tmh_state_offsets", "tmh_engine_create", "tmh_engine_destroy", "tmh_engine_path", "tmh_init",
                  "tmh_run", "tmh_step", "tmh_plan", "tmh_probe", "tmh_profile_enable", "tmh_profile_read",
-                 "tmh_set_shape_tables", "tmh_set_sites", "tmh_walk", "tmh_expand"):
+                 "tmh_set_shape_tables", "tmh_set_sites", "tmh_walk", "tmh_expand", "tmh_walk_part"):
         getattr(L, name).restype = C.c_int
     if L.tmh_abi_version() != TMH_ABI_VERSION:
         raise ImportError(f"libtmhpvsim ABI {L.tmh_abi_version()} != {TMH_ABI_VERSION}")

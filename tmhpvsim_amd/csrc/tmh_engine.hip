@@ -72,6 +72,16 @@ struct SegView {                   // P1 -> P2 scratch
     uint32_t kcap;
 };
 
+// The window-start values a walk takes from the PREVIOUS window's walk instead of
+// the state (tmh_walk_next): status and the (before, after) cloud-cover and wind
+// pairs at that window's end, so a walk can run while the previous window's
+// expansion and commit are still in flight.  status == NULL: read the state.
+struct PrevView {
+    const uint32_t* status;
+    const double* end_p1;   // [4][n]: cc before/after, ws before/after
+};
+
+
 // ------------------------------------------------------------ state I/O
 __device__ __forceinline__ void load_chain(const StateView& st, uint32_t c, Chain& ch)
 {
@@ -349,13 +359,14 @@ __global__ __launch_bounds__(256) void event_draws_kernel(DrawParams dp, uint64_
 // _next_hour push the markov state), so nothing extra is carried over.
 __global__ __launch_bounds__(256) void markov_cc_kernel(KParams kp, StateView st, uint64_t chain0, uint32_t n,
                                                         uint32_t nsteps, const int2* __restrict__ events,
-                                                        const uint32_t* __restrict__ n_events, double* evd)
+                                                        const uint32_t* __restrict__ n_events, double* evd,
+                                                        PrevView prev)
 {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n) return;
     const uint64_t chain = chain0 + c;
     const uint32_t ne = min(*n_events, ev_cap_dev(nsteps));
-    double state = st.mstate[c];
+    double state = prev.status ? prev.end_p1[(size_t)n + c] : st.mstate[c];   // the last hourly draw
     for (uint32_t e = 0; e < ne; ++e) {
         const int2 ev = events[e];
         if (!(ev.y & FL_HOUR)) continue;
@@ -600,11 +611,11 @@ __device__ __forceinline__ void fractions_at(const WinClock& w, int32_t j, doubl
 // keyed by (chain, call number) only, so they are drawn before the walk, at
 // full occupancy, instead of one wave-redundant Philox + pow per call inside it
 __global__ __launch_bounds__(256) void candidates_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
-                                                         SegView sg)
+                                                         SegView sg, PrevView prev)
 {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t k = blockIdx.y;
-    if (c >= n || st.status[c] != 0) return;
+    if (c >= n || (prev.status ? prev.status[c] : st.status[c]) != 0) return;
     const U4 b = keyed_block(dp.seed, chain0 + c, (uint64_t)(st.ncalls[c] + k), TAG_CLOUD, 0);
     sg.cand[(size_t)k * n + c] = pow_d(dp.alpha + dp.delta * u52(b.x, b.y), dp.expo);
 }
@@ -677,7 +688,8 @@ constexpr int RCH_FIXED = 4;   // chunks always processed (L <= 64 for 99.7 % of
 __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
                                                           int64_t W0, uint32_t nsteps, tmh_clock ck,
                                                           const int2* __restrict__ events,
-                                                          const uint32_t* __restrict__ n_events, SegView sg)
+                                                          const uint32_t* __restrict__ n_events, SegView sg,
+                                                          PrevView prev)
 {
     const int lane = threadIdx.x & 63, p = lane & 15, row0 = lane & ~15;
     const uint32_t c = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
@@ -685,8 +697,19 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
     const uint32_t cs = live ? c : 0;
     const uint64_t chain = chain0 + cs;
     const int64_t W1 = W0 + nsteps;
-    uint32_t status = live ? st.status[cs] : 0xFFFFFFFFu;
-    double ccb = st.sb[S_CC][cs], cca = st.sa[S_CC][cs], wsb = st.sb[S_WS][cs], wsa = st.sa[S_WS][cs];
+    uint32_t status = live ? (prev.status ? prev.status[cs] : st.status[cs]) : 0xFFFFFFFFu;
+    double ccb, cca, wsb, wsa;   // window-start cloud-cover and wind pairs
+    if (prev.status) {
+        ccb = prev.end_p1[cs];
+        cca = prev.end_p1[(size_t)n + cs];
+        wsb = prev.end_p1[2 * (size_t)n + cs];
+        wsa = prev.end_p1[3 * (size_t)n + cs];
+    } else {
+        ccb = st.sb[S_CC][cs];
+        cca = st.sa[S_CC][cs];
+        wsb = st.sb[S_WS][cs];
+        wsa = st.sa[S_WS][cs];
+    }
     int32_t fault = INT_MAX;
     uint32_t nrec = 0;
     double cl = st.cl[cs], clr = st.clr[cs];
@@ -1697,11 +1720,12 @@ int tmh_plan(struct tmh_engine* eng, int64_t step0, uint32_t n_steps, void* plan
     return hip_check(hipGetLastError(), "plan kernels launch");
 }
 
-enum { PH_WALK = 1, PH_EXPAND = 2, PH_ALL = 3 };
+enum { PH_DRAWS = 1, PH_SEGMENTS = 4, PH_WALK = PH_DRAWS | PH_SEGMENTS, PH_EXPAND = 2, PH_ALL = 7 };
 
 static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, int64_t step0,
                        uint32_t n_steps, const tmh_ustream* inj, const tmh_trace* trace, const tmh_stats* stats,
-                       const void* plan, void* scratch, size_t scratch_bytes, void* stream, int phases)
+                       const void* plan, void* scratch, size_t scratch_bytes, void* stream, int phases,
+                       PrevView prev = PrevView{nullptr, nullptr})
 {
     if (!eng || !state || !plan) return fail(TMH_E_INVAL, "NULL engine/state/plan");
     if (n_chains == 0 || n_steps == 0) return TMH_OK;
@@ -1756,20 +1780,24 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     const uint32_t cb = (n_chains + 255) / 256;
     const int64_t utc0 = eng->gp.clock.utc0;
     hipEvent_t t_step = phases == PH_ALL ? eng->mark(s) : nullptr;
-    if (phases & PH_WALK) {
-    hipLaunchKernelGGL(event_draws_kernel, dim3(sg.evcap, cb), dim3(256), 0, s, eng->dp, chain0, n_chains, n_steps,
-                       pv.events, pv.n_events, sg.evd);
-    if (eng->dp.markov)
-        hipLaunchKernelGGL(markov_cc_kernel, dim3(cb), dim3(256), 0, s, eng->kp, v, chain0, n_chains, n_steps,
+    if (phases & PH_DRAWS) {
+        hipLaunchKernelGGL(event_draws_kernel, dim3(sg.evcap, cb), dim3(256), 0, s, eng->dp, chain0, n_chains, n_steps,
                            pv.events, pv.n_events, sg.evd);
-    hipEvent_t t_cand = eng->mark(s);
-    hipLaunchKernelGGL(candidates_kernel, dim3(cb, sg.kcap), dim3(256), 0, s, eng->dp, v, chain0, n_chains, sg);
-    eng->close(TMH_K_CANDIDATES, t_cand, s);
+        if (eng->dp.markov)
+            hipLaunchKernelGGL(markov_cc_kernel, dim3(cb), dim3(256), 0, s, eng->kp, v, chain0, n_chains, n_steps,
+                               pv.events, pv.n_events, sg.evd, prev);
+        hipEvent_t t_cand = eng->mark(s);
+        hipLaunchKernelGGL(candidates_kernel, dim3(cb, sg.kcap), dim3(256), 0, s, eng->dp, v, chain0, n_chains, sg,
+                           prev);
+        eng->close(TMH_K_CANDIDATES, t_cand, s);
+        if (int rc = hip_check(hipGetLastError(), "draws kernels launch")) return rc;
+    }
+    if (phases & PH_SEGMENTS) {
     hipEvent_t t_seg = eng->mark(s);
     hipLaunchKernelGGL(segments_kernel, dim3((n_chains + 15) / 16), dim3(256), 0, s, eng->dp, v, chain0, n_chains,
-                       step0, n_steps, eng->gp.clock, pv.events, pv.n_events, sg);
+                       step0, n_steps, eng->gp.clock, pv.events, pv.n_events, sg, prev);
     eng->close(TMH_K_SEGMENTS, t_seg, s);
-    if (int rc = hip_check(hipGetLastError(), "draws/segments kernels launch")) return rc;
+    if (int rc = hip_check(hipGetLastError(), "segments kernel launch")) return rc;
     }
     if (!(phases & PH_EXPAND)) return TMH_OK;
     hipEvent_t t_exp = eng->mark(s);
@@ -1820,6 +1848,23 @@ int tmh_walk(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
 {
     return step_phases(eng, state, chain0, n_chains, step0, n_steps, nullptr, nullptr, nullptr, plan, scratch,
                        scratch_bytes, stream, PH_WALK);
+}
+
+int tmh_walk_part(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, int64_t step0,
+                  uint32_t n_steps, const void* plan, void* scratch, size_t scratch_bytes, const void* prev_scratch,
+                  uint32_t prev_n_steps, int parts, void* stream)
+{
+    if (parts & ~(TMH_WALK_DRAWS | TMH_WALK_SEGMENTS)) return fail(TMH_E_INVAL, "bad walk parts %d", parts);
+    if (eng && eng->path != TMH_PATH_TIME_PARALLEL) return fail(TMH_E_INVAL, "tmh_walk_part needs the time-parallel path");
+    PrevView prev{nullptr, nullptr};
+    if (prev_scratch) {
+        SegView ps;
+        scratch_layout(n_chains, prev_n_steps, const_cast<void*>(prev_scratch), &ps);
+        prev = PrevView{ps.status, ps.end_p1};
+    }
+    const int ph = ((parts & TMH_WALK_DRAWS) ? PH_DRAWS : 0) | ((parts & TMH_WALK_SEGMENTS) ? PH_SEGMENTS : 0);
+    return step_phases(eng, state, chain0, n_chains, step0, n_steps, nullptr, nullptr, nullptr, plan, scratch,
+                       scratch_bytes, stream, ph, prev);
 }
 
 int tmh_expand(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, int64_t step0,

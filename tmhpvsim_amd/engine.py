@@ -184,6 +184,11 @@ class BatchedSim:
                 res[f] = torch.empty(n_steps, self.n, dtype=dt, device=self.device)
         st = self._stats_struct()
         win = max(1, min(int(window), n_steps))
+        if self.path == "time_parallel" and n_steps > win:
+            with torch.cuda.device(self.device):
+                self._run_pipelined(n_steps, win, trace, res, st)
+            self.step += n_steps
+            return res
         ws = self.workspace(win)
         with torch.cuda.device(self.device):
             done = 0
@@ -198,6 +203,70 @@ class BatchedSim:
                 done += k
         self.step += n_steps
         return res
+
+    def _run_pipelined(self, n_steps, win, trace, res, st):
+        """Windows of the time-parallel path, pipelined: the segment walk of window
+        w+1 (tmh_walk_part SEGMENTS, on a high-priority stream) runs beside the
+        expansion of window w (on the current stream, which also builds each
+        window's plan and draws); two plan + scratch buffers.  Same bits as one
+        tmh_run per window (tests/test_gpu_parity.py)."""
+        torch = _torch()
+        L = self.L
+        main = torch.cuda.current_stream(self.device)
+        if getattr(self, "_wstream", None) is None:
+            self._wstream = torch.cuda.Stream(self.device, priority=torch.cuda.Stream.priority_range()[1])
+        walk = self._wstream
+        mptr, wptr = C.c_void_p(main.cuda_stream), C.c_void_p(walk.cuda_stream)
+        pb = L.tmh_plan_bytes(win)
+        bufs = [self.workspace(win), self.workspace(win)]
+        drawn = [torch.cuda.Event(), torch.cuda.Event()]
+        walked = [torch.cuda.Event(), torch.cuda.Event()]
+        wins = []
+        done = 0
+        while done < n_steps:
+            k = min(win, n_steps - done)
+            wins.append((self.step + done, k, done))
+            done += k
+
+        def views(w):
+            b = bufs[w & 1]
+            return C.c_void_p(b.data_ptr()), C.c_void_p(b.data_ptr() + pb), b.numel() - pb
+
+        def prev_of(w):
+            return (views(w - 1)[1], wins[w - 1][1]) if w > 0 else (None, 0)
+
+        def draws(w):      # plan + boundary draws + candidates of window w, on the main stream
+            s0, k, _ = wins[w]
+            plan, scr, nb = views(w)
+            _lib.check(L.tmh_plan(self._eng, s0, k, plan, mptr))
+            ps, pk = prev_of(w)
+            _lib.check(L.tmh_walk_part(self._eng, _ptr(self.state), self.chain0, self.n, s0, k, plan, scr, nb, ps, pk,
+                                       _lib.WALK_DRAWS, mptr))
+            drawn[w & 1].record(main)
+
+        def segments(w):   # the segment walk of window w, on the walk stream
+            s0, k, _ = wins[w]
+            plan, scr, nb = views(w)
+            walk.wait_event(drawn[w & 1])
+            ps, pk = prev_of(w)
+            _lib.check(L.tmh_walk_part(self._eng, _ptr(self.state), self.chain0, self.n, s0, k, plan, scr, nb, ps, pk,
+                                       _lib.WALK_SEGMENTS, wptr))
+            walked[w & 1].record(walk)
+
+        draws(0)
+        segments(0)
+        for w in range(len(wins)):
+            main.wait_event(walked[w & 1])
+            if w + 1 < len(wins):
+                draws(w + 1)       # buffer (w+1) & 1 was last read by expand(w-1), earlier on this stream
+                segments(w + 1)    # beside expand(w)
+            s0, k, off = wins[w]
+            plan, scr, nb = views(w)
+            tr = _lib.Trace(*(res[f][off:off + k].data_ptr() if f in trace else None
+                              for f in ("csi", "covered", "pv", "meter", "residual")), self.n)
+            _lib.check(L.tmh_expand(self._eng, _ptr(self.state), self.chain0, self.n, s0, k, None, C.byref(tr),
+                                    C.byref(st) if st is not None else None, plan, scr, nb, mptr))
+        self._keep = bufs   # allocated on the main stream, whose last work is the last expansion
 
     def plan(self, step0, n_steps):
         """Build the chain-independent plan of a window (tmh_plan); returns the uint8 buffer."""
