@@ -120,6 +120,50 @@ __device__ __forceinline__ void store_chain(const StateView& st, uint32_t c, con
 }
 
 // ------------------------------------------------------------ init kernel
+// The constructor's variates 2..11 (clear-day pair, cloudy-hour pair, the four
+// minute noises, the wind-speed pair: fp64 ndtri / gammaincinv, the bulk of the
+// constructor's time) one work-item per (chain, variate) instead of twelve in a
+// row per chain (keyed mode).  Parked in the chain's sigma row, entries
+// CAP-12.., which the constructor's next_cloud never reaches.
+constexpr int INIT_SLOT = CAP - 12;
+
+__device__ __forceinline__ void init_cc_pair(const KParams& kp, uint32_t c, const double* u, double& b, double& a)
+{
+    Chain ch;
+    ch.mstate = 1.0;
+    b = draw_cc(kp, c, ch, u[0]);
+    a = draw_cc(kp, c, ch, u[1]);
+}
+
+__global__ __launch_bounds__(256) void init_variates_kernel(KParams kp, StateView st, uint64_t chain0, uint32_t n,
+                                                            double hf)
+{
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    const int j = 2 + (int)blockIdx.y;   // variate 2..11
+    if (c >= n) return;
+    const uint64_t chain = chain0 + c;
+    const U4 blk = keyed_block(kp.seed, chain, 0, TAG_INIT, (uint32_t)(j >> 1));
+    const double u = (j & 1) ? u52(blk.z, blk.w) : u52(blk.x, blk.y);
+    double v;
+    if (j <= 3) {
+        v = normal(u, 0.99, 0.08);
+    } else if (j >= 10) {
+        v = 2.14 * gammaincinv(2.69, u);
+    } else {
+        const U4 b0 = keyed_block(kp.seed, chain, 0, TAG_INIT, 0);
+        const double u01[2] = {u52(b0.x, b0.y), u52(b0.z, b0.w)};
+        double ccb, cca;
+        init_cc_pair(kp, c, u01, ccb, cca);
+        const double cc = interp(ccb, cca, hf);
+        if (j <= 5) {   // clearskyindexmodel.py:68-82; 6/8 <= cc < 7/8 is the NameError
+            v = cc < 6.0 / 8 ? normal(u, 0.6784, 0.2046) : (cc < 7.0 / 8 ? NAN : gammaincinv(3.5624, u) * 0.0867 + 0.0);
+        } else {
+            v = j <= 7 ? scaled_noise(kp, u, 0.01, 0.003, cc) : scaled_noise(kp, u, 0.001, 0.0015, cc);
+        }
+    }
+    sig_c(st, c)[INIT_SLOT + j] = v;
+}
+
 // ClearskyindexModel.__init__ (clearskyindexmodel.py:57-99)
 template <int RNG>
 __global__ __launch_bounds__(256) void init_kernel(KParams kp, StateView st, uint64_t chain0, uint32_t n,
@@ -145,21 +189,31 @@ __global__ __launch_bounds__(256) void init_kernel(KParams kp, StateView st, uin
         dr.u = inj.u + (size_t)c * inj.stride;
         dr.len = inj.len;
     }
+    const double* pre = sig_c(st, c) + INIT_SLOT;   // keyed: variates 2..11 from init_variates_kernel
     double u[12];
-    for (int d = 0; d < 12; ++d) u[d] = dr.one(ch, 0, TAG_INIT, (uint32_t)(d >> 1), d & 1);
+    if constexpr (RNG == TMH_RNG_KEYED) {
+        dr.two(ch, 0, TAG_INIT, 0, u[0], u[1]);
+    } else {
+        for (int d = 0; d < 12; d += 2) dr.two(ch, 0, TAG_INIT, (uint32_t)(d >> 1), u[d], u[d + 1]);
+    }
     ch.s.b[S_CC] = draw_cc(kp, c, ch, u[0]);
     ch.s.a[S_CC] = draw_cc(kp, c, ch, u[1]);
-    ch.s.b[S_CLEAR_DAY] = normal(u[2], 0.99, 0.08);
-    ch.s.a[S_CLEAR_DAY] = normal(u[3], 0.99, 0.08);
+    if constexpr (RNG == TMH_RNG_KEYED) {
+        ch.s.b[S_CLEAR_DAY] = pre[2];
+        ch.s.a[S_CLEAR_DAY] = pre[3];
+    } else {
+        ch.s.b[S_CLEAR_DAY] = normal(u[2], 0.99, 0.08);
+        ch.s.a[S_CLEAR_DAY] = normal(u[3], 0.99, 0.08);
+    }
     bool name_error = false;
     for (int j = 0; j < 2; ++j) {   // :68-82
         const double cc = interp(ch.s.b[S_CC], ch.s.a[S_CC], hf);
         double v;
-        if (cc < 6.0 / 8) v = normal(u[4 + j], 0.6784, 0.2046);
+        if (cc < 6.0 / 8) v = RNG == TMH_RNG_KEYED ? pre[4 + j] : normal(u[4 + j], 0.6784, 0.2046);
         else if (cc < 7.0 / 8) {
             name_error = true;       // gamma.pdf(x, ...) with x undefined (:80)
             break;
-        } else v = gammaincinv(3.5624, u[4 + j]) * 0.0867 + 0.0;
+        } else v = RNG == TMH_RNG_KEYED ? pre[4 + j] : gammaincinv(3.5624, u[4 + j]) * 0.0867 + 0.0;
         if (j == 0) ch.s.b[S_CLOUDY_HOUR] = v;
         else ch.s.a[S_CLOUDY_HOUR] = v;
     }
@@ -169,21 +223,29 @@ __global__ __launch_bounds__(256) void init_kernel(KParams kp, StateView st, uin
         store_chain(st, c, ch);
         return;
     }
-    const double cch = interp(ch.s.b[S_CC], ch.s.a[S_CC], hf);
-    ch.s.b[S_CLOUDY_NOISE] = scaled_noise(kp, u[6], 0.01, 0.003, cch);
-    ch.s.a[S_CLOUDY_NOISE] = scaled_noise(kp, u[7], 0.01, 0.003, cch);
-    ch.s.b[S_CLEAR_NOISE] = scaled_noise(kp, u[8], 0.001, 0.0015, cch);
-    ch.s.a[S_CLEAR_NOISE] = scaled_noise(kp, u[9], 0.001, 0.0015, cch);
-    ch.s.b[S_WS] = 2.14 * gammaincinv(2.69, u[10]);
-    ch.s.a[S_WS] = 2.14 * gammaincinv(2.69, u[11]);
+    if constexpr (RNG == TMH_RNG_KEYED) {
+        ch.s.b[S_CLOUDY_NOISE] = pre[6];
+        ch.s.a[S_CLOUDY_NOISE] = pre[7];
+        ch.s.b[S_CLEAR_NOISE] = pre[8];
+        ch.s.a[S_CLEAR_NOISE] = pre[9];
+        ch.s.b[S_WS] = pre[10];
+        ch.s.a[S_WS] = pre[11];
+    } else {
+        const double cch = interp(ch.s.b[S_CC], ch.s.a[S_CC], hf);
+        ch.s.b[S_CLOUDY_NOISE] = scaled_noise(kp, u[6], 0.01, 0.003, cch);
+        ch.s.a[S_CLOUDY_NOISE] = scaled_noise(kp, u[7], 0.01, 0.003, cch);
+        ch.s.b[S_CLEAR_NOISE] = scaled_noise(kp, u[8], 0.001, 0.0015, cch);
+        ch.s.a[S_CLEAR_NOISE] = scaled_noise(kp, u[9], 0.001, 0.0015, cch);
+        ch.s.b[S_WS] = 2.14 * gammaincinv(2.69, u[10]);
+        ch.s.a[S_WS] = 2.14 * gammaincinv(2.69, u[11]);
+    }
     // CloudCoverBinary(cc.interpolate(0), ws.interpolate(0)) (:98-99)
     const double h0 = interp(ch.s.b[S_CC], ch.s.a[S_CC], 0.0);
     const double h = 0.95 < h0 ? 0.95 : h0;
     const double ws = interp(ch.s.b[S_WS], ch.s.a[S_WS], 0.0);
     double* sc = sig_c(st, c);
     double* sl = sig_l(st, c);
-    reset_sigma(sc, sl, ch, h);
-    const uint32_t f = next_cloud<RNG>(kp, sc, sl, ch, dr, h, ws, TAG_INIT_CLOUD);
+    const uint32_t f = next_cloud_fresh<RNG>(kp, sc, sl, ch, dr, h, ws, TAG_INIT_CLOUD);   // reset_sigma + next_cloud
     if (!f) {
         const double us = dr.one(ch, 0, TAG_INIT_SEC, 0, 0);
         ch.sec = (int32_t)((ch.cl + ch.clr) * us);   // cloud_cover_binary.py:68
@@ -1694,7 +1756,10 @@ int tmh_init(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
     dim3 grid((n_chains + 255) / 256), block(256);
     hipStream_t s = (hipStream_t)stream;
     if (eng->kp.rng_mode == TMH_RNG_KEYED)
+    {
+        hipLaunchKernelGGL(init_variates_kernel, dim3(grid.x, 10), block, 0, s, eng->kp, v, chain0, n_chains, hf);
         hipLaunchKernelGGL(init_kernel<TMH_RNG_KEYED>, grid, block, 0, s, eng->kp, v, chain0, n_chains, hf, iv);
+    }
     else
         hipLaunchKernelGGL(init_kernel<TMH_RNG_INJECTED>, grid, block, 0, s, eng->kp, v, chain0, n_chains, hf, iv);
     return hip_check(hipGetLastError(), "init_kernel launch");

@@ -291,6 +291,62 @@ __device__ uint32_t next_cloud(const KParams& kp, double* sc, double* sl, Chain&
     return TMH_CHAIN_ASSERT_BINARY;
 }
 
+// next_cloud on freshly reset sigma arrays: the constructor's call
+// (CloudCoverBinary.__init__, cloud_cover_binary.py:63-78, then :80-107).  After
+// reset_sigma entry k is exactly 300 (k + 1) and f * 300 (k + 1) (both resets of
+// the 40-try loop give the same arrays), so the scan computes the entries instead
+// of loading them and only the result is stored; same draws, same bits as
+// reset_sigma + next_cloud.
+template <int RNG>
+__device__ uint32_t next_cloud_fresh(const KParams& kp, double* sc, double* sl, Chain& ch, const Draw<RNG>& dr,
+                                     double h, double ws, uint32_t tag)
+{
+    const double f = 1.0 / h - 1.0;
+    int L0 = (int)(h * 12);
+    if (L0 > CAP) L0 = CAP;
+    const uint64_t ctr = ch.ncalls++;
+    for (int tries = 0; tries < 40; ++tries) {
+        const double u = dr.one(ch, ctr, tag, (uint32_t)(tries >> 1), tries & 1);
+        const double cl = pow(kp.alpha + kp.delta * u, kp.expo) / ws;
+        int last = -1;
+        double best = 0.0;
+        for (int k = 0; k < L0; ++k) {
+            const double sck = 300.0 * (k + 1);
+            const double nsc = cl + sck;
+            const double nsl = f * nsc;
+            const double tot = nsc + nsl;
+            if (nsl - f * sck > 0.0 && tot < 5400.0) {
+                const double d = fabs(tot - 3600.0);
+                if (last < 0 || d < best) {
+                    best = d;
+                    last = k;
+                }
+            }
+        }
+        if (last >= 0) {
+            if (last + 2 > CAP) return TMH_CHAIN_SIGMA_OVERFLOW;
+            const double sc_last = 300.0 * (last + 1);
+            const double clr = f * (cl + sc_last) - f * sc_last;   // f * (cl + sc[last]) - sl[last]
+            for (int k = last; k >= 0; --k) {
+                const double nsc = cl + 300.0 * (k + 1);
+                sc[k + 1] = nsc;
+                sl[k + 1] = f * nsc;
+            }
+            sc[0] = cl;
+            sl[0] = clr;
+            ch.L = last + 2;
+            ch.cl = cl;
+            ch.clr = clr;
+            ch.t1 = ceil_thr(cl);
+            ch.t2 = ceil_thr(cl + clr);
+            ch.sec = 0;
+            return 0;
+        }
+    }
+    reset_sigma(sc, sl, ch, h);   // the state an AssertionError leaves (:91)
+    return TMH_CHAIN_ASSERT_BINARY;
+}
+
 // Small by-value parameter block for the out-of-line / time-parallel paths
 // (avoids taking the address of the large kernel-argument struct).
 struct DrawParams {
