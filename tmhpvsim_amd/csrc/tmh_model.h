@@ -1094,10 +1094,11 @@ __device__ __forceinline__ void second_body(const KParams& kp, const R* row, uin
 {
     const R cloudcover = rinterp(fs, S_CC, row[G_HOURF]);   // == interp() bit for bit when R = double
     const R eps = z * (R(kp.sqrt6) * (R(0.001) + R(0.0015 * 8) * cloudcover)) + R(0);
-    if (covered)
-        csi = rinterp(fs, S_CLEAR_DAY, row[G_DAYF]) * (rinterp(fs, S_CLEAR_NOISE, row[G_MINF]) + eps);
-    else
-        csi = rinterp(fs, S_CLOUDY_HOUR, row[G_HOURF]) * (rinterp(fs, S_CLOUDY_NOISE, row[G_MINF]) + eps);
+    // both branches' factors, then a select on values (a select on the sampler
+    // index would make the compiler index the sampler arrays dynamically: scratch)
+    const R a_clear = rinterp(fs, S_CLEAR_DAY, row[G_DAYF]), a_cloudy = rinterp(fs, S_CLOUDY_HOUR, row[G_HOURF]);
+    const R n_clear = rinterp(fs, S_CLEAR_NOISE, row[G_MINF]), n_cloudy = rinterp(fs, S_CLOUDY_NOISE, row[G_MINF]);
+    csi = (covered ? a_clear : a_cloudy) * ((covered ? n_clear : n_cloudy) + eps);
 #ifdef TMH_DIAG_NO_PV
     pv = csi * row[G_GHICS];
 #else
