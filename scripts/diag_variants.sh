@@ -21,7 +21,7 @@ for v in $VARIANTS; do
   name=${v%%:*}
   echo "== $name"
   ( cd /tmp && TMHPVSIM_LIB=$ROOT/tmhpvsim_amd/libtmh_$name.so timeout -k 10 300 rocprofv3 --kernel-trace --stats \
-      --output-format csv -d "$OUT/$name" -o run -- python "$ROOT/bench.py" --steps ${STEPS:-3} --warmup 1 --pipeline ${PIPELINE:-1} --no-cpu-baseline \
+      --output-format csv -d "$OUT/$name" -o run -- python "$ROOT/bench.py" --steps ${STEPS:-3} --warmup 1 --pipeline ${PIPELINE:-1} --no-cpu-baseline ${BENCH_ARGS:-} \
       > "$OUT/$name.json" 2> "$OUT/$name.err" ) || exit $?
   cat "$OUT/$name.json"
 done

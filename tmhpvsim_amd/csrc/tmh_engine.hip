@@ -1096,7 +1096,10 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
 #define TMH_EXP_WAVES 6
 #endif
 template <typename R, int OUT, bool SITES>
-__global__ __launch_bounds__(256, (SITES || sizeof(R) == 8) ? 1 : TMH_EXP_WAVES) void expand_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0,
+#ifndef TMH_SITES_WAVES   // min waves per SIMD of the per-chain-site expansion: 2 (a few spills) is 35 % faster than 1
+#define TMH_SITES_WAVES 2
+#endif
+__global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 : TMH_EXP_WAVES)) void expand_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0,
                                                      uint32_t n, int64_t W0, uint32_t nsteps, int64_t utc0,
                                                      const double* __restrict__ tab64,
                                                      const float* __restrict__ tab32,

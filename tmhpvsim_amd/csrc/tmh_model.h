@@ -751,7 +751,8 @@ __device__ double linke_at(const double* lts, int doy, int leap)
 // restatement).  The sun's place depends on the instant only: one plan row per
 // step (sun_at).  The site part runs once per site and step in geom_kernel, or
 // per chain-second when every chain has its own site (tmh_set_sites, C5).
-enum { SUN_SIND = 0, SUN_COSD, SUN_TAND, SUN_EOT, SUN_MIN, SUN_DNIX, SUN_I0, SUN_TL, SUN_DOY, SUN_LEAP, SUN_W = 12 };
+enum { SUN_SIND = 0, SUN_COSD, SUN_TAND, SUN_EOT, SUN_MIN, SUN_DNIX, SUN_I0, SUN_TL, SUN_DOY, SUN_LEAP, SUN_RDNIX,
+       SUN_W = 12 };
 
 __device__ void sun_at(int64_t utc, int doy, int leap, const double* linke, double* o)
 {
@@ -785,6 +786,7 @@ __device__ void sun_at(int64_t utc, int doy, int leap, const double* linke, doub
     o[SUN_TL] = linke ? linke_at(linke, doy, leap) : 0.0;
     o[SUN_DOY] = doy;
     o[SUN_LEAP] = leap;
+    o[SUN_RDNIX] = 1.0 / o[SUN_DNIX];       // the fp32 row's reciprocal, once per step
 }
 
 // per-site constants of the geometry (site row: lat, lon, altitude, tilt, azimuth, albedo)
@@ -821,10 +823,13 @@ __device__ __forceinline__ SiteK site_k(const double* site)
 template <bool FULL>
 __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, double tl, const double* m, double* g)
 {
-    double tst = fmod(sun[SUN_MIN] + sun[SUN_EOT] + 4.0 * k.lon, 1440.0);
+    // fmod(x, 1440) for x in (-1440, 2880): one exact subtraction (Sterbenz) or none
+    double tst = sun[SUN_MIN] + sun[SUN_EOT] + 4.0 * k.lon;
+    if (tst >= 1440.0) tst -= 1440.0;
     if (tst < 0) tst += 1440.0;
     const double ha = rad(tst / 4.0 - 180.0);
-    const double cha = cos(ha);
+    double sha, cha;
+    sincos(ha, &sha, &cha);
     double czr = k.slat * sun[SUN_SIND] + k.clat * sun[SUN_COSD] * cha;
     czr = czr > 1.0 ? 1.0 : (czr < -1.0 ? -1.0 : czr);
     const double zen = deg(acos(czr));
@@ -832,10 +837,11 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     double de = 0.0;
     if (e0 >= -1.0 * (0.26667 + 0.5667)) de = k.refr / (60.0 * tan(rad(e0 + 10.3 / (e0 + 5.11))));
     const double azen = 90.0 - (e0 + de);
-    const double czs = cosd(azen);
+    double szs, czs;
+    sincos(rad(azen), &szs, &czs);
     if (!FULL && !(czs > 0.0)) return true;   // ghi_cs = cg1 * .. * max(cos(apparent zenith), 0) = 0
-    const double az = deg(atan2(sin(ha), cha * k.slat - sun[SUN_TAND] * k.clat)) + 180.0;
-    const double ct = cos(rad(zen));
+    const double az = deg(atan2(sha, cha * k.slat - sun[SUN_TAND] * k.clat)) + 180.0;
+    const double ct = czr;   // cos(rad(deg(acos(czr)))): the same to ~3e-16 absolute
     g[G_COSZ] = ct;
     g[G_CSIMAX] = 27.21 * exp(-114 * ct) + 1.665 * exp(-4.494 * ct) + 1.08;   // pvmodel.py:52-58
     const double dni_extra = sun[SUN_DNIX];
@@ -852,9 +858,10 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     amd = amd * 101325.0 / 101325.0;
     amd = amd < 12.0 ? amd : (isnan(amd) ? amd : 12.0);
     g[G_AM] = amd;
-    g[G_KNC] = 0.866 - 0.122 * amd + 0.0121 * (amd * amd) - 0.000653 * pow(amd, 3.0) + 0.000014 * pow(amd, 4.0);
+    const double amd2 = amd * amd;
+    g[G_KNC] = 0.866 - 0.122 * amd + 0.0121 * amd2 - 0.000653 * (amd2 * amd) + 0.000014 * (amd2 * amd2);
     g[G_DISCOK] = zen > 87.0 ? 0.0 : 1.0;
-    double proj = k.ctilt * czs + k.stilt * sind(azen) * cosd(az - k.saz);    // haydavies / aoi (pvmodel.py:66-72)
+    double proj = k.ctilt * czs + k.stilt * szs * cosd(az - k.saz);          // haydavies / aoi (pvmodel.py:66-72)
     proj = proj > 1.0 ? 1.0 : (proj < -1.0 ? -1.0 : proj);
     const double cos_tt = proj > 0.0 ? proj : 0.0;
     g[G_RB] = cos_tt / (czs > 0.01745 ? czs : 0.01745);
@@ -862,7 +869,7 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     g[G_TERM2] = k.term2;
     g[G_GFAC] = k.gfac;
     const double aoi = deg(acos(proj));
-    g[G_COSAOI] = cos(rad(aoi));
+    g[G_COSAOI] = proj;   // cos(rad(aoi)): the same to ~3e-16 absolute
     double f1 = (((m[4] * am_abs + m[3]) * am_abs + m[2]) * am_abs + m[1]) * am_abs + m[0];   // sapm spectral
     f1 = isnan(f1) ? 0.0 : f1;
     g[G_F1] = f1 > 0.0 ? f1 : 0.0;
@@ -876,13 +883,13 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
 // the kernels' row of one chain's own site (fp32 rows carry the reciprocals
 // of I0h and dni_extra, like geom_kernel's fp32 table)
 template <typename R>
-__device__ __forceinline__ void site_row(const double* g, R* row)
+__device__ __forceinline__ void site_row(const double* g, const double* sun, R* row)
 {
 #pragma unroll
     for (int i = G_COSZ; i <= G_F2; ++i) row[i] = (R)g[i];
     if constexpr (sizeof(R) == 4) {
         row[G_I0H] = (float)(1.0 / g[G_I0H]);
-        row[G_DNIEXTRA] = (float)(1.0 / g[G_DNIEXTRA]);
+        row[G_DNIEXTRA] = (float)sun[SUN_RDNIX];
     }
 }
 
@@ -909,7 +916,7 @@ __device__ __forceinline__ bool lane_row(LaneSite& ls, const double* sun, const 
     }
     double g[ROW];
     if (site_geom<false>(ls.k, sun, tl, module, g)) return true;
-    site_row<R>(g, row);
+    site_row<R>(g, sun, row);
     return g[G_GHICS] == 0.0;
 }
 
