@@ -5,20 +5,22 @@
 //
 //  * sequential (chain_kernel): one work-item per chain runs the seconds of a
 //    window in order, exactly like ClearskyindexModel.next.  Used for injected
-//    uniform streams (the reference's consumption order is data dependent) and
-//    for the markov cloud-cover mode.
+//    uniform streams (the reference's consumption order is data dependent).
 //
-//  * time-parallel (keyed Philox, faithful mode): the only data-dependent
-//    sequential process is CloudCoverBinary's cloud/clear segment sequence.
-//      P1 segments_kernel: one wavefront per chain walks from segment end to
-//         segment end (next_cloud with the sigma scan spread over 64 lanes and
-//         a butterfly argmin) and records each segment as (first clear step,
-//         next call step).
-//      P2 expand_kernel: one work-item per (chain, block of 256 seconds)
+//  * time-parallel (keyed Philox, both cloud-cover modes): the only sequential
+//    processes are CloudCoverBinary's cloud/clear segment sequence and, in
+//    markov mode, the hour-to-hour cloud cover.
+//      draws: event_draws_kernel (day/hour boundary draws), markov_cc_kernel
+//         (markov mode), candidates_kernel (the next calls' try-0 lengths).
+//      P1 segments_kernel: four chains per wavefront, one per 16-lane row, walk
+//         from segment end to segment end (next_cloud with the sigma scan spread
+//         over the row, DPP argmin and shift) and record each segment as
+//         (first clear step, next call step).
+//      P2 expand_kernel: one work-item per (chain, block of 128 seconds)
 //         rebuilds the sampler state at the block start from the keyed draws
 //         of the last boundary events (block descriptors), then runs the fused
-//         per-second body.  Every draw is keyed by (chain, step), so P2's
-//         outputs are bit-identical to the sequential kernel's.
+//         per-second body.  Every draw is keyed by (chain, step or call number),
+//         so P2's outputs are bit-identical to the sequential kernel's.
 //
 // Per-window, chain-independent work (wall-clock fractions, boundary flags,
 // solar geometry, clear-sky irradiance, SAPM spectral/AOI factors, the boundary
@@ -1083,7 +1085,7 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
 }
 
 // ------------------------------------------------------------ P2: expand
-// One work-item per (chain, block of 256 seconds).  The boundary draws come
+// One work-item per (chain, block of 128 seconds).  The boundary draws come
 // from the draw tables, so the per-second loop holds only the R copies of the
 // sampler pairs and does no fp64 work in fp32 mode.
 #ifndef TMH_ROW_PREFETCH
