@@ -120,8 +120,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # TMH_BENCH_SHARE_GPU=1 (rehearsal only): every rank on device 0 over gloo, so
+        # the N > 1 path runs on a one-GPU box; the scaling runs use one GPU per rank, RCCL
+        if os.environ.get("TMH_BENCH_SHARE_GPU") == "1":
+            torch.cuda.set_device(0)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
