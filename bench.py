@@ -39,8 +39,9 @@ TRACE_BYTES = 12               # meter + pv + residual, fp32
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="c2", choices=["c2", "c4", "c5"],
-                    help="c2: the headline (BASELINE.json configs[1]); c4: 16,384 chains x the year 2019 "
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
+                    help="c2: the headline (BASELINE.json configs[1]); c3: 1,048,576 chains x 1 day, stats, one "
+                         "batch in flight (126 GB of scratch); c4: 16,384 chains x the year 2019 "
                          "(Europe/Berlin wall clock, stats, day windows); c5: the lat/lon sweep (65,536 sites x 1 "
                          "week, markov cc with per-site tables, per-site PV geometry, stats mode, day windows)")
     ap.add_argument("--gpus", type=int, default=1)
@@ -62,13 +63,14 @@ def parse():
                     help="issue each batch as one tmh_step (batches then run in lockstep across streams)")
     ap.add_argument("--walk-priority", default="high", choices=["high", "normal"],
                     help="HIP stream priority of the construction + segment walk (pipelined batches)")
-    ap.add_argument("--pipeline", type=int, default=3,
+    ap.add_argument("--pipeline", type=int, default=None,
                     help="batches in flight on separate HIP streams (1 = no overlap): the segment walks of the "
                          "next batches (latency-bound, one wave per SIMD) run beside this batch's expansion")
     a = ap.parse_args()
     c5, c4 = a.workload == "c5", a.workload == "c4"
-    a.chains = a.chains or {"c2": 4096, "c4": 16384, "c5": 65536}[a.workload]
-    a.seconds = a.seconds or {"c2": 86400, "c4": 365 * 86400, "c5": 604800}[a.workload]
+    a.chains = a.chains or {"c2": 4096, "c3": 1048576, "c4": 16384, "c5": 65536}[a.workload]
+    a.seconds = a.seconds or {"c2": 86400, "c3": 86400, "c4": 365 * 86400, "c5": 604800}[a.workload]
+    a.pipeline = a.pipeline or (1 if a.workload == "c3" else 3)
     a.mode = a.mode or ("trace" if a.workload == "c2" else "stats")
     a.cc = a.cc or ("markov" if c5 else "faithful")
     a.window = min(a.window or (86400 if (c5 or c4) else a.seconds), a.seconds)
