@@ -108,3 +108,33 @@ def test_shapes_csv_round_trip(tmp_path):
     t2, i2 = load_site_tables(tmp_path / "t.npz")
     np.testing.assert_array_equal(np.nan_to_num(t2, nan=-1), np.nan_to_num(tab, nan=-1))
     np.testing.assert_array_equal(i2, is_t)
+
+
+def test_infer_shapes_recovers_a_known_table():
+    """The offline fitting replacement (params.infer_shapes): steps drawn from a known
+    table (the default one) per bin, states spread over each bin, are fitted back."""
+    import scipy.stats
+    from tmhpvsim_amd.params import EDGES, infer_shapes
+    rng = np.random.default_rng(7)
+    base = np.array(SHAPES)
+    lefts = np.concatenate([[0.0], EDGES[:-1]])
+    cc = []
+    for i in range(6):   # series of (state, state + step) pairs, one bin at a time
+        m = 20000
+        st = rng.uniform(lefts[i] + 1e-9, EDGES[i], m)
+        if SHAPE_IS_T[i]:
+            stp = scipy.stats.t.rvs(base[i, 3], loc=base[i, 0], scale=base[i, 1], size=m, random_state=rng)
+        else:
+            stp = scipy.stats.laplace_asymmetric.rvs(base[i, 2], loc=base[i, 0], scale=base[i, 1], size=m,
+                                                     random_state=rng)
+        pair = np.stack([st, st + stp], axis=1)
+        cc.append(np.concatenate([pair, np.full((m, 1), np.nan)], axis=1).ravel())   # NaN breaks the pairs
+    sh, it = infer_shapes(np.concatenate(cc))
+    np.testing.assert_array_equal(it, SHAPE_IS_T)
+    for i in range(6):
+        np.testing.assert_allclose(sh[i, 1], base[i, 1], rtol=0.05)                 # scale
+        assert abs(sh[i, 0] - base[i, 0]) < 0.05 * base[i, 1]                       # loc, in scales
+        if SHAPE_IS_T[i]:
+            np.testing.assert_allclose(sh[i, 3], base[i, 3], rtol=0.3)              # df
+        else:
+            np.testing.assert_allclose(sh[i, 2], base[i, 2], rtol=0.05)             # kappa

@@ -227,3 +227,38 @@ def site_grid(n_lat=256, n_lon=256, lat=(35.0, 60.0), lon=(-10.0, 30.0), base: S
     g[..., 6] = b.temp_air
     g[..., 7] = b.wind_speed
     return g.reshape(-1, 8)
+
+
+def infer_shapes(cc, edges=EDGES, dists=("al", "al", "t", "al", "al", "al"), lag=1):
+    """Fit a 6-bin shape table to an hourly total-cloud-cover series: the
+    replacement for the reference's offline fitting (cloud_cover_hourly.py:110-190,
+    pymc3 posterior means on ERA-5 data; pymc3 and the data are not available).
+    Steps cc[t + lag] - cc[t] are grouped by the bin of cc[t] exactly as
+    get_cloud_cover selects a bin (np.searchsorted(edges, state), :309-314) and
+    fitted by maximum likelihood: the asymmetric Laplace of :93-104 is scipy's
+    laplace_asymmetric (same density in kappa), Student-t is scipy's t.
+    Returns (shapes [6, 4] (loc, scale, kappa, df), is_t [6]) for
+    save_shapes_csv / ModelParams / site tables."""
+    import scipy.stats
+
+    cc = np.asarray(cc, dtype=np.float64)
+    state, step = cc[:-lag], cc[lag:] - cc[:-lag]
+    ok = np.isfinite(state) & np.isfinite(step)
+    state, step = state[ok], step[ok]
+    b = np.searchsorted(np.asarray(edges, dtype=np.float64), state, side="left")
+    shapes = np.full((len(edges), 4), np.nan)
+    is_t = np.zeros(len(edges), dtype=np.int32)
+    for i, dist in enumerate(dists):
+        x = step[b == i]
+        if len(x) < 10:
+            raise ValueError(f"bin {i} has {len(x)} steps: too few to fit")
+        if dist == "al":
+            kappa, loc, scale = scipy.stats.laplace_asymmetric.fit(x)
+            shapes[i, :3] = loc, scale, kappa
+        elif dist == "t":
+            df, loc, scale = scipy.stats.t.fit(x)
+            shapes[i, 0], shapes[i, 1], shapes[i, 3] = loc, scale, df
+            is_t[i] = 1
+        else:
+            raise NotImplementedError(f"distribution {dist!r} is not implemented")
+    return shapes, is_t
