@@ -68,6 +68,13 @@ def test_null_arguments_rejected():
     assert L.tmh_engine_path(None) == -1
     assert L.tmh_probe(0, 0.0, None, None, 1, None) == -1
     assert L.tmh_state_offsets(4, None) == -1
+    assert L.tmh_set_shape_tables(None, None, None, 0) == -1
+    assert L.tmh_set_sites(None, None, None, 0) == -1
+    assert L.tmh_walk(None, None, 0, 1, 0, 1, None, None, 0, None) == -1
+    assert L.tmh_expand(None, None, 0, 1, 0, 1, None, None, None, None, None, 0, None) == -1
+    assert L.tmh_walk_part(None, None, 0, 1, 0, 1, None, None, 0, None, 0, 3, None) == -1
+    assert L.tmh_walk_part(None, None, 0, 1, 0, 1, None, None, 0, None, 0, 8, None) == -1
+    assert b"parts" in L.tmh_last_error()
 
 
 def test_params_struct_matches_header():
