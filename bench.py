@@ -34,7 +34,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-TRACE_BYTES = 12               # meter + pv + residual, fp32
+TRACE_BYTES = 12               # meter + pv + residual, fp32 (24 in fp64)
 
 
 def parse():
@@ -355,7 +355,8 @@ def main():
         elapsed, kmean = float(t[0]), float(t[1])
     chain_seconds = world * n * secs * args.steps
     value = chain_seconds / elapsed
-    achieved = TRACE_BYTES * n * secs / (kmean / 1e3) / 1e9
+    TB = TRACE_BYTES * (2 if args.precision == "fp64" else 1)
+    achieved = TB * n * secs / (kmean / 1e3) / 1e9
     line = {
         "metric": "simulated chain-seconds/sec (node) at 1/2/4/8 GPUs + % HBM roofline",
         "value": value, "unit": "chain-seconds/s", "n_gpus": world, "steps": args.steps,
@@ -371,17 +372,17 @@ def main():
         "roofline": ({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": achieved / HBM_PEAK_GBS, "traffic": traffic(args, n, secs),
                       "kernel": "expand_kernel (P2, " + sim.path + ")", "kernel_ms": kmean,
-                      "bytes_per_launch": TRACE_BYTES * n * secs,
+                      "bytes_per_launch": TB * n * secs,
                       # the same launch with no other batch in flight (one extra batch after the timed region)
-                      "alone": {"kernel_ms": alone_ms, "achieved": TRACE_BYTES * n * secs / (alone_ms / 1e3) / 1e9,
-                                "frac": TRACE_BYTES * n * secs / (alone_ms / 1e3) / 1e9 / HBM_PEAK_GBS}}
+                      "alone": {"kernel_ms": alone_ms, "achieved": TB * n * secs / (alone_ms / 1e3) / 1e9,
+                                "frac": TB * n * secs / (alone_ms / 1e3) / 1e9 / HBM_PEAK_GBS}}
                      if args.mode == "trace" else
                      {"bound": "valu", "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
                       "kernel": "expand_kernel (P2, " + sim.path + ")", "kernel_ms": kmean,
                       "note": "stats mode stores no trace; VALU counters under profiles/"}),
         "phases_ms": phases,
         # whole-pipeline rate: trace bytes of all batches / wall time (kernels overlap across batches)
-        "effective_trace_gbs": (TRACE_BYTES * n * secs / (elapsed / args.steps) / 1e9) if args.mode == "trace" else None,
+        "effective_trace_gbs": (TB * n * secs / (elapsed / args.steps) / 1e9) if args.mode == "trace" else None,
         "faulted_chains": bad,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
