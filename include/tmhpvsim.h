@@ -254,7 +254,8 @@ int tmh_profile_enable(struct tmh_engine* eng, int on);
 int tmh_profile_read(struct tmh_engine* eng, int kernel, double* total_ms, int* launches);
 
 /* Device math probes for parity tests: out[i] = f(a, x[i]) with
- * f = 0 ndtri, 1 gammaincinv, 2 stdtrit, 3 al_ppf, 4 ndtri (fp32 path). */
+ * f = 0 ndtri, 1 gammaincinv, 2 stdtrit, 3 al_ppf, 4 ndtri (fp32 path),
+ * 8 ndtri of the fp64 per-second noise (unpolished). */
 int tmh_probe(int fn, double a, const double* x, double* out, uint32_t n, void* stream);
 
 #ifdef __cplusplus

@@ -63,6 +63,9 @@ def test_probe_math():
         np.testing.assert_allclose(probe(3, SHAPES[b][2], u), O.al_ppf(u, SHAPES[b][2]), rtol=1e-14)
     z32 = probe(4, 0, u)
     np.testing.assert_allclose(z32, O.ndtri(u), rtol=2e-6, atol=1e-6)
+    w = np.random.default_rng(1).integers(0, 2 ** 32, 20000, dtype=np.uint64)
+    u32 = (w.astype(np.float64) + 0.5) * 2.0 ** -32            # the fp64 per-second noise's uniforms
+    np.testing.assert_allclose(probe(8, 0, u32), O.ndtri(u32), rtol=2e-15)
 
 
 # ------------------------------------------------------------------ reference fixtures

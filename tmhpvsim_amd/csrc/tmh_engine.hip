@@ -1333,6 +1333,7 @@ __global__ void probe_kernel(int fn, double a, const double* x, double* out, uin
         case 2: v = stdtrit(a, x[i]); break;
         case 3: v = al_ppf(x[i], a); break;
         case 4: v = (double)ndtri_f(x[i]); break;
+        case 8: v = normcdfinv(x[i]); break;   // the fp64 per-second noise quantile
         case 5: {   // wavefront argmin (first index on ties) of x[wave lanes]; needs full waves
             double dm;
             int km;
