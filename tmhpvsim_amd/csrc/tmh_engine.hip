@@ -72,6 +72,8 @@ struct SegView {                   // P1 -> P2 scratch
     uint32_t evcap;
     double* cand;                  // [kcap][n] try-0 cloud lengths (before / ws) of the window's next kcap calls
     uint32_t kcap;
+    void* mtab;                    // [nmin][2][n] R: the _next_min draws (cloudy, clear noise) of every minute boundary
+    uint32_t nmin;
 };
 
 // The window-start values a walk takes from the PREVIOUS window's walk instead of
@@ -451,6 +453,47 @@ __device__ __forceinline__ void minute_draws(const DrawParams& dp, uint64_t chai
     clear = minute_noise<R>(u52(u.z, u.w), 0.001, 0.0015, cc, dp.sqrt09);
 }
 
+// The _next_min draws of every (candidate minute boundary, chain) of the window,
+// one work-item each, before the expansion: minute m sits at window step
+// fm + 60 m; its cloud-cover pair is the one in force there (the last two hourly
+// draws at or before it, or the window-start pair).  The expansion and the
+// block-start reconstruction read them instead of drawing in their loops.
+template <typename R>
+__global__ __launch_bounds__(256) void minute_table_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
+                                                           int64_t W0, uint32_t nsteps, int64_t fm,
+                                                           const double* __restrict__ tab64,
+                                                           const int2* __restrict__ events,
+                                                           const uint32_t* __restrict__ n_events, SegView sg)
+{
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t m = blockIdx.y;
+    const int64_t jm = fm + 60 * (int64_t)m;
+    if (c >= n || jm >= (int64_t)nsteps) return;
+    const int64_t step = W0 + jm;
+    const int ne = (int)min(*n_events, ev_cap_dev(nsteps));
+    int lo = 0, hi = ne;   // h0 = number of boundary events at or before the step, minus one
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((int64_t)events[mid].x <= step) lo = mid + 1;
+        else hi = mid;
+    }
+    const int h0 = lo - 1, h1 = lo - 2;
+    const double* evd = sg.evd;
+    double pb, pa;
+    if (h0 < 0) {
+        pb = st.sb[S_CC][c];
+        pa = st.sa[S_CC][c];
+    } else {
+        pa = evd[(size_t)h0 * 4 * n + c];
+        pb = h1 < 0 ? st.sa[S_CC][c] : evd[(size_t)h1 * 4 * n + c];
+    }
+    double cloudy, clear;
+    minute_draws<R>(dp, chain0 + c, step, interp(pb, pa, tab64[(size_t)jm * ROW + G_HOURF]), cloudy, clear);
+    R* t = reinterpret_cast<R*>(sg.mtab);
+    t[(size_t)(2 * m) * n + c] = (R)cloudy;
+    t[(size_t)(2 * m + 1) * n + c] = (R)clear;
+}
+
 // cc / clear_day / noise pairs described by `d`, from the draw tables (start = window start)
 // what the minute draws of a block start / window end need
 struct MinuteCtx {
@@ -478,36 +521,17 @@ __device__ __forceinline__ void samplers_at(const BlockDesc& d, const SegView& s
         s.b[S_CLEAR_DAY] = d.cd1 >= 0 ? cdv(d.cd1) : s.a[S_CLEAR_DAY];
         s.a[S_CLEAR_DAY] = na;
     }
-    if (d.q0 >= 0) {   // the last two minute boundaries: draws recomputed from their keys
-        // cloud-cover pair in force at a minute boundary: hour events sit on minute
-        // boundaries, so at q0 it is the pair of the block start; at q1 it is the
-        // one before h0 when h0 happened at q0
-        const double cc_st_b = st.sb[S_CC][c], cc_st_a = st.sa[S_CC][c];
-        auto hour_val = [&](int32_t h, double fallback) { return h >= 0 ? evd[(size_t)h * 4 * n + c] : fallback; };
-        auto draw_q = [&](int32_t q, bool before_h0, double& cloudy, double& clear) {
-            const int64_t jq = mc.fm + 60 * (int64_t)q;
-            double pb, pa;
-            if (!before_h0 || d.h0 < 0) {       // pair after h0 (or the window-start pair)
-                pa = hour_val(d.h0, cc_st_a);
-                pb = d.h0 < 0 ? cc_st_b : hour_val(d.h1, cc_st_a);
-            } else {                            // pair after h1
-                pa = hour_val(d.h1, cc_st_a);
-                pb = d.h1 < 0 ? cc_st_b : hour_val(d.h2, cc_st_a);
-            }
-            const double cc = interp(pb, pa, mc.tab64[(size_t)jq * ROW + G_HOURF]);
-            minute_draws<R>(mc.dp, mc.chain, mc.W0 + jq, cc, cloudy, clear);
-        };
-        double ca, la;
-        draw_q(d.q0, false, ca, la);
+    if (d.q0 >= 0) {   // the last two minute boundaries: their draws from the minute table
+        const R* t = reinterpret_cast<const R*>(sg.mtab);
         if (d.q1 >= 0) {
-            const bool h0_at_q0 = d.h0 >= 0 && (int64_t)mc.events[d.h0].x == mc.W0 + mc.fm + 60 * (int64_t)d.q0;
-            draw_q(d.q1, h0_at_q0, s.b[S_CLOUDY_NOISE], s.b[S_CLEAR_NOISE]);
+            s.b[S_CLOUDY_NOISE] = (double)t[(size_t)(2 * d.q1) * n + c];
+            s.b[S_CLEAR_NOISE] = (double)t[(size_t)(2 * d.q1 + 1) * n + c];
         } else {
             s.b[S_CLOUDY_NOISE] = s.a[S_CLOUDY_NOISE];
             s.b[S_CLEAR_NOISE] = s.a[S_CLEAR_NOISE];
         }
-        s.a[S_CLOUDY_NOISE] = ca;
-        s.a[S_CLEAR_NOISE] = la;
+        s.a[S_CLOUDY_NOISE] = (double)t[(size_t)(2 * d.q0) * n + c];
+        s.a[S_CLEAR_NOISE] = (double)t[(size_t)(2 * d.q0 + 1) * n + c];
     }
 }
 
@@ -1129,7 +1153,6 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
     const int2* rec = sg.rec + (size_t)(live ? c : 0) * sg.cap;
     uint32_t jr = 0, evi = 0;
     FSamp<R> fs;
-    double ccb = 0.0, cca = 0.0;   // fp64 cloud-cover pair: the scale of the minute draws
     const MinuteCtx mc{dp, chain, W0, fm, events, (int)min(*n_events, ev_cap_dev(nsteps)), tab64};
     LaneSite ls{};   // per-chain sites (C5): this chain's site constants
     if constexpr (SITES) {
@@ -1149,8 +1172,6 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
         const BlockDesc d = desc[b];
         evi = (uint32_t)d.evi;
         if (alive && b > 0) samplers_at<R>(d, sg, n, c, s, mc, st);
-        ccb = s.b[S_CC];
-        cca = s.a[S_CC];
         to_real(fs, s);
     }
     if (alive) {   // segment containing the block start: first record with next-call step > start
@@ -1201,21 +1222,18 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
                     fs.a[S_CLEAR_DAY] = (R)evd[eo + 2 * (size_t)n];
                 }
                 if (fl & FL_HOUR) {
-                    ccb = cca;
-                    cca = evd[eo];
                     fs.b[S_CC] = fs.a[S_CC];
-                    fs.a[S_CC] = (R)cca;
+                    fs.a[S_CC] = (R)evd[eo];
                     fs.b[S_CLEAR_DAY] = fs.a[S_CLEAR_DAY];
                     fs.a[S_CLEAR_DAY] = (R)evd[eo + 3 * (size_t)n];
                 }
             }
-            if (fl & FL_MIN) {                         // _next_min, drawn here from its key
-                double cloudy, clear;
-                minute_draws<R>(dp, chain, step, interp(ccb, cca, tab64[(size_t)j * ROW + G_HOURF]), cloudy, clear);
+            if (fl & FL_MIN) {                         // _next_min: from the minute table
+                const R* mt = reinterpret_cast<const R*>(sg.mtab) + (size_t)(2 * (((int32_t)j - (int32_t)fm) / 60)) * n + c;
                 fs.b[S_CLOUDY_NOISE] = fs.a[S_CLOUDY_NOISE];
-                fs.a[S_CLOUDY_NOISE] = (R)cloudy;
+                fs.a[S_CLOUDY_NOISE] = mt[0];
                 fs.b[S_CLEAR_NOISE] = fs.a[S_CLEAR_NOISE];
-                fs.a[S_CLEAR_NOISE] = (R)clear;
+                fs.a[S_CLEAR_NOISE] = mt[n];
             }
             const int32_t stepi = (int32_t)step;   // steps < 2^31 (tmh_step checks the window)
             if (stepi >= seg.y) {   // next_cloud happened at seg.y
@@ -1484,6 +1502,12 @@ size_t scratch_layout(uint32_t n, uint32_t n_steps, void* base, SegView* v)
         v->cand = (double*)(b + o);
     }
     o += align_up((size_t)n * kc * 8);
+    const uint32_t nmin = n_steps / 60 + 2;
+    if (v) {
+        v->nmin = nmin;
+        v->mtab = (void*)(b + o);
+    }
+    o += align_up((size_t)n * nmin * 2 * 8);
     return o;
 }
 
@@ -1872,6 +1896,18 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     }
     if (!(phases & PH_EXPAND)) return TMH_OK;
     hipEvent_t t_exp = eng->mark(s);
+    {   // the window's minute draws, one work-item each (read by the expansion and the commit)
+        const int64_t fmh = first_minute_host(utc0, step0);
+        const uint32_t nm = fmh < (int64_t)n_steps ? (uint32_t)((n_steps - 1 - fmh) / 60 + 1) : 0;
+        if (nm) {
+            if (f64)
+                hipLaunchKernelGGL(minute_table_kernel<double>, dim3(cb, nm), dim3(256), 0, s, eng->dp, v, chain0,
+                                   n_chains, step0, n_steps, fmh, pv.tab64, pv.events, pv.n_events, sg);
+            else
+                hipLaunchKernelGGL(minute_table_kernel<float>, dim3(cb, nm), dim3(256), 0, s, eng->dp, v, chain0,
+                                   n_chains, step0, n_steps, fmh, pv.tab64, pv.events, pv.n_events, sg);
+        }
+    }
     dim3 grid2(nblk_of(n_steps), cb);
     const bool no_stats = !sv.hist && !sv.acc;
     const int out = (no_stats && tv.pv && tv.meter && tv.residual && !tv.csi && !tv.covered) ? OUT_TRACE3
