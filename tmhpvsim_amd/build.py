@@ -8,7 +8,8 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = [os.path.join(HERE, "csrc", "tmh_engine.hip")]
-DEPS = SRC + [os.path.join(HERE, "csrc", "tmh_math.h"), os.path.join(ROOT, "include", "tmhpvsim.h")]
+DEPS = SRC + [os.path.join(HERE, "csrc", "tmh_math.h"), os.path.join(HERE, "csrc", "tmh_model.h"),
+        os.path.join(ROOT, "include", "tmhpvsim.h")]
 LIB = os.path.join(HERE, "libtmhpvsim.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 

@@ -1109,6 +1109,24 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
 }
 
 // ------------------------------------------------------------ P2: expand
+// one trace row's store: a buffer resource on the wave-uniform row base (SGPRs)
+// plus the lane's 32-bit byte offset, non-temporal (the trace is written once);
+// no per-lane 64-bit address arithmetic.  0x00020000: gfx9 raw-buffer dword 3.
+template <typename R>
+__device__ __forceinline__ void row_store(void* base, size_t row_off, uint32_t lane_off, R v)
+{
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(base) + row_off, 0, -1, 0x00020000);
+    if constexpr (sizeof(R) == 8)
+    {
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        const uint64_t u = (uint64_t)__double_as_longlong(v);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)u, (uint32_t)(u >> 32)}, rs, (int)lane_off, 0, 2 /* nt */);
+    }
+    else
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (int)lane_off, 0, 2 /* nt */);
+}
+
 // One work-item per (chain, block of 128 seconds).  The boundary draws come
 // from the draw tables, so the per-second loop holds only the R copies of the
 // sampler pairs and does no fp64 work in fp32 mode.
@@ -1268,11 +1286,12 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
             emit<R, OUT>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok);
 #else
         if constexpr (OUT == OUT_TRACE3) {   // row pointers are wave-uniform: 32-bit lane offsets only
-            if (live) {
-                const size_t ro = (size_t)j * tr.ld;
-                __builtin_nontemporal_store(pv, reinterpret_cast<R*>(tr.pv) + ro + c);
-                __builtin_nontemporal_store(meter, reinterpret_cast<R*>(tr.meter) + ro + c);
-                __builtin_nontemporal_store(res, reinterpret_cast<R*>(tr.residual) + ro + c);
+            if (live) {                        // (SGPR row base + zero-extended lane byte offset: no 64-bit VALU adds)
+                const size_t ro = (size_t)j * tr.ld * sizeof(R);
+                const uint32_t lo = c * (uint32_t)sizeof(R);
+                row_store(tr.pv, ro, lo, pv);
+                row_store(tr.meter, ro, lo, meter);
+                row_store(tr.residual, ro, lo, res);
             }
         } else if (live) {
             emit<R, OUT>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok);

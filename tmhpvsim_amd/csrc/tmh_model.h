@@ -1011,15 +1011,17 @@ __device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float 
     const float kt = fminf(fmaxf(ghi * g[G_I0H], 0.0f), 1.0f);
     // DISC Kn (pvlib irradiance.disc): coefficient sets split at kt = 0.6
     // (the model's literal coefficients: compile-time constants, no SGPRs)
+    // Both sets are evaluated (one literal FMA per Horner step) and the results
+    // selected: cheaper than selecting twelve coefficient pairs per lane, and bit
+    // for bit the same (the low set's zero leading terms drop out exactly, kt >= 0).
     const bool lo = kt <= 0.6f;
-    const float a3 = lo ? -2.222f : 11.56f, a2 = lo ? 2.286f : -27.49f, a1 = lo ? -1.56f : 21.77f,
-                a0 = lo ? 0.512f : -5.743f;
-    const float b3 = lo ? 0.0f : 31.9f, b2 = lo ? 0.0f : 66.05f, b1 = lo ? 0.962f : -118.5f, b0 = lo ? 0.37f : 41.4f;
-    const float c3 = lo ? 0.0f : 73.81f, c2 = lo ? -2.048f : -222.0f, c1 = lo ? 0.932f : 184.2f,
-                c0 = lo ? -0.28f : -47.01f;
-    const float a = fmaf(fmaf(fmaf(a3, kt, a2), kt, a1), kt, a0);
-    const float b = fmaf(fmaf(fmaf(b3, kt, b2), kt, b1), kt, b0);
-    const float cc = fmaf(fmaf(fmaf(c3, kt, c2), kt, c1), kt, c0);
+    const float a_lo = fmaf(fmaf(fmaf(-2.222f, kt, 2.286f), kt, -1.56f), kt, 0.512f);
+    const float a_hi = fmaf(fmaf(fmaf(11.56f, kt, -27.49f), kt, 21.77f), kt, -5.743f);
+    const float b_lo = fmaf(0.962f, kt, 0.37f);
+    const float b_hi = fmaf(fmaf(fmaf(31.9f, kt, 66.05f), kt, -118.5f), kt, 41.4f);
+    const float c_lo = fmaf(fmaf(-2.048f, kt, 0.932f), kt, -0.28f);
+    const float c_hi = fmaf(fmaf(fmaf(73.81f, kt, -222.0f), kt, 184.2f), kt, -47.01f);
+    const float a = lo ? a_lo : a_hi, b = lo ? b_lo : b_hi, cc = lo ? c_lo : c_hi;
     const float dkn = fmaf(b, __builtin_amdgcn_exp2f(cc * g[G_AM] * 1.44269504088896341f), a);
     float dni = (g[G_KNC] - dkn) * g[G_I0];
     dni = (g[G_DISCOK] != 0.0f && ghi >= 0.0f && dni >= 0.0f) ? dni : 0.0f;
