@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--cpu-sample-chains", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--path", default="auto", choices=["auto", "sequential", "time_parallel"])
+    ap.add_argument("--build-on", default="expand", choices=["expand", "walk"],
+                    help="stream of each batch's construction, plan and draws: in order on the expansion "
+                         "stream, or ahead of its walk on the high-priority walk stream")
     ap.add_argument("--no-stagger", dest="stagger", action="store_false",
                     help="issue each batch as one tmh_step (batches then run in lockstep across streams)")
     ap.add_argument("--walk-priority", default="high", choices=["high", "normal"],
@@ -165,6 +168,7 @@ def main():
             self.wptr = C.c_void_p(self.wstream.cuda_stream)
             self.walked = torch.cuda.Event()
             self.done = torch.cuda.Event()
+            self.expanded = None   # recorded after this context's last expansion
             self.state = torch.zeros(L.tmh_state_bytes(n), dtype=torch.uint8, device=dev)
             self.plan = torch.empty(L.tmh_plan_bytes(win), dtype=torch.uint8, device=dev)
             self.scratch = torch.empty(L.tmh_scratch_bytes(n, win), dtype=torch.uint8, device=dev)
@@ -244,15 +248,21 @@ def main():
                                     C.byref(cx.tr), C.byref(cx.st) if cx.st is not None else None, pl, sc,
                                     cx.scratch.numel(), cx.sptr))
 
-    def build(k):      # construction of batch k's chains, its plan and draws, on the expansion stream
-        cx = ctxs[k % len(ctxs)]      # (in order after the expansion that last used this context;
-        cx.chain0 = (rank + k * world) * n   # beside a running expansion these small grids would starve)
-        _lib.check(L.tmh_init(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, None, eptr))
-        _lib.check(L.tmh_plan(sim._eng, 0, secs, C.c_void_p(cx.plan.data_ptr()), eptr))
+    def build(k):      # construction of batch k's chains, its plan and draws
+        cx = ctxs[k % len(ctxs)]
+        cx.chain0 = (rank + k * world) * n
+        if args.build_on == "walk":   # on the batch's high-priority walk stream, after the expansion
+            bs, bp = cx.wstream, cx.wptr   # that last used this context: beside the running expansion
+            if cx.expanded is not None:
+                bs.wait_event(cx.expanded)
+        else:                          # in order on the expansion stream
+            bs, bp = estream, eptr
+        _lib.check(L.tmh_init(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, None, bp))
+        _lib.check(L.tmh_plan(sim._eng, 0, secs, C.c_void_p(cx.plan.data_ptr()), bp))
         _lib.check(L.tmh_walk_part(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs,
                                    C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
-                                   cx.scratch.numel(), None, 0, _lib.WALK_DRAWS, eptr))
-        cx.done.record(estream)
+                                   cx.scratch.numel(), None, 0, _lib.WALK_DRAWS, bp))
+        cx.done.record(bs)
 
     def start(k):      # the segment walk of batch k, on its context's walk stream
         cx = ctxs[k % len(ctxs)]
@@ -269,6 +279,9 @@ def main():
                                 C.byref(cx.tr), C.byref(cx.st) if cx.st is not None else None,
                                 C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
                                 cx.scratch.numel(), eptr))
+        if cx.expanded is None:
+            cx.expanded = torch.cuda.Event()
+        cx.expanded.record(estream)
 
     def run_batches(k0, cnt):
         """Batches k0 .. k0 + cnt - 1.  One-window batches are software-pipelined:
@@ -368,7 +381,8 @@ def main():
                                 f"with per-site tables, per-site PV geometry, {win} s windows, Europe/Berlin, ")
                                + f"{args.start[:10]}, {args.mode} mode ({'meter+pv+residual fp32 trace' if args.mode == 'trace' else 'on-GPU stats'})",
                    "chains_per_gpu": n, "seconds": secs, "parallelism": f"chains sharded over {world} GPU(s)",
-                   "batches_in_flight": len(ctxs), "staggered": bool(args.stagger and nwin == 1)},
+                   "batches_in_flight": len(ctxs), "staggered": bool(args.stagger and nwin == 1),
+                   "construction_on": args.build_on},
         "roofline": ({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": achieved / HBM_PEAK_GBS, "traffic": traffic(args, n, secs),
                       "kernel": "expand_kernel (P2, " + sim.path + ")", "kernel_ms": kmean,

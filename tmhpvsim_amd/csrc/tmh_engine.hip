@@ -288,10 +288,16 @@ __global__ __launch_bounds__(256) void geom_kernel(GParams gp, int64_t step0, ui
     if (g[G_GHICS] == 0.0) fl |= FL_NIGHT;   // ghi_cs = 0 -> pv = 0 whatever the csi
     g[G_FLAGS] = (double)fl;
     double* o64 = tab64 + (size_t)j * ROW;
-    float* o32 = tab32 + (size_t)j * ROW;
+    float* o32 = tab32 + (size_t)j * ROW32;
     for (int i = 0; i < ROW; ++i) {
         o64[i] = g[i];
         o32[i] = (float)g[i];
+    }
+    const int fr[3] = {G_MINF, G_HOURF, G_DAYF}, fc[3] = {G_MINF_C, G_HOURF_C, G_DAYF_C};
+    for (int i = 0; i < 3; ++i) {   // (1 - f, f) pairs, 1 - f rounded in fp32 as the kernels computed it
+        const float f = (float)g[fr[i]];
+        o32[fc[i]] = 1.0f - f;
+        o32[fc[i] + 1] = f;
     }
     o32[G_FLAGS] = __uint_as_float(fl);
     o32[G_I0H] = (float)(1.0 / g[G_I0H]);   // fp32 path multiplies by reciprocals
@@ -313,7 +319,7 @@ __global__ __launch_bounds__(1024) void events_kernel(const float* __restrict__ 
     uint32_t c = 0;
     for (uint32_t q = lo; q < hi; ++q) {
         const uint64_t j = (uint64_t)(first + 60 * (int64_t)q);
-        if (__float_as_uint(tab32[j * ROW + G_FLAGS]) & (FL_DAY | FL_HOUR)) ++c;
+        if (__float_as_uint(tab32[j * ROW32 + G_FLAGS]) & (FL_DAY | FL_HOUR)) ++c;
     }
     cnt[t] = c;
     __syncthreads();
@@ -326,7 +332,7 @@ __global__ __launch_bounds__(1024) void events_kernel(const float* __restrict__ 
     uint32_t o = cnt[t] - c;
     for (uint32_t q = lo; q < hi; ++q) {
         const uint64_t j = (uint64_t)(first + 60 * (int64_t)q);
-        const uint32_t fl = __float_as_uint(tab32[j * ROW + G_FLAGS]) & (FL_DAY | FL_HOUR);
+        const uint32_t fl = __float_as_uint(tab32[j * ROW32 + G_FLAGS]) & (FL_DAY | FL_HOUR);
         if (fl) {
             if (o < cap) events[o] = make_int2((int)(step0 + (int64_t)j), (int)fl);
             ++o;
@@ -577,12 +583,12 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
     }
     for (uint32_t j = 0; j < nsteps; ++j) {
         const uint64_t step = (uint64_t)(step0 + j);
-        const float* r32 = tab32 + (size_t)j * ROW;
+        const float* r32 = tab32 + (size_t)j * ROW32;
         const double* r64 = tab64 + (size_t)j * ROW;
         const uint32_t fl = __float_as_uint(r32[G_FLAGS]);
-        R row[ROW];
+        R row[row_w<R>()];
 #pragma unroll
-        for (int i = 0; i < ROW; ++i) row[i] = sizeof(R) == 8 ? (R)r64[i] : (R)r32[i];
+        for (int i = 0; i < row_w<R>(); ++i) row[i] = sizeof(R) == 8 ? (R)r64[i] : (R)r32[i];
         R csi = R(NAN), pv = R(NAN), meter = R(NAN), res = R(NAN);
         uint8_t cov = 255;
         bool ok = false;
@@ -637,7 +643,7 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
                         const bool night = lane_row<R>(ls, sun + (size_t)j * SUN_W, kp.module, row);
                         flp = night ? (fl | FL_NIGHT) : (fl & ~(uint32_t)FL_NIGHT);
                     }
-                    second_body<R>(kp, row, flp, fs, covered, z, mtr, csi, pv, meter, res);
+                    second_body<R>(kp, kp.pvf, row, flp, fs, covered, z, mtr, csi, pv, meter, res);
                     ok = true;
                 }
             }
@@ -1211,19 +1217,19 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
     // ahead, so its latency hides behind the previous step's arithmetic
     auto load_row = [&](uint32_t j, R* r) {
 #pragma unroll
-        for (int i = 0; i < ROW; ++i)
-            r[i] = sizeof(R) == 8 ? (R)tab64[(size_t)j * ROW + i] : (R)tab32[(size_t)j * ROW + i];
+        for (int i = 0; i < row_w<R>(); ++i)
+            r[i] = sizeof(R) == 8 ? (R)tab64[(size_t)j * ROW + i] : (R)tab32[(size_t)j * ROW32 + i];
     };
 #if TMH_ROW_PREFETCH
-    R row_nx[ROW];
+    R row_nx[row_w<R>()];
     load_row(j0, row_nx);
 #endif
     for (uint32_t j = j0; j < j1; ++j) {
         const int64_t step = W0 + j;
-        R row[ROW];
+        R row[row_w<R>()];
 #if TMH_ROW_PREFETCH
 #pragma unroll
-        for (int i = 0; i < ROW; ++i) row[i] = row_nx[i];
+        for (int i = 0; i < row_w<R>(); ++i) row[i] = row_nx[i];
         if (j + 1 < j1) load_row(j + 1, row_nx);
 #else
         load_row(j, row);
@@ -1277,7 +1283,7 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
                 const bool night = lane_row<R>(ls, sun + (size_t)j * SUN_W, kp.module, row);
                 flp = night ? (fl | FL_NIGHT) : (fl & ~(uint32_t)FL_NIGHT);
             }
-            second_body<R>(kp, row, flp, fs, covered, noise_z<R>(odd ? pair.z : pair.x), meter_w<R>(odd ? pair.w : pair.y),
+            second_body<R>(kp, kp.pvf, row, flp, fs, covered, noise_z<R>(odd ? pair.z : pair.x), meter_w<R>(odd ? pair.w : pair.y),
                            csi, pv, meter, res);
         }
         if (fl & (FL_DAY | FL_HOUR)) ++evi;
@@ -1472,7 +1478,7 @@ size_t plan_layout(uint32_t n_steps, void* base, PlanView* v)
     if (v) v->tab64 = (double*)(b + o);
     o += align_up((size_t)n_steps * ROW * 8);
     if (v) v->tab32 = (float*)(b + o);
-    o += align_up((size_t)n_steps * ROW * 4);
+    o += align_up((size_t)n_steps * ROW32 * 4);
     if (v) v->events = (int2*)(b + o);
     o += align_up((size_t)ev_cap(n_steps) * 8);
     if (v) v->n_events = (uint32_t*)(b + o);

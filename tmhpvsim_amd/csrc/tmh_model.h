@@ -50,8 +50,15 @@ enum : uint32_t { FL_DAY = 1, FL_HOUR = 2, FL_MIN = 4, FL_NIGHT = 8 };
 enum {
     G_MINF = 0, G_HOURF = 1, G_DAYF = 2, G_FLAGS = 3, G_COSZ = 4, G_CSIMAX = 5, G_GHICS = 6,
     G_I0H = 7, G_I0 = 8, G_KNC = 9, G_AM = 10, G_DISCOK = 11, G_RB = 12, G_DNIEXTRA = 13,
-    G_TERM2 = 14, G_GFAC = 15, G_COSAOI = 16, G_F1 = 17, G_F2 = 18
+    G_TERM2 = 14, G_GFAC = 15, G_COSAOI = 16, G_F1 = 17, G_F2 = 18,
+    // fp32 table only: each clock fraction again beside its complement 1 - f
+    // (computed in fp32 exactly as the kernels did), 8-byte aligned pairs, so an
+    // interpolation f a + (1 - f) b is one packed multiply on an SGPR pair + an add
+    G_MINF_C = 20, G_MINF2 = 21, G_HOURF_C = 22, G_HOURF2 = 23, G_DAYF_C = 24, G_DAYF2 = 25
 };
+#define ROW32 26   // fp32 clock/geometry row width (the fp64 row is ROW = TMH_GEOM_FIELDS)
+template <typename R>
+constexpr int row_w() { return sizeof(R) == 8 ? ROW : ROW32; }
 
 enum { S_CC = 0, S_CLEAR_DAY = 1, S_CLOUDY_HOUR = 2, S_CLOUDY_NOISE = 3, S_CLEAR_NOISE = 4, S_WS = 5 };
 
@@ -1076,6 +1083,17 @@ __device__ __forceinline__ R rinterp(const FSamp<R>& f, int k, R frac)
     return frac * f.a[k] + (R(1) - frac) * f.b[k];
 }
 
+// the same from a row's fraction field fi: the fp32 row holds (1 - f, f) as a pair
+template <typename R>
+__device__ __forceinline__ R rinterp_row(const FSamp<R>& f, int k, const R* row, int fi)
+{
+    if constexpr (sizeof(R) == 8) return rinterp(f, k, row[fi]);
+    else {
+        const int pc = fi == G_MINF ? G_MINF_C : (fi == G_HOURF ? G_HOURF_C : G_DAYF_C);
+        return row[pc + 1] * f.a[k] + row[pc] * f.b[k];
+    }
+}
+
 // clearskyindexmodel.py:146-160 + pvmodel.py:53-80 + metersim.py:51 + pvsim.py:83
 // per-second draws from the step's two Philox words (keyed mode): the noise's
 // standard normal and the meter (metersim.py:51, 9000 u in [0, 9000))
@@ -1102,21 +1120,22 @@ __device__ __forceinline__ R meter_w(uint32_t w)
 }
 
 template <typename R>
-__device__ __forceinline__ void second_body(const KParams& kp, const R* row, uint32_t fl, const FSamp<R>& fs,
-                                            bool covered, R z, R meter_in, R& csi, R& pv, R& meter, R& res)
+__device__ __forceinline__ void second_body(const KParams& kp, const PVF& pk, const R* row, uint32_t fl,
+                                            const FSamp<R>& fs, bool covered, R z, R meter_in, R& csi, R& pv, R& meter,
+                                            R& res)
 {
-    const R cloudcover = rinterp(fs, S_CC, row[G_HOURF]);   // == interp() bit for bit when R = double
+    const R cloudcover = rinterp_row(fs, S_CC, row, G_HOURF);   // == interp() bit for bit when R = double
     const R eps = z * (R(kp.sqrt6) * (R(0.001) + R(0.0015 * 8) * cloudcover)) + R(0);
     // both branches' factors, then a select on values (a select on the sampler
     // index would make the compiler index the sampler arrays dynamically: scratch)
-    const R a_clear = rinterp(fs, S_CLEAR_DAY, row[G_DAYF]), a_cloudy = rinterp(fs, S_CLOUDY_HOUR, row[G_HOURF]);
-    const R n_clear = rinterp(fs, S_CLEAR_NOISE, row[G_MINF]), n_cloudy = rinterp(fs, S_CLOUDY_NOISE, row[G_MINF]);
+    const R a_clear = rinterp_row(fs, S_CLEAR_DAY, row, G_DAYF), a_cloudy = rinterp_row(fs, S_CLOUDY_HOUR, row, G_HOURF);
+    const R n_clear = rinterp_row(fs, S_CLEAR_NOISE, row, G_MINF), n_cloudy = rinterp_row(fs, S_CLOUDY_NOISE, row, G_MINF);
     csi = (covered ? a_clear : a_cloudy) * ((covered ? n_clear : n_cloudy) + eps);
 #ifdef TMH_DIAG_NO_PV
     pv = csi * row[G_GHICS];
 #else
     if constexpr (sizeof(R) == 8) pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power<R>(kp, row, csi) : R(0);
-    else pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power_f(kp.pvf, row, csi) : 0.0f;
+    else pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power_f(pk, row, csi) : 0.0f;
 #endif
     meter = meter_in;
     res = meter - pv;
