@@ -289,19 +289,17 @@ __global__ __launch_bounds__(256) void geom_kernel(GParams gp, int64_t step0, ui
     g[G_FLAGS] = (double)fl;
     double* o64 = tab64 + (size_t)j * ROW;
     float* o32 = tab32 + (size_t)j * ROW32;
-    for (int i = 0; i < ROW; ++i) {
-        o64[i] = g[i];
-        o32[i] = (float)g[i];
-    }
-    const int fr[3] = {G_MINF, G_HOURF, G_DAYF}, fc[3] = {G_MINF_C, G_HOURF_C, G_DAYF_C};
+    for (int i = 0; i < ROW; ++i) o64[i] = g[i];
+    const int fr[3] = {G_MINF, G_HOURF, G_DAYF}, fc[3] = {G32_MINF_C, G32_HOURF_C, G32_DAYF_C};
     for (int i = 0; i < 3; ++i) {   // (1 - f, f) pairs, 1 - f rounded in fp32 as the kernels computed it
         const float f = (float)g[fr[i]];
         o32[fc[i]] = 1.0f - f;
         o32[fc[i] + 1] = f;
     }
-    o32[G_FLAGS] = __uint_as_float(fl);
-    o32[G_I0H] = (float)(1.0 / g[G_I0H]);   // fp32 path multiplies by reciprocals
-    o32[G_DNIEXTRA] = (float)(1.0 / g[G_DNIEXTRA]);
+    for (int i = G_COSZ; i <= G_F2; ++i) o32[i + G32] = (float)g[i];
+    o32[G_FLAGS + G32] = __uint_as_float(fl);
+    o32[G_I0H + G32] = (float)(1.0 / g[G_I0H]);   // fp32 path multiplies by reciprocals
+    o32[G_DNIEXTRA + G32] = (float)(1.0 / g[G_DNIEXTRA]);
 }
 
 // Compact the window's day/hour boundary steps, in order (one workgroup).
@@ -319,7 +317,7 @@ __global__ __launch_bounds__(1024) void events_kernel(const float* __restrict__ 
     uint32_t c = 0;
     for (uint32_t q = lo; q < hi; ++q) {
         const uint64_t j = (uint64_t)(first + 60 * (int64_t)q);
-        if (__float_as_uint(tab32[j * ROW32 + G_FLAGS]) & (FL_DAY | FL_HOUR)) ++c;
+        if (__float_as_uint(tab32[j * ROW32 + G_FLAGS + G32]) & (FL_DAY | FL_HOUR)) ++c;
     }
     cnt[t] = c;
     __syncthreads();
@@ -332,7 +330,7 @@ __global__ __launch_bounds__(1024) void events_kernel(const float* __restrict__ 
     uint32_t o = cnt[t] - c;
     for (uint32_t q = lo; q < hi; ++q) {
         const uint64_t j = (uint64_t)(first + 60 * (int64_t)q);
-        const uint32_t fl = __float_as_uint(tab32[j * ROW32 + G_FLAGS]) & (FL_DAY | FL_HOUR);
+        const uint32_t fl = __float_as_uint(tab32[j * ROW32 + G_FLAGS + G32]) & (FL_DAY | FL_HOUR);
         if (fl) {
             if (o < cap) events[o] = make_int2((int)(step0 + (int64_t)j), (int)fl);
             ++o;
@@ -585,7 +583,7 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
         const uint64_t step = (uint64_t)(step0 + j);
         const float* r32 = tab32 + (size_t)j * ROW32;
         const double* r64 = tab64 + (size_t)j * ROW;
-        const uint32_t fl = __float_as_uint(r32[G_FLAGS]);
+        const uint32_t fl = __float_as_uint(r32[G_FLAGS + G32]);
         R row[row_w<R>()];
 #pragma unroll
         for (int i = 0; i < row_w<R>(); ++i) row[i] = sizeof(R) == 8 ? (R)r64[i] : (R)r32[i];
@@ -1136,6 +1134,9 @@ __device__ __forceinline__ void row_store(void* base, size_t row_off, uint32_t l
 // One work-item per (chain, block of 128 seconds).  The boundary draws come
 // from the draw tables, so the per-second loop holds only the R copies of the
 // sampler pairs and does no fp64 work in fp32 mode.
+#ifndef TMH_PVF_VGPR   // leading PVF fields pinned in VGPRs in the fp32 expansion
+#define TMH_PVF_VGPR 22
+#endif
 #ifndef TMH_ROW_PREFETCH
 #define TMH_ROW_PREFETCH 0
 #endif
@@ -1170,6 +1171,16 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
     const uint32_t j0 = b * BLOCK_STEPS, j1 = min(j0 + (uint32_t)BLOCK_STEPS, nsteps);
     const uint64_t chain = chain0 + c;
     const int64_t fm = first_minute(utc0, W0);
+    // the fp32 PV constants as per-lane registers (VGPRs): held in SGPRs across
+    // the loop they are spilled to VGPR lanes and read back by v_readlane each step
+    PVF pkv = kp.pvf;
+#if TMH_PVF_VGPR
+    if constexpr (sizeof(R) == 4 && !SITES) {
+        float* f = reinterpret_cast<float*>(&pkv);
+#pragma unroll
+        for (int i = 0; i < TMH_PVF_VGPR; ++i) asm volatile("v_mov_b32 %0, %1" : "=v"(f[i]) : "s"(f[i]));
+    }
+#endif
     Acc acc{0.0, 0.0, 0.0, -INFINITY};
     bool alive = false;
     int32_t fault = INT_MAX;
@@ -1234,7 +1245,7 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
 #else
         load_row(j, row);
 #endif
-        const uint32_t fl = sizeof(R) == 8 ? (uint32_t)tab64[(size_t)j * ROW + G_FLAGS] : __float_as_uint(row[G_FLAGS]);
+        const uint32_t fl = sizeof(R) == 8 ? (uint32_t)tab64[(size_t)j * ROW + G_FLAGS] : __float_as_uint(row[G_FLAGS + G32]);
         R csi = R(NAN), pv = R(NAN), meter = R(NAN), res = R(NAN);
         uint8_t cov = 255;
         const bool ok = alive && (int32_t)j < fault;
@@ -1283,7 +1294,7 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
                 const bool night = lane_row<R>(ls, sun + (size_t)j * SUN_W, kp.module, row);
                 flp = night ? (fl | FL_NIGHT) : (fl & ~(uint32_t)FL_NIGHT);
             }
-            second_body<R>(kp, kp.pvf, row, flp, fs, covered, noise_z<R>(odd ? pair.z : pair.x), meter_w<R>(odd ? pair.w : pair.y),
+            second_body<R>(kp, pkv, row, flp, fs, covered, noise_z<R>(odd ? pair.z : pair.x), meter_w<R>(odd ? pair.w : pair.y),
                            csi, pv, meter, res);
         }
         if (fl & (FL_DAY | FL_HOUR)) ++evi;

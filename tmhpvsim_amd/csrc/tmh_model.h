@@ -50,15 +50,20 @@ enum : uint32_t { FL_DAY = 1, FL_HOUR = 2, FL_MIN = 4, FL_NIGHT = 8 };
 enum {
     G_MINF = 0, G_HOURF = 1, G_DAYF = 2, G_FLAGS = 3, G_COSZ = 4, G_CSIMAX = 5, G_GHICS = 6,
     G_I0H = 7, G_I0 = 8, G_KNC = 9, G_AM = 10, G_DISCOK = 11, G_RB = 12, G_DNIEXTRA = 13,
-    G_TERM2 = 14, G_GFAC = 15, G_COSAOI = 16, G_F1 = 17, G_F2 = 18,
-    // fp32 table only: each clock fraction again beside its complement 1 - f
-    // (computed in fp32 exactly as the kernels did), 8-byte aligned pairs, so an
-    // interpolation f a + (1 - f) b is one packed multiply on an SGPR pair + an add
-    G_MINF_C = 20, G_MINF2 = 21, G_HOURF_C = 22, G_HOURF2 = 23, G_DAYF_C = 24, G_DAYF2 = 25
+    G_TERM2 = 14, G_GFAC = 15, G_COSAOI = 16, G_F1 = 17, G_F2 = 18
 };
-#define ROW32 26   // fp32 clock/geometry row width (the fp64 row is ROW = TMH_GEOM_FIELDS)
+// fp32 row (ROW32 = 22 floats, the kernels' scalar loads): each clock fraction
+// beside its complement 1 - f (rounded in fp32 exactly as the kernels would),
+// 8-byte aligned pairs, so an interpolation f a + (1 - f) b is one packed
+// multiply on an SGPR pair plus an add; then flags and G_COSZ..G_F2, i.e. the
+// fp64 row's field G_X (X >= FLAGS) sits at G_X + G32.  Kept compact: every
+// field is held in SGPRs through the step.
+enum { G32_MINF_C = 0, G32_MINF = 1, G32_HOURF_C = 2, G32_HOURF = 3, G32_DAYF_C = 4, G32_DAYF = 5, G32 = 3 };
+#define ROW32 22
 template <typename R>
 constexpr int row_w() { return sizeof(R) == 8 ? ROW : ROW32; }
+template <typename R>   // the row as the fp64 field layout (G_FLAGS..G_F2) sees it
+constexpr int row_off() { return sizeof(R) == 8 ? 0 : G32; }
 
 enum { S_CC = 0, S_CLEAR_DAY = 1, S_CLOUDY_HOUR = 2, S_CLOUDY_NOISE = 3, S_CLEAR_NOISE = 4, S_WS = 5 };
 
@@ -890,8 +895,9 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
 // the kernels' row of one chain's own site (fp32 rows carry the reciprocals
 // of I0h and dni_extra, like geom_kernel's fp32 table)
 template <typename R>
-__device__ __forceinline__ void site_row(const double* g, const double* sun, R* row)
+__device__ __forceinline__ void site_row(const double* g, const double* sun, R* row_base)
 {
+    R* row = row_base + row_off<R>();
 #pragma unroll
     for (int i = G_COSZ; i <= G_F2; ++i) row[i] = (R)g[i];
     if constexpr (sizeof(R) == 4) {
@@ -1089,7 +1095,7 @@ __device__ __forceinline__ R rinterp_row(const FSamp<R>& f, int k, const R* row,
 {
     if constexpr (sizeof(R) == 8) return rinterp(f, k, row[fi]);
     else {
-        const int pc = fi == G_MINF ? G_MINF_C : (fi == G_HOURF ? G_HOURF_C : G_DAYF_C);
+        const int pc = fi == G_MINF ? G32_MINF_C : (fi == G_HOURF ? G32_HOURF_C : G32_DAYF_C);
         return row[pc + 1] * f.a[k] + row[pc] * f.b[k];
     }
 }
@@ -1132,10 +1138,10 @@ __device__ __forceinline__ void second_body(const KParams& kp, const PVF& pk, co
     const R n_clear = rinterp_row(fs, S_CLEAR_NOISE, row, G_MINF), n_cloudy = rinterp_row(fs, S_CLOUDY_NOISE, row, G_MINF);
     csi = (covered ? a_clear : a_cloudy) * ((covered ? n_clear : n_cloudy) + eps);
 #ifdef TMH_DIAG_NO_PV
-    pv = csi * row[G_GHICS];
+    pv = csi * row[G_GHICS + row_off<R>()];
 #else
     if constexpr (sizeof(R) == 8) pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power<R>(kp, row, csi) : R(0);
-    else pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power_f(pk, row, csi) : 0.0f;
+    else pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power_f(pk, row + G32, csi) : 0.0f;
 #endif
     meter = meter_in;
     res = meter - pv;
