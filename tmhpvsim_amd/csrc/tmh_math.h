@@ -40,7 +40,17 @@ __device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c
         // about 25 % less issue time per block on gfx950 (scripts/micro/philox_bench.hip)
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        // rounds 0-1: the counter words are mostly wave-uniform (step, tag, chain
+        // high word) and plain xors fold into SALU; from round 2 on both words are
+        // per lane and the three-way xor is one gfx950 v_bitop3_b32 (0x96 = a^b^c)
+        uint32_t n0, n2;
+        if (r < 2) {
+            n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+            n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        } else {
+            n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, k0, 0x96);
+            n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, k1, 0x96);
+        }
         c0 = n0;
         c1 = (uint32_t)p1;
         c2 = n2;
