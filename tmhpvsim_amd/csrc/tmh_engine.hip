@@ -1135,7 +1135,7 @@ __device__ __forceinline__ void row_store(void* base, size_t row_off, uint32_t l
 // from the draw tables, so the per-second loop holds only the R copies of the
 // sampler pairs and does no fp64 work in fp32 mode.
 #ifndef TMH_PVF_VGPR   // leading PVF fields pinned in VGPRs in the fp32 expansion
-#define TMH_PVF_VGPR 22
+#define TMH_PVF_VGPR 25
 #endif
 #ifndef TMH_ROW_PREFETCH
 #define TMH_ROW_PREFETCH 0
@@ -1706,6 +1706,9 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
         f.ic2 = (float)iv[6];
         f.ic3 = (float)iv[7];
         f.pnt = (float)iv[8];
+        f.pacoc = (float)(iv[0] > 0.0 ? iv[0] : 0.0);
+        f.eps0 = (float)(k.sqrt6 * 0.001);
+        f.eps1 = (float)(k.sqrt6 * (0.0015 * 8));
     }
     memcpy(e->gp.site, p->site, sizeof e->gp.site);
     memcpy(e->gp.linke, p->linke, sizeof e->gp.linke);

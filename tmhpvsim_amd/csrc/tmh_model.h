@@ -18,6 +18,8 @@ namespace tmh {
 struct PVF {
     float tmod_k, temp_air, dt_1e3, fd, bvmpo, mbvmp, nkq, impo_c0, impo_c1, aimp, vmpo, c2ns, c3ns;
     float paco, pdco, vdco, pso, ic0, ic1, ic2, ic3, pnt;
+    float pacoc;        // max(Paco, 0): the upper bound of the final clamp
+    float eps0, eps1;   // sqrt(6) 0.001, sqrt(6) 0.0015 * 8: the noise scale is eps0 + eps1 cc
 };
 
 struct KParams {
@@ -1048,7 +1050,8 @@ __device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float 
     const float Ee = g[G_F1] * fmaf(poa_direct, g[G_F2], k.fd * poa_diffuse) * 1e-3f;
     const float Bvmpo = fmaf(k.mbvmp, 1.0f - Ee, k.bvmpo);
     const float delta = k.nkq * (tcell + 273.15f);
-    const float logEe = Ee > 0.0f ? __builtin_amdgcn_logf(Ee) * 0.693147180559945309f : (Ee == 0.0f ? -INFINITY : NAN);
+    // the hardware log2 already gives -inf at +-0 and NaN below 0 or at NaN
+    const float logEe = __builtin_amdgcn_logf(Ee) * 0.693147180559945309f;
     const float dt25 = tcell - 25.0f;
     const float imp = fmaf(k.impo_c1, Ee, k.impo_c0) * Ee * fmaf(k.aimp, dt25, 1.0f);
     const float dl = delta * logEe;
@@ -1060,11 +1063,10 @@ __device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float 
     const float B = k.pso * fmaf(k.ic2, dv, 1.0f);
     const float C = k.ic0 * fmaf(k.ic3, dv, 1.0f);
     const float AmB = A - B, pmB = pdc - B;
-    float ac = fmaf(C, pmB * pmB, fmaf(-C, AmB, k.paco * __builtin_amdgcn_rcpf(AmB)) * pmB);
-    ac = isnan(ac) ? ac : fminf(ac, k.paco);
-    if (pdc < k.pso) ac = -fabsf(k.pnt);
-    if (isnan(ac)) return 0.0f;   // .fillna(0.)
-    return fmaxf(ac, 0.0f);       // .clip(lower=0.)
+    const float ac = fmaf(C, pmB * pmB, fmaf(-C, AmB, k.paco * __builtin_amdgcn_rcpf(AmB)) * pmB);
+    // min(ac, Paco) unless NaN, -|Pnt| below the cut-in, .fillna(0), .clip(lower=0):
+    // -|Pnt| <= 0 clips to 0 and a NaN fills to 0; the rest is one med3 into [0, Paco]
+    return (pdc < k.pso || isnan(ac)) ? 0.0f : __builtin_amdgcn_fmed3f(ac, 0.0f, k.pacoc);
 }
 
 // ------------------------------------------------------------ fused per-second body
@@ -1131,7 +1133,9 @@ __device__ __forceinline__ void second_body(const KParams& kp, const PVF& pk, co
                                             R& res)
 {
     const R cloudcover = rinterp_row(fs, S_CC, row, G_HOURF);   // == interp() bit for bit when R = double
-    const R eps = z * (R(kp.sqrt6) * (R(0.001) + R(0.0015 * 8) * cloudcover)) + R(0);
+    R eps;
+    if constexpr (sizeof(R) == 8) eps = z * (R(kp.sqrt6) * (R(0.001) + R(0.0015 * 8) * cloudcover)) + R(0);
+    else eps = z * fmaf(pk.eps1, cloudcover, pk.eps0);   // fp32: the scale as one FMA (z is never 0)
     // both branches' factors, then a select on values (a select on the sampler
     // index would make the compiler index the sampler arrays dynamically: scratch)
     const R a_clear = rinterp_row(fs, S_CLEAR_DAY, row, G_DAYF), a_cloudy = rinterp_row(fs, S_CLOUDY_HOUR, row, G_HOURF);
