@@ -59,13 +59,14 @@ def parse():
     ap.add_argument("--cpu-sample-chains", type=int, default=8192)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--path", default="auto", choices=["auto", "sequential", "time_parallel"])
-    ap.add_argument("--build-on", default="expand", choices=["expand", "walk"],
+    ap.add_argument("--build-on", default=None, choices=["expand", "walk"],
                     help="stream of each batch's construction, plan and draws: in order on the expansion "
-                         "stream, or ahead of its walk on the high-priority walk stream")
+                         "stream, or ahead of its walk on the walk stream (default: walk for c2, else expand)")
     ap.add_argument("--no-stagger", dest="stagger", action="store_false",
                     help="issue each batch as one tmh_step (batches then run in lockstep across streams)")
-    ap.add_argument("--walk-priority", default="high", choices=["high", "normal"],
-                    help="HIP stream priority of the construction + segment walk (pipelined batches)")
+    ap.add_argument("--walk-priority", default=None, choices=["high", "normal"],
+                    help="HIP stream priority of the construction + segment walk (pipelined batches; "
+                         "default: normal for c2, where construction shares the walk stream, else high)")
     ap.add_argument("--pipeline", type=int, default=None,
                     help="batches in flight on separate HIP streams (1 = no overlap): the segment walks of the "
                          "next batches (latency-bound, one wave per SIMD) run beside this batch's expansion")
@@ -78,6 +79,10 @@ def parse():
     a.cc = a.cc or ("markov" if c5 else "faithful")
     a.window = min(a.window or (86400 if (c5 or c4) else a.seconds), a.seconds)
     a.start = a.start or ("2019-01-01 00:00:00" if c4 else "2019-09-05 00:00:00")
+    # C2 (same-box A/B, r01): construction on the walk stream at normal priority
+    # 1.94e11 chain-s/s vs 1.82e11 on the expansion stream with high-priority walks
+    a.build_on = a.build_on or ("walk" if a.workload == "c2" else "expand")
+    a.walk_priority = a.walk_priority or ("normal" if a.workload == "c2" else "high")
     return a
 
 
@@ -251,7 +256,7 @@ def main():
     def build(k):      # construction of batch k's chains, its plan and draws
         cx = ctxs[k % len(ctxs)]
         cx.chain0 = (rank + k * world) * n
-        if args.build_on == "walk":   # on the batch's high-priority walk stream, after the expansion
+        if args.build_on == "walk":   # on the batch's walk stream, after the expansion
             bs, bp = cx.wstream, cx.wptr   # that last used this context: beside the running expansion
             if cx.expanded is not None:
                 bs.wait_event(cx.expanded)
@@ -382,7 +387,7 @@ def main():
                                + f"{args.start[:10]}, {args.mode} mode ({'meter+pv+residual fp32 trace' if args.mode == 'trace' else 'on-GPU stats'})",
                    "chains_per_gpu": n, "seconds": secs, "parallelism": f"chains sharded over {world} GPU(s)",
                    "batches_in_flight": len(ctxs), "staggered": bool(args.stagger and nwin == 1),
-                   "construction_on": args.build_on},
+                   "construction_on": args.build_on, "walk_priority": args.walk_priority},
         "roofline": ({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": achieved / HBM_PEAK_GBS, "traffic": traffic(args, n, secs),
                       "kernel": "expand_kernel (P2, " + sim.path + ")", "kernel_ms": kmean,
