@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--walk-priority", default=None, choices=["high", "normal"],
                     help="HIP stream priority of the construction + segment walk (pipelined batches; "
                          "default: normal for c2, where construction shares the walk stream, else high)")
+    ap.add_argument("--expand-priority", default="normal", choices=["high", "normal"],
+                    help="HIP stream priority of the expansion stream (pipelined batches)")
     ap.add_argument("--pipeline", type=int, default=None,
                     help="batches in flight on separate HIP streams (1 = no overlap): the segment walks of the "
                          "next batches (latency-bound, one wave per SIMD) run beside this batch's expansion")
@@ -197,7 +199,7 @@ def main():
     # one stream for every batch's expansion: expansions run back to back, in order
     # (they fill the chip on their own), while the walks of the next batches run on
     # their contexts' high-priority streams beside them
-    estream = torch.cuda.Stream(dev)
+    estream = torch.cuda.Stream(dev, priority=prio_hi if args.expand_priority == "high" else prio_lo)
     eptr = C.c_void_p(estream.cuda_stream)
     torch.cuda.synchronize()
     L.tmh_profile_enable(sim._eng, 1)
