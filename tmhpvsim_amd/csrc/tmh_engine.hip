@@ -1143,8 +1143,8 @@ __device__ __forceinline__ void row_store(void* base, size_t row_off, uint32_t l
 #ifndef TMH_DIAG_EXP_LDS   // diagnostic: extra LDS per expand workgroup (caps its occupancy)
 #define TMH_DIAG_EXP_LDS 0
 #endif
-#ifndef TMH_EXP_WAVES   // min waves per SIMD of the fp32 single-site expansion: 6 = at most 80 VGPRs (-3.5 % vs 5)
-#define TMH_EXP_WAVES 6
+#ifndef TMH_EXP_WAVES   // min waves per SIMD of the fp32 single-site expansion: 7 = at most 72 VGPRs (alone -4 % vs 6, no VGPR spills)
+#define TMH_EXP_WAVES 7
 #endif
 template <typename R, int OUT, bool SITES>
 #ifndef TMH_SITES_WAVES   // min waves per SIMD of the per-chain-site expansion: 2 (a few spills) is 35 % faster than 1
