@@ -1146,11 +1146,14 @@ __device__ __forceinline__ void row_store(void* base, size_t row_off, uint32_t l
 #ifndef TMH_EXP_WAVES   // min waves per SIMD of the fp32 single-site expansion: 7 = at most 72 VGPRs (alone -4 % vs 6, no VGPR spills)
 #define TMH_EXP_WAVES 7
 #endif
+#ifndef TMH_EXP_WAVES_STATS   // the same for the statistics / other outputs (C3, C4): 6 = 80 VGPRs
+#define TMH_EXP_WAVES_STATS 6
+#endif
 template <typename R, int OUT, bool SITES>
 #ifndef TMH_SITES_WAVES   // min waves per SIMD of the per-chain-site expansion: 2 (a few spills) is 35 % faster than 1
 #define TMH_SITES_WAVES 2
 #endif
-__global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 : TMH_EXP_WAVES)) void expand_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0,
+__global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 : (OUT == OUT_TRACE3 ? TMH_EXP_WAVES : TMH_EXP_WAVES_STATS))) void expand_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0,
                                                      uint32_t n, int64_t W0, uint32_t nsteps, int64_t utc0,
                                                      const double* __restrict__ tab64,
                                                      const float* __restrict__ tab32,
