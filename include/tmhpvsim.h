@@ -51,6 +51,7 @@ extern "C" {
 #define TMH_CHAIN_SIGMA_OVERFLOW 3  /* sigma arrays exceed TMH_SIGMA_CAP (no reference analogue) */
 #define TMH_CHAIN_U_EXHAUSTED 4     /* injected uniform stream ran out */
 #define TMH_CHAIN_SEGMENT_OVERFLOW 5 /* > n_steps/8 + 64 cloud segments in one window (time-parallel path) */
+#define TMH_CHAIN_GUARD_OVERFLOW 6   /* fp32 guard-band records of the batch exceeded their room (never observed; time-parallel path) */
 
 /* ---- modes ---- */
 #define TMH_CC_FAITHFUL 0  /* reference: a fresh get_cloud_cover generator per hourly draw */
@@ -241,6 +242,20 @@ int tmh_expand(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_
 int tmh_walk_part(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, int64_t step0,
                   uint32_t n_steps, const void* plan, void* scratch, size_t scratch_bytes,
                   const void* prev_scratch, uint32_t prev_n_steps, int parts, void* stream);
+
+/* tmh_expand in its two halves, for callers that overlap independent batches
+ * (bench.py): TMH_EXPAND_KERNEL = the window's minute draws and the P2
+ * expansion (traces / statistics); TMH_EXPAND_COMMIT = the fp32 guard-band
+ * recomputation (fixup) and the state / statistics commit.  The commit half is
+ * latency-bound (a few waves); on a second stream, after an event recorded
+ * behind the kernel half, it runs beside the next batch's expansion.  Order:
+ * KERNEL then COMMIT on the same buffers; the traces and statistics are final
+ * after COMMIT.  tmh_expand == KERNEL | COMMIT. */
+#define TMH_EXPAND_KERNEL 1
+#define TMH_EXPAND_COMMIT 2
+int tmh_expand_part(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, int64_t step0,
+                    uint32_t n_steps, const tmh_ustream* inj, const tmh_trace* trace, const tmh_stats* stats,
+                    const void* plan, void* scratch, size_t scratch_bytes, int parts, void* stream);
 
 /* Kernel timing (measurement only).  While enabled, tmh_step records HIP
  * events, on the stream each kernel runs on, around the kernels of the

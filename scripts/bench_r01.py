@@ -30,7 +30,7 @@ import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -175,7 +175,6 @@ def main():
             self.wptr = C.c_void_p(self.wstream.cuda_stream)
             self.walked = torch.cuda.Event()
             self.done = torch.cuda.Event()
-            self.kernel_done = torch.cuda.Event()
             self.expanded = None   # recorded after this context's last expansion
             self.state = torch.zeros(L.tmh_state_bytes(n), dtype=torch.uint8, device=dev)
             self.plan = torch.empty(L.tmh_plan_bytes(win), dtype=torch.uint8, device=dev)
@@ -280,19 +279,16 @@ def main():
                                    cx.scratch.numel(), None, 0, _lib.WALK_SEGMENTS, cx.wptr))
         cx.walked.record(cx.wstream)
 
-    def finish(k):     # second half: the expansion (trace / stats) on the expansion stream, then its
-        cx = ctxs[k % len(ctxs)]   # commit (fp32 guard-band fixup + state) on the batch's walk stream,
-        estream.wait_event(cx.walked)   # beside the next batch's expansion (tmh_expand_part)
-        args_ = (sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs, None, C.byref(cx.tr),
-                 C.byref(cx.st) if cx.st is not None else None, C.c_void_p(cx.plan.data_ptr()),
-                 C.c_void_p(cx.scratch.data_ptr()), cx.scratch.numel())
-        _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_KERNEL, eptr))
-        cx.kernel_done.record(estream)
-        cx.wstream.wait_event(cx.kernel_done)
-        _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_COMMIT, cx.wptr))
+    def finish(k):     # second half: expansion (trace / stats) and commit (tmh_expand)
+        cx = ctxs[k % len(ctxs)]
+        estream.wait_event(cx.walked)
+        _lib.check(L.tmh_expand(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs, None,
+                                C.byref(cx.tr), C.byref(cx.st) if cx.st is not None else None,
+                                C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
+                                cx.scratch.numel(), eptr))
         if cx.expanded is None:
             cx.expanded = torch.cuda.Event()
-        cx.expanded.record(cx.wstream)
+        cx.expanded.record(estream)
 
     def run_batches(k0, cnt):
         """Batches k0 .. k0 + cnt - 1.  One-window batches are software-pipelined:
@@ -323,7 +319,6 @@ def main():
         estream.synchronize()
         for cx in ctxs:
             cx.stream.synchronize()
-            cx.wstream.synchronize()
         hist = sum(cx.hist for cx in ctxs)
         acc = torch.stack([cx.acc for cx in ctxs])
         tot = dict(energy_pv=acc[:, 0].sum(), energy_meter=acc[:, 1].sum(), energy_residual=acc[:, 2].sum(),

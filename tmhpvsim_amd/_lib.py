@@ -22,14 +22,14 @@ TMH_FP32, TMH_FP64 = 0, 1
 PATH_AUTO, PATH_SEQUENTIAL, PATH_TIME_PARALLEL = 0, 1, 2
 CHAIN_STATUS = {0: "ok", 1: "NameError (init)", 2: "AssertionError (CloudCoverBinary)",
                 3: "sigma capacity exceeded", 4: "injected stream exhausted",
-                5: "segment capacity exceeded"}
+                5: "segment capacity exceeded", 6: "fp32 guard-band records exceeded"}
 STATE_FIELDS = ["sb_cc", "sb_clear_day", "sb_cloudy_hour", "sb_cloudy_noise", "sb_clear_noise", "sb_ws",
                 "sa_cc", "sa_clear_day", "sa_cloudy_hour", "sa_cloudy_noise", "sa_clear_noise", "sa_ws",
                 "cloud_length", "clear_length", "markov_state", "sec", "sigma_len", "pos", "status",
-                "ncalls", "sigma_cloud", "sigma_clear", "reserved0", "reserved1"]
+                "ncalls", "sigma_cloud", "sigma_clear", "fn_cloudy", "fn_clear"]
 STATE_DTYPES = {**{f: np.float64 for f in STATE_FIELDS[:15]}, "sec": np.int32, "sigma_len": np.int32,
                 "pos": np.uint32, "status": np.uint32, "ncalls": np.uint32, "sigma_cloud": np.float64,
-                "sigma_clear": np.float64}
+                "sigma_clear": np.float64, "fn_cloudy": np.float32, "fn_clear": np.float32}
 
 
 class Params(C.Structure):
@@ -64,9 +64,10 @@ EXPORTS = ["tmh_abi_version", "tmh_last_error", "tmh_state_bytes", "tmh_state_of
            "tmh_scratch_bytes", "tmh_workspace_bytes", "tmh_engine_create", "tmh_engine_destroy", "tmh_engine_path",
            "tmh_init", "tmh_run", "tmh_plan", "tmh_step", "tmh_probe", "tmh_profile_enable", "tmh_profile_read",
            "tmh_set_shape_tables", "tmh_set_sites", "tmh_walk", "tmh_expand",
-           "tmh_walk_part"]
+           "tmh_walk_part", "tmh_expand_part"]
 K_EXPAND, K_SEGMENTS, K_CANDIDATES, K_STEP = 0, 1, 2, 3
 WALK_DRAWS, WALK_SEGMENTS = 1, 2
+EXPAND_KERNEL, EXPAND_COMMIT = 1, 2
 
 _lib = None
 
@@ -113,6 +114,9 @@ def load():
     L.tmh_walk_part.argtypes = [p, p, u64, u32, i64, u32, p, p, sz, p, u32, C.c_int, p]
     L.tmh_expand.argtypes = [p, p, u64, u32, i64, u32, C.POINTER(UStream), C.POINTER(Trace), C.POINTER(Stats), p, p,
                              sz, p]
+    if hasattr(L, "tmh_expand_part"):   # (absent from round-1 builds, which same-box A/B runs still load)
+        L.tmh_expand_part.argtypes = [p, p, u64, u32, i64, u32, C.POINTER(UStream), C.POINTER(Trace),
+                                      C.POINTER(Stats), p, p, sz, C.c_int, p]
     L.tmh_probe.argtypes = [C.c_int, C.c_double, p, p, u32, p]
     L.tmh_profile_enable.argtypes = [p, C.c_int]
     L.tmh_set_shape_tables.argtypes = [p, p, p, u32]
@@ -120,8 +124,10 @@ def load():
     L.tmh_profile_read.argtypes = [p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int)]
     for name in ("tmh_state_offsets", "tmh_engine_create", "tmh_engine_destroy", "tmh_engine_path", "tmh_init",
                  "tmh_run", "tmh_step", "tmh_plan", "tmh_probe", "tmh_profile_enable", "tmh_profile_read",
-                 "tmh_set_shape_tables", "tmh_set_sites", "tmh_walk", "tmh_expand", "tmh_walk_part"):
-        getattr(L, name).restype = C.c_int
+                 "tmh_set_shape_tables", "tmh_set_sites", "tmh_walk", "tmh_expand", "tmh_walk_part",
+                 "tmh_expand_part"):
+        if hasattr(L, name):
+            getattr(L, name).restype = C.c_int
     if L.tmh_abi_version() != TMH_ABI_VERSION:
         raise ImportError(f"libtmhpvsim ABI {L.tmh_abi_version()} != {TMH_ABI_VERSION}")
     _lib = L

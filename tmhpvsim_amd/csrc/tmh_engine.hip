@@ -49,6 +49,7 @@ namespace {
 #define TMH_BLOCK_STEPS 128
 #endif
 constexpr int BLOCK_STEPS = TMH_BLOCK_STEPS;   // seconds per P2 work-item
+static_assert(BLOCK_STEPS <= 128, "FixRec holds a 128-bit mask of a block's seconds");
 
 struct BlockDesc {                 // as of the step before the block start; -1 = none in the window
     int32_t q0, q1;                // minute-draw indices of the last two minute boundaries
@@ -74,6 +75,20 @@ struct SegView {                   // P1 -> P2 scratch
     uint32_t kcap;
     void* mtab;                    // [nmin][2][n] R: the _next_min draws (cloudy, clear noise) of every minute boundary
     uint32_t nmin;
+    struct FixRec* fix;            // [fixcap] fp32 guard-band seconds for fixup_kernel
+    uint32_t fixcap;
+    uint32_t* nfix;                // records appended (> fixcap: some were lost, see commit_kernel)
+    double* corr;                  // [2][n] exact pv / residual sum corrections of the fixed seconds
+};
+
+// A (chain, 128-s block) of the fp32 expansion with a second in a guard band of
+// the PV chain's discontinuities (pv_power_f): fixup_kernel recomputes it.
+struct FixRec {
+    uint32_t c;                    // chain index in the batch
+    uint32_t b;                    // block
+    uint32_t jr;                   // segment record index at the block's last step
+    uint32_t pad;
+    uint4 mask;                    // bit i: second b * 128 + i lies in a guard band
 };
 
 // The window-start values a walk takes from the PREVIOUS window's walk instead of
@@ -256,6 +271,9 @@ __global__ __launch_bounds__(256) void init_kernel(KParams kp, StateView st, uin
     }
     if (f && !ch.status) ch.status = f;
     store_chain(st, c, ch);
+    // the fp32 kernels' noise pairs start as the constructor's draws rounded
+    st.fn[0][c] = make_float2((float)ch.s.b[S_CLOUDY_NOISE], (float)ch.s.a[S_CLOUDY_NOISE]);
+    st.fn[1][c] = make_float2((float)ch.s.b[S_CLEAR_NOISE], (float)ch.s.a[S_CLEAR_NOISE]);
 }
 
 // ------------------------------------------------------------ plan kernels
@@ -300,6 +318,7 @@ __global__ __launch_bounds__(256) void geom_kernel(GParams gp, int64_t step0, ui
     o32[G_FLAGS + G32] = __uint_as_float(fl);
     o32[G_I0H + G32] = (float)(1.0 / g[G_I0H]);   // fp32 path multiplies by reciprocals
     o32[G_DNIEXTRA + G32] = (float)(1.0 / g[G_DNIEXTRA]);
+    o32[G_AM + G32] = (float)(g[G_AM] * LOG2E);   // exp(c am) = exp2(c * am log2 e)
 }
 
 // Compact the window's day/hour boundary steps, in order (one workgroup).
@@ -347,25 +366,18 @@ __host__ __device__ __forceinline__ int64_t first_minute(int64_t utc0, int64_t W
 }
 inline int64_t first_minute_host(int64_t utc0, int64_t W0) { return first_minute(utc0, W0); }
 
-// Descriptor of the sampler state after step W0 + min(b * BLOCK_STEPS, n) - 1,
-// for b = 0 .. nblk (the last one describes the window end).
-__global__ __launch_bounds__(256) void desc_kernel(int64_t step0, uint32_t n, int64_t utc0,
-                                                   const int2* __restrict__ events,
-                                                   const uint32_t* __restrict__ n_events, BlockDesc* desc,
-                                                   uint32_t nblk)
+// Descriptor of the sampler state after step p (window [step0, step0 + n), p >=
+// step0): the last two minute draws, hour and clear-day events at or before p.
+__device__ BlockDesc desc_for(int64_t step0, uint32_t n, int64_t utc0, const int2* __restrict__ events, int ne,
+                              int64_t p)
 {
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b > nblk) return;
     BlockDesc d{-1, -1, -1, -1, -1, -1, 0, -1};
-    const int64_t jb = min((int64_t)b * BLOCK_STEPS, (int64_t)n);
-    if (jb > 0) {
-        const int64_t p = step0 + jb - 1;                  // last step before the block
+    {
         const int64_t lo = step0 > 1 ? step0 : 1;          // step 0 is the constructor time
         const int64_t fm = first_minute(utc0, step0);
         const int64_t m0 = p - (((utc0 + p) % 60) + 60) % 60;
         if (m0 >= lo) d.q0 = (int32_t)((m0 - step0 - fm) / 60);
         if (m0 - 60 >= lo) d.q1 = (int32_t)((m0 - 60 - step0 - fm) / 60);
-        const int ne = (int)min(*n_events, ev_cap_dev(n));
         int a = 0, z = ne;                                  // last event <= p
         while (a < z) {
             const int mid = (a + z) / 2;
@@ -394,7 +406,50 @@ __global__ __launch_bounds__(256) void desc_kernel(int64_t step0, uint32_t n, in
             }
         }
     }
-    desc[b] = d;
+    return d;
+}
+
+// desc_for(p) from an earlier descriptor d (of some step before p, evi = its first
+// event after it): the window's events up to p applied forward (clear_day's day
+// push before its hour push), the minute indices taken at p
+__device__ __forceinline__ BlockDesc desc_advance(BlockDesc d, int64_t step0, int64_t utc0,
+                                                  const int2* __restrict__ events, int ne, int64_t p)
+{
+    int i = d.evi;
+    for (; i < ne && (int64_t)events[i].x <= p; ++i) {
+        const int fl = events[i].y;
+        if (fl & FL_DAY) {
+            d.cd1 = d.cd0;
+            d.cd0 = 2 * i;
+        }
+        if (fl & FL_HOUR) {
+            d.h2 = d.h1;
+            d.h1 = d.h0;
+            d.h0 = i;
+            d.cd1 = d.cd0;
+            d.cd0 = 2 * i + 1;
+        }
+    }
+    d.evi = i;
+    const int64_t lo = step0 > 1 ? step0 : 1, fm = first_minute(utc0, step0);
+    const int64_t m0 = p - (((utc0 + p) % 60) + 60) % 60;
+    d.q0 = m0 >= lo ? (int32_t)((m0 - step0 - fm) / 60) : -1;
+    d.q1 = m0 - 60 >= lo ? (int32_t)((m0 - 60 - step0 - fm) / 60) : -1;
+    return d;
+}
+
+// Descriptor of the sampler state after step W0 + min(b * BLOCK_STEPS, n) - 1,
+// for b = 0 .. nblk (the last one describes the window end).
+__global__ __launch_bounds__(256) void desc_kernel(int64_t step0, uint32_t n, int64_t utc0,
+                                                   const int2* __restrict__ events,
+                                                   const uint32_t* __restrict__ n_events, BlockDesc* desc,
+                                                   uint32_t nblk)
+{
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > nblk) return;
+    const int64_t jb = min((int64_t)b * BLOCK_STEPS, (int64_t)n);
+    desc[b] = jb > 0 ? desc_for(step0, n, utc0, events, (int)min(*n_events, ev_cap_dev(n)), step0 + jb - 1)
+                     : BlockDesc{-1, -1, -1, -1, -1, -1, 0, -1};
 }
 
 // ------------------------------------------------------------ boundary draws
@@ -447,34 +502,29 @@ __global__ __launch_bounds__(256) void markov_cc_kernel(KParams kp, StateView st
 }
 
 // _next_min draws of every (minute boundary, chain): clearskyindexmodel.py:86-95,109-111
-// the two _next_min draws of the minute boundary at window step j (keyed by step)
+// the two _next_min draws of the minute boundary at window step j (keyed by step):
+// fp64 (minute_noise) or the fp32 kernels' copies (minute_noise_fast)
 template <typename R>
 __device__ __forceinline__ void minute_draws(const DrawParams& dp, uint64_t chain, int64_t step, double cc,
                                              double& cloudy, double& clear)
 {
     const U4 u = keyed_block(dp.seed, chain, (uint64_t)step, TAG_BOUNDARY, 2);
-    cloudy = minute_noise<R>(u52(u.x, u.y), 0.01, 0.003, cc, dp.sqrt09);
-    clear = minute_noise<R>(u52(u.z, u.w), 0.001, 0.0015, cc, dp.sqrt09);
+    if constexpr (sizeof(R) == 8) {
+        cloudy = minute_noise<R>(u52(u.x, u.y), 0.01, 0.003, cc, dp.sqrt09);
+        clear = minute_noise<R>(u52(u.z, u.w), 0.001, 0.0015, cc, dp.sqrt09);
+    } else {
+        cloudy = minute_noise_fast(u52(u.x, u.y), 0.01, 0.003, cc, dp.sqrt09);
+        clear = minute_noise_fast(u52(u.z, u.w), 0.001, 0.0015, cc, dp.sqrt09);
+    }
 }
 
-// The _next_min draws of every (candidate minute boundary, chain) of the window,
-// one work-item each, before the expansion: minute m sits at window step
-// fm + 60 m; its cloud-cover pair is the one in force there (the last two hourly
-// draws at or before it, or the window-start pair).  The expansion and the
-// block-start reconstruction read them instead of drawing in their loops.
-template <typename R>
-__global__ __launch_bounds__(256) void minute_table_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
-                                                           int64_t W0, uint32_t nsteps, int64_t fm,
-                                                           const double* __restrict__ tab64,
-                                                           const int2* __restrict__ events,
-                                                           const uint32_t* __restrict__ n_events, SegView sg)
+// the cloud cover in force at the minute boundary at window step jm (the last
+// two hourly draws at or before it, or the window-start pair), interpolated
+__device__ __forceinline__ double minute_cc(const StateView& st, const SegView& sg, uint32_t n, uint32_t c,
+                                            int64_t W0, int64_t jm, const int2* __restrict__ events, int ne,
+                                            const double* __restrict__ tab64)
 {
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t m = blockIdx.y;
-    const int64_t jm = fm + 60 * (int64_t)m;
-    if (c >= n || jm >= (int64_t)nsteps) return;
     const int64_t step = W0 + jm;
-    const int ne = (int)min(*n_events, ev_cap_dev(nsteps));
     int lo = 0, hi = ne;   // h0 = number of boundary events at or before the step, minus one
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
@@ -491,8 +541,32 @@ __global__ __launch_bounds__(256) void minute_table_kernel(DrawParams dp, StateV
         pa = evd[(size_t)h0 * 4 * n + c];
         pb = h1 < 0 ? st.sa[S_CC][c] : evd[(size_t)h1 * 4 * n + c];
     }
+    return interp(pb, pa, tab64[(size_t)jm * ROW + G_HOURF]);
+}
+
+// The _next_min draws of every (candidate minute boundary, chain) of the window,
+// one work-item each, before the expansion: minute m sits at window step
+// fm + 60 m.  The expansion and the block-start reconstruction read them instead
+// of drawing in their loops.  R = float: the fp32 kernels' copies (float table).
+template <typename R>
+__global__ __launch_bounds__(256) void minute_table_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
+                                                           int64_t W0, uint32_t nsteps, int64_t fm,
+                                                           const double* __restrict__ tab64,
+                                                           const int2* __restrict__ events,
+                                                           const uint32_t* __restrict__ n_events, SegView sg)
+{
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t m = blockIdx.y;
+    const int64_t jm = fm + 60 * (int64_t)m;
+    if (m == 0 && c < n) {   // the expansion's guard-band bookkeeping (this kernel runs just before it)
+        if (c == 0) *sg.nfix = 0;
+        sg.corr[c] = 0.0;
+        sg.corr[(size_t)n + c] = 0.0;
+    }
+    if (c >= n || jm >= (int64_t)nsteps) return;
+    const int ne = (int)min(*n_events, ev_cap_dev(nsteps));
     double cloudy, clear;
-    minute_draws<R>(dp, chain0 + c, step, interp(pb, pa, tab64[(size_t)jm * ROW + G_HOURF]), cloudy, clear);
+    minute_draws<R>(dp, chain0 + c, W0 + jm, minute_cc(st, sg, n, c, W0, jm, events, ne, tab64), cloudy, clear);
     R* t = reinterpret_cast<R*>(sg.mtab);
     t[(size_t)(2 * m) * n + c] = (R)cloudy;
     t[(size_t)(2 * m + 1) * n + c] = (R)clear;
@@ -509,6 +583,7 @@ struct MinuteCtx {
     const double* tab64;
 };
 
+// R = float: the noise pairs are the fp32 copies (the caller starts them from StateView::fn)
 template <typename R>
 __device__ __forceinline__ void samplers_at(const BlockDesc& d, const SegView& sg, uint32_t n, uint32_t c, Samp& s,
                                             const MinuteCtx& mc, const StateView& st)
@@ -537,6 +612,138 @@ __device__ __forceinline__ void samplers_at(const BlockDesc& d, const SegView& s
         s.a[S_CLOUDY_NOISE] = (double)t[(size_t)(2 * d.q0) * n + c];
         s.a[S_CLEAR_NOISE] = (double)t[(size_t)(2 * d.q0 + 1) * n + c];
     }
+}
+
+// the cloud cover in force after descriptor d's step (back = 1: before its last
+// hour push), interpolated at hour fraction hf
+__device__ __forceinline__ double desc_cc(const BlockDesc& d, int back, const StateView& st, const SegView& sg,
+                                          uint32_t n, uint32_t c, double hf)
+{
+    const int h0 = back ? d.h1 : d.h0, h1 = back ? d.h2 : d.h1;
+    double pb, pa;
+    if (h0 < 0) {
+        pb = st.sb[S_CC][c];
+        pa = st.sa[S_CC][c];
+    } else {
+        pa = sg.evd[(size_t)h0 * 4 * n + c];
+        pb = h1 < 0 ? st.sa[S_CC][c] : sg.evd[(size_t)h1 * 4 * n + c];
+    }
+    return interp(pb, pa, hf);
+}
+
+// fp32 mode: the fp64 noise pairs described by `d` (s starts from the state's
+// fp64 pairs): the minute draws of d.q0 / d.q1 computed again in fp64 (the fp32
+// minute table holds the fast copies only).  Every hour event at or before d's
+// step is at or before minute q0 (hour boundaries are minute boundaries), so q0
+// draws with d's cloud-cover pair, q1 with the pair before an hour push at q0.
+__device__ __forceinline__ void exact_noise_at(const BlockDesc& d, const DrawParams& dp, const StateView& st,
+                                               const SegView& sg, uint32_t n, uint32_t c, uint64_t chain0,
+                                               int64_t W0, int64_t fm, const int2* events, const double* tab64,
+                                               Samp& s)
+{
+    if (d.q0 < 0) return;
+    const int64_t jm0 = fm + 60 * (int64_t)d.q0;
+    double cl, cr;
+    if (d.q1 >= 0) {
+        const int64_t jm1 = jm0 - 60;
+        const int back = (d.h0 >= 0 && (int64_t)events[d.h0].x == W0 + jm0) ? 1 : 0;
+        minute_draws<double>(dp, chain0 + c, W0 + jm1, desc_cc(d, back, st, sg, n, c, tab64[(size_t)jm1 * ROW + G_HOURF]),
+                             cl, cr);
+        s.b[S_CLOUDY_NOISE] = cl;
+        s.b[S_CLEAR_NOISE] = cr;
+    } else {
+        s.b[S_CLOUDY_NOISE] = s.a[S_CLOUDY_NOISE];
+        s.b[S_CLEAR_NOISE] = s.a[S_CLEAR_NOISE];
+    }
+    minute_draws<double>(dp, chain0 + c, W0 + jm0, desc_cc(d, 0, st, sg, n, c, tab64[(size_t)jm0 * ROW + G_HOURF]), cl,
+                         cr);
+    s.a[S_CLOUDY_NOISE] = cl;
+    s.a[S_CLEAR_NOISE] = cr;
+}
+
+// the fp32 state's fast noise pairs into a Samp about to be rounded to float
+__device__ __forceinline__ void load_fast_noise(const StateView& st, uint32_t c, Samp& s)
+{
+    const float2 a = st.fn[0][c], b = st.fn[1][c];
+    s.b[S_CLOUDY_NOISE] = a.x;
+    s.a[S_CLOUDY_NOISE] = a.y;
+    s.b[S_CLEAR_NOISE] = b.x;
+    s.a[S_CLEAR_NOISE] = b.y;
+}
+
+// One second of a chain at window step j, rebuilt outside the expansion: the
+// sampler state (window-start state + desc_for(j) over the fp64 draw tables, as
+// a block start does), the covered bit (segment records) and the step's Philox
+// words.  fixup_kernel uses it for the fp32 expansion's guard-band seconds
+// (pv_power_f: DISC's kt = 0.6 split, the inverter's Pso cut-in): `pv32` is the
+// second as the fp32 expansion emitted it (the same fp32 arithmetic on the same
+// values), `pv64` the fp64 kernel's second, whose branch falls as in the fp64
+// reference.
+template <bool SITES>
+__device__ __forceinline__ bool redo_second(const KParams& kp, const DrawParams& dp, const StateView& st,
+                                            const SegView& sg, uint32_t n, uint32_t c, uint64_t chain0, int64_t W0,
+                                            int64_t utc0, uint32_t j, const BlockDesc& db, uint32_t jr_end,
+                                            const int2* events, int ne, const double* tab64, const float* tab32,
+                                            const double* sun, float& pv32, float& meter32, float& pv64)
+{   // returns whether the fp32 second lies in a guard band (then pv64 is set)
+    const int64_t step = W0 + (int64_t)j;
+    const BlockDesc d = desc_advance(db, W0, utc0, events, ne, step);   // db: the block's descriptor
+    Samp s;   // the fp32 kernels' samplers: fast noise copies
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        s.b[k] = st.sb[k][c];
+        s.a[k] = st.sa[k][c];
+    }
+    load_fast_noise(st, c, s);
+    const MinuteCtx mc{};
+    samplers_at<float>(d, sg, n, c, s, mc, st);
+    Samp sx = s;   // the fp64 samplers: the state's fp64 noise pairs + the fp64 minute draws
+    sx.b[S_CLOUDY_NOISE] = st.sb[S_CLOUDY_NOISE][c];
+    sx.a[S_CLOUDY_NOISE] = st.sa[S_CLOUDY_NOISE][c];
+    sx.b[S_CLEAR_NOISE] = st.sb[S_CLEAR_NOISE][c];
+    sx.a[S_CLEAR_NOISE] = st.sa[S_CLEAR_NOISE][c];
+    exact_noise_at(d, dp, st, sg, n, c, chain0, W0, first_minute(utc0, W0), events, tab64, sx);
+    const int2* rec = sg.rec + (size_t)c * sg.cap;   // the segment holding the step: first next-call step > step,
+    uint32_t k = jr_end;                             // at or before the one of the block's last step
+    while (k > 0 && (int64_t)rec[k - 1].y > step) --k;
+    const bool covered = step < (int64_t)rec[k].x;
+    const U4 pb = keyed_block(kp.seed, chain0 + c, (uint64_t)step >> 1, TAG_STEP2, 0);
+    const bool odd = step & 1;
+    LaneSite ls{};
+    if constexpr (SITES) {
+        ls.k = site_k(kp.sites + (size_t)c * 8);
+        ls.linke = kp.site_linke ? kp.site_linke + (size_t)c * 12 : nullptr;
+        ls.tl_doy = -1;
+    }
+    bool risky;
+    {   // fp32, as expand_kernel<float>
+        FSamp<float> f;
+        to_real(f, s);
+        float row[ROW32];
+#pragma unroll
+        for (int i = 0; i < ROW32; ++i) row[i] = tab32[(size_t)j * ROW32 + i];
+        float csi, m, r;
+        const uint32_t fl = __float_as_uint(row[G_FLAGS + G32]) & ~(uint32_t)FL_NIGHT;
+        uint32_t flp = __float_as_uint(row[G_FLAGS + G32]);
+        if constexpr (SITES) flp = lane_row<float>(ls, sun + (size_t)j * SUN_W, kp.module, row) ? (fl | FL_NIGHT) : fl;
+        second_body<float>(kp, kp.pvf, row, flp, f, covered, noise_z<float>(odd ? pb.z : pb.x),
+                           meter_w<float>(odd ? pb.w : pb.y), csi, pv32, m, r, risky);
+        meter32 = m;
+    }
+    if (!risky) return false;
+    {   // fp64, as expand_kernel<double>
+        FSamp<double> f;
+        to_real(f, sx);
+        double row[ROW];
+#pragma unroll
+        for (int i = 0; i < ROW; ++i) row[i] = tab64[(size_t)j * ROW + i];
+        if constexpr (SITES) lane_row<double>(ls, sun + (size_t)j * SUN_W, kp.module, row);
+        double csi, pv, m, r;
+        second_body<double>(kp, kp.pvf, row, 0u, f, covered, noise_z<double>(odd ? pb.z : pb.x), 0.0, csi, pv, m, r,
+                            risky);
+        pv64 = (float)pv;
+    }
+    return true;
 }
 
 // ------------------------------------------------------------ sequential kernel
@@ -572,6 +779,14 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
     double* sl = live ? sig_l(st, c) : nullptr;
     FSamp<R> fs;
     to_real(fs, ch.s);
+    float2 fnc{0.f, 0.f}, fnl{0.f, 0.f};   // fp32: the fast noise pairs (StateView::fn) the fp32 second samples
+    if constexpr (sizeof(R) == 4) {
+        if (live) {
+            fnc = st.fn[0][c];
+            fnl = st.fn[1][c];
+        }
+        set_fast_noise(fs, fnc, fnl);
+    }
     Acc acc{0.0, 0.0, 0.0, -INFINITY};
     LaneSite ls{};   // per-chain sites (tmh_set_sites)
     if (kp.sites) {
@@ -609,8 +824,13 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
                     const double cc = interp(ch.s.b[S_CC], ch.s.a[S_CC], hf);
                     push(ch.s, S_CLOUDY_NOISE, minute_noise<R>(u0, 0.01, 0.003, cc, kp.sqrt09));
                     push(ch.s, S_CLEAR_NOISE, minute_noise<R>(u1, 0.001, 0.0015, cc, kp.sqrt09));
+                    if constexpr (sizeof(R) == 4) {
+                        fnc = make_float2(fnc.y, minute_noise_fast(u0, 0.01, 0.003, cc, kp.sqrt09));
+                        fnl = make_float2(fnl.y, minute_noise_fast(u1, 0.001, 0.0015, cc, kp.sqrt09));
+                    }
                 }
                 to_real(fs, ch.s);
+                if constexpr (sizeof(R) == 4) set_fast_noise(fs, fnc, fnl);
             }
             ch.sec += 1;                                 // CloudCoverBinary.__next__
             while (ch.sec >= ch.t2 && ch.status == 0) {  // segment over: next_cloud(); next(self)
@@ -627,11 +847,15 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
                 const U4 pb = keyed_block(kp.seed, chain, (uint64_t)step >> 1, TAG_STEP2, 0);
                 const bool odd = step & 1;
                 R z = noise_z<R>(odd ? pb.z : pb.x);
+                double z64 = 0.0;   // fp32: the fp64 quantile for the guard-band recomputation
                 const R mtr = meter_w<R>(odd ? pb.w : pb.y);
                 if constexpr (RNG == TMH_RNG_INJECTED) {
                     const double ue = dr.one(ch, step, TAG_STEP, 0, 0);
                     if constexpr (sizeof(R) == 8) z = ndtri(ue);
-                    else z = ndtri_f(ue);
+                    else {
+                        z = ndtri_f(ue);
+                        z64 = ue;   // quantile taken on the rare path only
+                    }
                 }
                 if (ch.status == 0) {
                     const bool covered = ch.sec < ch.t1;
@@ -641,7 +865,23 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
                         const bool night = lane_row<R>(ls, sun + (size_t)j * SUN_W, kp.module, row);
                         flp = night ? (fl | FL_NIGHT) : (fl & ~(uint32_t)FL_NIGHT);
                     }
-                    second_body<R>(kp, kp.pvf, row, flp, fs, covered, z, mtr, csi, pv, meter, res);
+                    bool risky;
+                    second_body<R>(kp, kp.pvf, row, flp, fs, covered, z, mtr, csi, pv, meter, res, risky);
+                    if constexpr (sizeof(R) == 4) {
+                        if (risky) {   // guard band of a PV discontinuity: the fp64 second (pv_fp64_tp)
+                            FSamp<double> f64;
+                            to_real(f64, ch.s);
+                            double row64[ROW];
+                            for (int i = 0; i < ROW; ++i) row64[i] = r64[i];
+                            if (kp.sites) lane_row<double>(ls, sun + (size_t)j * SUN_W, kp.module, row64);
+                            const double zz = RNG == TMH_RNG_INJECTED ? ndtri(z64) : noise_z<double>(odd ? pb.z : pb.x);
+                            double c64, p64, m64, r64s;
+                            bool rk;
+                            second_body<double>(kp, kp.pvf, row64, flp, f64, covered, zz, 0.0, c64, p64, m64, r64s, rk);
+                            pv = (float)p64;
+                            res = meter - pv;
+                        }
+                    }
                     ok = true;
                 }
             }
@@ -650,6 +890,10 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
     }
     if (live) {
         store_chain(st, c, ch);
+        if constexpr (sizeof(R) == 4) {
+            st.fn[0][c] = fnc;
+            st.fn[1][c] = fnl;
+        }
         if (sv.acc) {
             sv.acc[c] += acc.pv;
             sv.acc[(size_t)n + c] += acc.m;
@@ -1134,8 +1378,11 @@ __device__ __forceinline__ void row_store(void* base, size_t row_off, uint32_t l
 // One work-item per (chain, block of 128 seconds).  The boundary draws come
 // from the draw tables, so the per-second loop holds only the R copies of the
 // sampler pairs and does no fp64 work in fp32 mode.
+#ifndef TMH_HELD_LDS
+#define TMH_HELD_LDS 1
+#endif
 #ifndef TMH_PVF_VGPR   // leading PVF fields pinned in VGPRs in the fp32 expansion
-#define TMH_PVF_VGPR 25
+#define TMH_PVF_VGPR 24
 #endif
 #ifndef TMH_ROW_PREFETCH
 #define TMH_ROW_PREFETCH 0
@@ -1207,6 +1454,7 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
             s.b[k] = st.sb[k][c];
             s.a[k] = st.sa[k][c];
         }
+        if constexpr (sizeof(R) == 4) load_fast_noise(st, c, s);
         const BlockDesc d = desc[b];
         evi = (uint32_t)d.evi;
         if (alive && b > 0) samplers_at<R>(d, sg, n, c, s, mc, st);
@@ -1238,6 +1486,12 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
     R row_nx[row_w<R>()];
     load_row(j0, row_nx);
 #endif
+#if TMH_HELD_LDS   // the guard-band seconds of the lane's block, a bit each, in LDS: no register carried through the loop
+    __shared__ uint4 held_lds[256];
+    held_lds[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
+#else
+    bool held_any = false;   // fp32: some second of this block lies in a guard band (pv_power_f)
+#endif
     for (uint32_t j = j0; j < j1; ++j) {
         const int64_t step = W0 + j;
         R row[row_w<R>()];
@@ -1251,6 +1505,7 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
         const uint32_t fl = sizeof(R) == 8 ? (uint32_t)tab64[(size_t)j * ROW + G_FLAGS] : __float_as_uint(row[G_FLAGS + G32]);
         R csi = R(NAN), pv = R(NAN), meter = R(NAN), res = R(NAN);
         uint8_t cov = 255;
+        bool held = false;   // fp32: PV in a guard band, recomputed in fp64 by fixup_kernel
         const bool ok = alive && (int32_t)j < fault;
         if (ok) {
             if (fl & (FL_DAY | FL_HOUR)) {            // _next_day, _next_hour
@@ -1298,12 +1553,22 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
                 flp = night ? (fl | FL_NIGHT) : (fl & ~(uint32_t)FL_NIGHT);
             }
             second_body<R>(kp, pkv, row, flp, fs, covered, noise_z<R>(odd ? pair.z : pair.x), meter_w<R>(odd ? pair.w : pair.y),
-                           csi, pv, meter, res);
+                           csi, pv, meter, res, held);
+            if constexpr (sizeof(R) == 4) {
+#if TMH_HELD_LDS
+                if (held) {   // (j - j0) is wave-uniform: the word and the bit are scalars
+                    uint32_t* hw = reinterpret_cast<uint32_t*>(&held_lds[threadIdx.x]) + ((j - j0) >> 5);
+                    *hw |= 1u << ((j - j0) & 31);
+                }
+#else
+                held_any |= held;   // guard band of a PV discontinuity: fixup_kernel redoes this block's such seconds in fp64
+#endif
+            }
         }
         if (fl & (FL_DAY | FL_HOUR)) ++evi;
 #ifdef TMH_DIAG_NO_STORE
         if (live && csi == R(-12345))
-            emit<R, OUT>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok);
+            emit<R, OUT>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok, held);
 #else
         if constexpr (OUT == OUT_TRACE3) {   // row pointers are wave-uniform: 32-bit lane offsets only
             if (live) {                        // (SGPR row base + zero-extended lane byte offset: no 64-bit VALU adds)
@@ -1314,9 +1579,21 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
                 row_store(tr.residual, ro, lo, res);
             }
         } else if (live) {
-            emit<R, OUT>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok);
+            emit<R, OUT>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok, held);
         }
 #endif
+    }
+    if constexpr (sizeof(R) == 4) {
+#if TMH_HELD_LDS
+        const uint4 hm = held_lds[threadIdx.x];
+        const bool held_any = (hm.x | hm.y | hm.z | hm.w) != 0;
+#else
+        const uint4 hm = make_uint4(~0u, ~0u, ~0u, ~0u);   // every second of the block
+#endif
+        if (held_any) {   // (chain, block, seconds) for fixup_kernel (outside the loop: no registers held across it)
+            const uint32_t k = atomicAdd(sg.nfix, 1u);
+            if (k < sg.fixcap) sg.fix[k] = FixRec{c, b, jr, 0u, hm};
+        }
     }
     if (live && sv.acc) {
         const size_t o = (size_t)b * n + c, stride = (size_t)sg.nblk * n;
@@ -1329,6 +1606,68 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < sv.n_bins; i += blockDim.x)
             if (lds_hist[i]) atomicAdd((unsigned long long*)&sv.hist[i], (unsigned long long)lds_hist[i]);
+    }
+}
+
+// fmax into a double in global memory (compare-and-swap; rare: fixup_kernel only)
+__device__ void atomic_fmax(double* p, double v)
+{
+    unsigned long long* a = reinterpret_cast<unsigned long long*>(p);
+    unsigned long long old = *a;
+    while (v > __longlong_as_double((long long)old)) {
+        const unsigned long long seen = atomicCAS(a, old, (unsigned long long)__double_as_longlong(v));
+        if (seen == old) break;
+        old = seen;
+    }
+}
+
+// The fp32 expansion's guard-band seconds (the blocks FixRec lists), recomputed
+// in fp64 (redo_second) after the expansion and before the commit: the trace's pv and
+// residual are overwritten; the statistics get the exact differences of the
+// sums (fp32 values in fp64 differ exactly, so the corrections add up in any
+// order), the final residual's maximum and histogram count (the expansion left
+// these seconds out of both).  Grid-stride over (record, second of the block).
+template <bool SITES>
+__global__ __launch_bounds__(256) void fixup_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
+                                                    int64_t W0, uint32_t nsteps, int64_t utc0,
+                                                    const double* __restrict__ tab64, const float* __restrict__ tab32,
+                                                    const double* __restrict__ sun,
+                                                    const int2* __restrict__ events,
+                                                    const uint32_t* __restrict__ n_events,
+                                                    const BlockDesc* __restrict__ desc, SegView sg, TraceView tr,
+                                                    StatsView sv)
+{
+    const uint32_t nrec = min(*sg.nfix, sg.fixcap);
+    const int ne = (int)min(*n_events, ev_cap_dev(nsteps));
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < 4 * nrec; t += gridDim.x * blockDim.x) {
+      const FixRec fr = sg.fix[t >> 2];   // four work-items per record, one per 32-second mask word
+      const uint32_t w = t & 3;
+      uint32_t mw = w == 0 ? fr.mask.x : (w == 1 ? fr.mask.y : (w == 2 ? fr.mask.z : fr.mask.w));
+      const uint32_t c = fr.c;
+      const BlockDesc db = desc[fr.b];
+      while (mw) {   // usually one second
+        const uint32_t i = 32 * w + (uint32_t)__builtin_ctz(mw);
+        mw &= mw - 1;
+        const uint32_t j = fr.b * BLOCK_STEPS + i;
+        float pv32, meter, pv;
+        if (!redo_second<SITES>(kp, dp, st, sg, n, c, chain0, W0, utc0, j, db, fr.jr, events, ne, tab64, tab32, sun,
+                                pv32, meter, pv))
+            continue;
+        const float res = meter - pv, res32 = meter - pv32;   // second_body's residual
+        const size_t o = (size_t)j * tr.ld + c;
+        if (tr.pv) reinterpret_cast<float*>(tr.pv)[o] = pv;
+        if (tr.residual) reinterpret_cast<float*>(tr.residual)[o] = res;
+        if (sv.acc) {
+            atomicAdd(&sg.corr[c], (double)pv - (double)pv32);
+            atomicAdd(&sg.corr[(size_t)n + c], (double)res - (double)res32);
+            atomic_fmax(&sg.part[3 * (size_t)sg.nblk * n + (size_t)(j / BLOCK_STEPS) * n + c], (double)res);
+        }
+        if (sv.hist) {
+            const double x = ((double)res - sv.lo) * sv.scale;
+            const int bin = x < 0.0 ? 0 : (x >= (double)(sv.n_bins - 1) ? (int)sv.n_bins - 1 : (int)x);
+            atomicAdd((unsigned long long*)&sv.hist[bin], 1ull);
+        }
+      }
     }
 }
 
@@ -1351,14 +1690,18 @@ __global__ __launch_bounds__(256) void commit_kernel(StateView st, uint32_t n, S
             r += sg.part[2 * stride + o];
             mx = fmax(mx, sg.part[3 * stride + o]);
         }
+        p += sg.corr[c];                 // fixup_kernel's exact corrections
+        r += sg.corr[(size_t)n + c];
         sv.acc[c] += p;
         sv.acc[(size_t)n + c] += m;
         sv.acc[2 * (size_t)n + c] += r;
         sv.acc[3 * (size_t)n + c] = fmax(sv.acc[3 * (size_t)n + c], mx);
     }
     if (st.status[c] != 0) return;
-    st.status[c] = sg.status[c];
-    if (sg.status[c] != 0) return;
+    // records lost (never observed: room for ~100x the measured rate): the batch's
+    // chains are marked, as it is not known whose seconds were not recomputed
+    st.status[c] = *sg.nfix > sg.fixcap ? TMH_CHAIN_GUARD_OVERFLOW : sg.status[c];
+    if (st.status[c] != 0) return;
     Samp sp;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
@@ -1368,7 +1711,20 @@ __global__ __launch_bounds__(256) void commit_kernel(StateView st, uint32_t n, S
     MinuteCtx mc = mc0;
     mc.chain += c;
     mc.ne = (int)min(*n_events, sg.evcap);
-    samplers_at<R>(*desc_end, sg, n, c, sp, mc, st);
+    if constexpr (sizeof(R) == 4) {   // the fast noise copies from the fp32 table, the fp64 pairs drawn again
+        Samp sf = sp;
+        load_fast_noise(st, c, sf);
+        samplers_at<float>(*desc_end, sg, n, c, sf, mc, st);
+        st.fn[0][c] = make_float2((float)sf.b[S_CLOUDY_NOISE], (float)sf.a[S_CLOUDY_NOISE]);
+        st.fn[1][c] = make_float2((float)sf.b[S_CLEAR_NOISE], (float)sf.a[S_CLEAR_NOISE]);
+        exact_noise_at(*desc_end, mc.dp, st, sg, n, c, mc0.chain, mc.W0, mc.fm, mc.events, mc.tab64, sp);
+        for (int k : {S_CC, S_CLEAR_DAY}) {
+            sp.b[k] = sf.b[k];
+            sp.a[k] = sf.a[k];
+        }
+    } else {
+        samplers_at<R>(*desc_end, sg, n, c, sp, mc, st);
+    }
 #pragma unroll
     for (int k = 0; k < 5; ++k) {   // cc, clear_day, cloudy_hour (unchanged), noises
         st.sb[k][c] = sp.b[k];
@@ -1428,7 +1784,8 @@ int hip_check(hipError_t e, const char* what)
 constexpr size_t ALIGN = 256;
 size_t align_up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
-// state field order: sb[6], sa[6], cl, clr, mstate, sec, L, pos, status, ncalls, sigma_cloud, sigma_clear, -, -
+// state field order: sb[6], sa[6], cl, clr, mstate, sec, L, pos, status, ncalls, sigma_cloud, sigma_clear,
+// fn cloudy, fn clear
 void state_layout(uint32_t n, uint64_t* off, size_t* total)
 {
     size_t o = 0;
@@ -1439,6 +1796,7 @@ void state_layout(uint32_t n, uint64_t* off, size_t* total)
         if (f < 15) bytes = d;
         else if (f < 20) bytes = w;
         else if (f < 22) bytes = d * CAP;
+        else bytes = d;   // fn pairs (float2)
         o += align_up(bytes);
     }
     *total = o;
@@ -1465,6 +1823,8 @@ StateView make_view(void* base, uint32_t n)
     v.ncalls = (uint32_t*)(b + off[19]);
     v.sc = (double*)(b + off[20]);
     v.sl = (double*)(b + off[21]);
+    v.fn[0] = (float2*)(b + off[22]);
+    v.fn[1] = (float2*)(b + off[23]);
     v.n = n;
     return v;
 }
@@ -1505,6 +1865,9 @@ size_t plan_layout(uint32_t n_steps, void* base, PlanView* v)
 }
 
 uint32_t seg_cap(uint32_t n_steps) { return n_steps / 8 + 64; }
+// (chain, block)s with a guard-band second of the fp32 PV chain: ~1e-5 of the
+// chain-seconds are such seconds, ~1.3e-3 of the blocks; room for 1/16
+uint32_t fix_cap(uint32_t n, uint32_t n_steps) { return (uint32_t)((uint64_t)n * nblk_of(n_steps) / 16) + 1024; }
 
 size_t scratch_layout(uint32_t n, uint32_t n_steps, void* base, SegView* v)
 {
@@ -1547,6 +1910,16 @@ size_t scratch_layout(uint32_t n, uint32_t n_steps, void* base, SegView* v)
         v->mtab = (void*)(b + o);
     }
     o += align_up((size_t)n * nmin * 2 * 8);
+    const uint32_t fc = fix_cap(n, n_steps);
+    if (v) {
+        v->fixcap = fc;
+        v->fix = (FixRec*)(b + o);
+    }
+    o += align_up((size_t)fc * sizeof(FixRec));
+    if (v) v->nfix = (uint32_t*)(b + o);   // nfix | corr[2][n]: zeroed before each expansion
+    o += ALIGN;
+    if (v) v->corr = (double*)(b + o);
+    o += align_up((size_t)n * 2 * 8);
     return o;
 }
 
@@ -1857,7 +2230,7 @@ int tmh_plan(struct tmh_engine* eng, int64_t step0, uint32_t n_steps, void* plan
     return hip_check(hipGetLastError(), "plan kernels launch");
 }
 
-enum { PH_DRAWS = 1, PH_SEGMENTS = 4, PH_WALK = PH_DRAWS | PH_SEGMENTS, PH_EXPAND = 2, PH_ALL = 7 };
+enum { PH_DRAWS = 1, PH_SEGMENTS = 4, PH_WALK = PH_DRAWS | PH_SEGMENTS, PH_EXPAND = 2, PH_COMMIT = 8, PH_ALL = 15 };
 
 static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, int64_t step0,
                        uint32_t n_steps, const tmh_ustream* inj, const tmh_trace* trace, const tmh_stats* stats,
@@ -1936,11 +2309,15 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     eng->close(TMH_K_SEGMENTS, t_seg, s);
     if (int rc = hip_check(hipGetLastError(), "segments kernel launch")) return rc;
     }
-    if (!(phases & PH_EXPAND)) return TMH_OK;
+    if (phases & PH_EXPAND) {
     hipEvent_t t_exp = eng->mark(s);
     {   // the window's minute draws, one work-item each (read by the expansion and the commit)
         const int64_t fmh = first_minute_host(utc0, step0);
         const uint32_t nm = fmh < (int64_t)n_steps ? (uint32_t)((n_steps - 1 - fmh) / 60 + 1) : 0;
+        if (!nm)   // minute_table_kernel zeroes the guard-band bookkeeping; a window without a minute boundary:
+            if (int rc = hip_check(hipMemsetAsync(sg.nfix, 0, (size_t)((char*)(sg.corr + 2 * (size_t)n_chains) - (char*)sg.nfix), s),
+                                   "hipMemsetAsync"))
+                return rc;
         if (nm) {
             if (f64)
                 hipLaunchKernelGGL(minute_table_kernel<double>, dim3(cb, nm), dim3(256), 0, s, eng->dp, v, chain0,
@@ -1973,6 +2350,18 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
 #undef LAUNCH
     eng->close(TMH_K_EXPAND, t_exp, s);
     if (int rc = hip_check(hipGetLastError(), "expand_kernel launch")) return rc;
+    }
+    if (!(phases & PH_COMMIT)) return TMH_OK;
+    if (!f64 && eng->kp.with_pv) {   // the fp32 guard-band seconds, in fp64
+        const uint32_t gx = 64;   // grid-stride over the (few, ~1e-3 of the blocks) records
+        if (eng->kp.sites)
+            hipLaunchKernelGGL(fixup_kernel<true>, dim3(gx), dim3(256), 0, s, eng->kp, eng->dp, v, chain0, n_chains, step0,
+                               n_steps, utc0, pv.tab64, pv.tab32, pv.sun, pv.events, pv.n_events, pv.desc, sg, tv, sv);
+        else
+            hipLaunchKernelGGL(fixup_kernel<false>, dim3(gx), dim3(256), 0, s, eng->kp, eng->dp, v, chain0, n_chains, step0,
+                               n_steps, utc0, pv.tab64, pv.tab32, pv.sun, pv.events, pv.n_events, pv.desc, sg, tv, sv);
+        if (int rc = hip_check(hipGetLastError(), "fixup_kernel launch")) return rc;
+    }
     const MinuteCtx mc{eng->dp, chain0, step0, first_minute_host(utc0, step0), pv.events, 0, pv.tab64};
     if (f64)
         hipLaunchKernelGGL(commit_kernel<double>, dim3(cb), dim3(256), 0, s, v, n_chains, sg, sv, mc, pv.n_events,
@@ -2021,7 +2410,19 @@ int tmh_expand(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_
                const void* plan, void* scratch, size_t scratch_bytes, void* stream)
 {
     return step_phases(eng, state, chain0, n_chains, step0, n_steps, inj, trace, stats, plan, scratch, scratch_bytes,
-                       stream, PH_EXPAND);
+                       stream, PH_EXPAND | PH_COMMIT);
+}
+
+int tmh_expand_part(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, int64_t step0,
+                    uint32_t n_steps, const tmh_ustream* inj, const tmh_trace* trace, const tmh_stats* stats,
+                    const void* plan, void* scratch, size_t scratch_bytes, int parts, void* stream)
+{
+    if (parts & ~(TMH_EXPAND_KERNEL | TMH_EXPAND_COMMIT)) return fail(TMH_E_INVAL, "bad expand parts %d", parts);
+    if (eng && eng->path != TMH_PATH_TIME_PARALLEL && parts != (TMH_EXPAND_KERNEL | TMH_EXPAND_COMMIT))
+        return fail(TMH_E_INVAL, "tmh_expand_part in parts needs the time-parallel path");
+    const int ph = ((parts & TMH_EXPAND_KERNEL) ? PH_EXPAND : 0) | ((parts & TMH_EXPAND_COMMIT) ? PH_COMMIT : 0);
+    return step_phases(eng, state, chain0, n_chains, step0, n_steps, inj, trace, stats, plan, scratch, scratch_bytes,
+                       stream, ph);
 }
 
 int tmh_run(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, int64_t step0,

@@ -78,6 +78,7 @@ struct StateView {
     int32_t *sec, *L;
     uint32_t *pos, *status, *ncalls;
     double *sc, *sl;
+    float2* fn[2];   // fp32 mode: the (before, after) cloudy / clear noise pairs the fp32 kernels sample (minute_noise_fast)
     uint32_t n;
 };
 
@@ -176,18 +177,23 @@ __device__ __forceinline__ double scaled_noise(const KParams& kp, double u, doub
 }
 
 // _next_min noise draw (clearskyindexmodel.py:86-88, 109-111): the reference's
-// fp64 formula in fp64 mode; in fp32 mode the quantile and the affine map run in
-// fp32 (the scale is formed in fp64 and rounded), the value is kept exactly as a
-// double.  Shared by every kernel path so the paths agree bit for bit.
+// fp64 formula.  Shared by every kernel path so the paths agree bit for bit.
+// fp64 mode samples it; fp32 mode keeps it in the state's sampler pairs (the
+// rare fp64 recomputation of a second, redo_second, needs these values) and
+// samples minute_noise_fast.
 template <typename R>
 __device__ __forceinline__ double minute_noise(double u, double s0, double s1, double cc, double sqrt09)
 {
-    if constexpr (sizeof(R) == 8) {
-        return normal(u, 1.0, sqrt09 * (s0 + s1 * 8 * cc));
-    } else {
-        const float sc = (float)(sqrt09 * (s0 + s1 * 8 * cc));
-        return (double)(ndtri_f(u) * sc + 1.0f);
-    }
+    return normal(u, 1.0, sqrt09 * (s0 + s1 * 8 * cc));
+}
+
+// the fp32 path's copy of the same draw: the quantile and the affine map in fp32
+// (the scale formed in fp64 and rounded); the state's fn pairs and the fp32
+// minute table hold these
+__device__ __forceinline__ float minute_noise_fast(double u, double s0, double s1, double cc, double sqrt09)
+{
+    const float sc = (float)(sqrt09 * (s0 + s1 * 8 * cc));
+    return ndtri_f(u) * sc + 1.0f;
 }
 
 // hourly cloud cover: next(get_cloud_cover(distributions)) (cloud_cover_hourly.py:309-316);
@@ -894,8 +900,10 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     return g[G_GHICS] == 0.0;
 }
 
+constexpr double LOG2E = 1.44269504088896340736;   // the fp32 row's airmass is am log2 e (pv_power_f)
+
 // the kernels' row of one chain's own site (fp32 rows carry the reciprocals
-// of I0h and dni_extra, like geom_kernel's fp32 table)
+// of I0h and dni_extra and the airmass times log2 e, like geom_kernel's fp32 table)
 template <typename R>
 __device__ __forceinline__ void site_row(const double* g, const double* sun, R* row_base)
 {
@@ -905,6 +913,7 @@ __device__ __forceinline__ void site_row(const double* g, const double* sun, R* 
     if constexpr (sizeof(R) == 4) {
         row[G_I0H] = (float)(1.0 / g[G_I0H]);
         row[G_DNIEXTRA] = (float)sun[SUN_RDNIX];
+        row[G_AM] = (float)(g[G_AM] * LOG2E);
     }
 }
 
@@ -1016,20 +1025,61 @@ __device__ __forceinline__ R pv_power(const KParams& kp, const R* g, R csi)
 }
 
 
-// fp32 PV chain: the same model as pv_power<float>, with fused multiply-adds,
+// DISC's Kn polynomials (pvlib irradiance.disc, pvmodel.py:63) re-expanded
+// about kt = 0.6f: p(kt) = sum_k d_k t^k with t = kt - 0.6f (exact in fp32 for
+// kt in [0.3, 1.2], Sterbenz).  In the literal form the high set's terms reach
+// ~30 around kt = 0.6 where a(kt) is ~0.08: fp32 Horner then loses ~9 bits and
+// the PV error reaches 4e-5 at airmass 3-4; the shifted coefficients stay of
+// the size of the result there (same FMA count).  d_k = sum_{i>=k} C(i,k) c_i x0^(i-k),
+// evaluated in fp64 at compile time and rounded once.
+struct Cubic {
+    double c0, c1, c2, c3;
+};
+constexpr double DISC_X0 = (double)0.6f;
+constexpr float disc_shift(const Cubic& p, int k)
+{
+    const double x = DISC_X0;
+    return (float)(k == 0   ? ((p.c3 * x + p.c2) * x + p.c1) * x + p.c0
+                   : k == 1 ? (3.0 * p.c3 * x + 2.0 * p.c2) * x + p.c1
+                   : k == 2 ? 3.0 * p.c3 * x + p.c2
+                            : p.c3);
+}
+constexpr Cubic DISC_A_LO{0.512, -1.56, 2.286, -2.222}, DISC_A_HI{-5.743, 21.77, -27.49, 11.56};
+constexpr Cubic DISC_B_LO{0.37, 0.962, 0.0, 0.0}, DISC_B_HI{41.4, -118.5, 66.05, 31.9};
+constexpr Cubic DISC_C_LO{-0.28, 0.932, -2.048, 0.0}, DISC_C_HI{-47.01, 184.2, -222.0, 73.81};
+
+template <int DEG>   // Horner over the shifted coefficients d_DEG .. d_0
+__device__ __forceinline__ float disc_poly(const Cubic& p, float t)
+{
+    float v = disc_shift(p, DEG);
+#pragma unroll
+    for (int k = DEG - 1; k >= 0; --k) v = fmaf(v, t, disc_shift(p, k));
+    return v;
+}
+
+// Guard band of the fp32 chain's two discontinuities (DISC's kt = 0.6 split and
+// the inverter's p_dc < Pso cut-in): a second whose fp32 kt or p_dc lies this
+// close to its threshold may have fallen on the other side than the fp64
+// reference, and is recomputed in fp64 (pv_fp64_*).  The fp32 kt differs from
+// the fp64 one by < 4e-7 (csi <= 4.5e-7 relative, measured over 4e7 points, plus
+// three roundings), p_dc by < 1e-5 relative.
+constexpr float KT_GUARD = 4e-6f, PDC_GUARD = 1e-4f;
+
+// fp32 PV chain: the model of pv_power<double>, with fused multiply-adds,
 // fp32 constants rounded once on the host (KParams::pvf) and the hardware
-// exp / log; within the fp32 tolerance of the fp64 oracle
-__device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float csi)
+// exp / log; within 1e-5 of the fp64 oracle.  `risky`: the second
+// lies in a guard band and must be recomputed in fp64.
+__device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float csi, bool& risky)
 {
     const float c = fminf(csi, g[G_CSIMAX]);
     const float ghi = c * g[G_GHICS];
     const float kt = fminf(fmaxf(ghi * g[G_I0H], 0.0f), 1.0f);
-    // DISC Kn (pvlib irradiance.disc): coefficient sets split at kt = 0.6
-    // (the model's literal coefficients: compile-time constants, no SGPRs)
-    // Both sets are evaluated (one literal FMA per Horner step) and the results
-    // selected: cheaper than selecting twelve coefficient pairs per lane, and bit
-    // for bit the same (the low set's zero leading terms drop out exactly, kt >= 0).
+    // DISC Kn: coefficient sets split at kt = 0.6 (compile-time constants, no
+    // SGPRs).  Both sets are evaluated and the results selected: cheaper than
+    // selecting twelve coefficient pairs per lane.
     const bool lo = kt <= 0.6f;
+    const float t = kt - 0.6f;
+#ifdef TMH_DIAG_LITERAL_DISC   // diagnostic builds only: the literal (unshifted) coefficients
     const float a_lo = fmaf(fmaf(fmaf(-2.222f, kt, 2.286f), kt, -1.56f), kt, 0.512f);
     const float a_hi = fmaf(fmaf(fmaf(11.56f, kt, -27.49f), kt, 21.77f), kt, -5.743f);
     const float b_lo = fmaf(0.962f, kt, 0.37f);
@@ -1037,7 +1087,13 @@ __device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float 
     const float c_lo = fmaf(fmaf(-2.048f, kt, 0.932f), kt, -0.28f);
     const float c_hi = fmaf(fmaf(fmaf(73.81f, kt, -222.0f), kt, 184.2f), kt, -47.01f);
     const float a = lo ? a_lo : a_hi, b = lo ? b_lo : b_hi, cc = lo ? c_lo : c_hi;
-    const float dkn = fmaf(b, __builtin_amdgcn_exp2f(cc * g[G_AM] * 1.44269504088896341f), a);
+#else
+    const float a = lo ? disc_poly<3>(DISC_A_LO, t) : disc_poly<3>(DISC_A_HI, t);
+    const float b = lo ? disc_poly<1>(DISC_B_LO, t) : disc_poly<3>(DISC_B_HI, t);
+    const float cc = lo ? disc_poly<2>(DISC_C_LO, t) : disc_poly<3>(DISC_C_HI, t);
+#endif
+    // exp(cc am) = exp2(cc * (am log2 e)): the fp32 row holds am log2 e (one rounding)
+    const float dkn = fmaf(b, __builtin_amdgcn_exp2f(cc * g[G_AM]), a);
     float dni = (g[G_KNC] - dkn) * g[G_I0];
     dni = (g[G_DISCOK] != 0.0f && ghi >= 0.0f && dni >= 0.0f) ? dni : 0.0f;
     const float dhi = fmaf(-dni, g[G_COSZ], ghi);
@@ -1064,6 +1120,11 @@ __device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float 
     const float C = k.ic0 * fmaf(k.ic3, dv, 1.0f);
     const float AmB = A - B, pmB = pdc - B;
     const float ac = fmaf(C, pmB * pmB, fmaf(-C, AmB, k.paco * __builtin_amdgcn_rcpf(AmB)) * pmB);
+#ifdef TMH_DIAG_NO_GUARD   // diagnostic builds only: cost of the guard band
+    risky = false;
+#else
+    risky = fabsf(t) < KT_GUARD || fabsf(pdc - k.pso) < PDC_GUARD * k.pso;
+#endif
     // min(ac, Paco) unless NaN, -|Pnt| below the cut-in, .fillna(0), .clip(lower=0):
     // -|Pnt| <= 0 clips to 0 and a NaN fills to 0; the rest is one med3 into [0, Paco]
     return (pdc < k.pso || isnan(ac)) ? 0.0f : __builtin_amdgcn_fmed3f(ac, 0.0f, k.pacoc);
@@ -1083,6 +1144,16 @@ __device__ __forceinline__ void to_real(FSamp<R>& f, const Samp& s)
         f.b[k] = (R)s.b[k];
         f.a[k] = (R)s.a[k];
     }
+}
+
+// fp32: the noise samplers hold the fast draws (minute_noise_fast), not the state's fp64 ones
+template <typename R>
+__device__ __forceinline__ void set_fast_noise(FSamp<R>& f, float2 cloudy, float2 clear)
+{
+    f.b[S_CLOUDY_NOISE] = cloudy.x;
+    f.a[S_CLOUDY_NOISE] = cloudy.y;
+    f.b[S_CLEAR_NOISE] = clear.x;
+    f.a[S_CLEAR_NOISE] = clear.y;
 }
 
 template <typename R>
@@ -1127,11 +1198,14 @@ __device__ __forceinline__ R meter_w(uint32_t w)
     else return fminf(fmaf((float)w, 9000.0f * 0x1p-32f, 9000.0f * 0x1p-33f), 8999.9990234375f);   // largest float < 9000
 }
 
+// risky (fp32 only): pv lies in pv_power_f's guard band; the caller recomputes
+// the second in fp64 (pv_fp64_*) and replaces pv and res
 template <typename R>
 __device__ __forceinline__ void second_body(const KParams& kp, const PVF& pk, const R* row, uint32_t fl,
                                             const FSamp<R>& fs, bool covered, R z, R meter_in, R& csi, R& pv, R& meter,
-                                            R& res)
+                                            R& res, bool& risky)
 {
+    risky = false;
     const R cloudcover = rinterp_row(fs, S_CC, row, G_HOURF);   // == interp() bit for bit when R = double
     R eps;
     if constexpr (sizeof(R) == 8) eps = z * (R(kp.sqrt6) * (R(0.001) + R(0.0015 * 8) * cloudcover)) + R(0);
@@ -1145,7 +1219,7 @@ __device__ __forceinline__ void second_body(const KParams& kp, const PVF& pk, co
     pv = csi * row[G_GHICS + row_off<R>()];
 #else
     if constexpr (sizeof(R) == 8) pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power<R>(kp, row, csi) : R(0);
-    else pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power_f(pk, row + G32, csi) : 0.0f;
+    else pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power_f(pk, row + G32, csi, risky) : 0.0f;
 #endif
     meter = meter_in;
     res = meter - pv;
@@ -1170,9 +1244,12 @@ enum : int {
     OUT_STATS = 2     // statistics only, no trace
 };
 
+// held: a guard-band second whose pv / residual fixup_kernel replaces; it enters
+// the sums here (fixup_kernel adds the exact difference) but not the maximum or
+// the histogram (fixup_kernel adds its final value)
 template <typename R, int OUT = OUT_ANY>
 __device__ __forceinline__ void emit(const TraceView& tr, const StatsView& sv, uint32_t* lds_hist, uint64_t o,
-                                     uint8_t cov, R csi, R pv, R meter, R res, Acc& acc, bool ok)
+                                     uint8_t cov, R csi, R pv, R meter, R res, Acc& acc, bool ok, bool held = false)
 {
     if constexpr (OUT == OUT_TRACE3) {
         __builtin_nontemporal_store(pv, reinterpret_cast<R*>(tr.pv) + o);
@@ -1192,9 +1269,9 @@ __device__ __forceinline__ void emit(const TraceView& tr, const StatsView& sv, u
             acc.pv += (double)pv;
             acc.m += (double)meter;
             acc.r += (double)res;
-            acc.mx = fmax(acc.mx, (double)res);
+            if (!held) acc.mx = fmax(acc.mx, (double)res);
         }
-        if (sv.hist) {
+        if (sv.hist && !held) {
             const double x = ((double)res - sv.lo) * sv.scale;
             const int bin = x < 0.0 ? 0 : (x >= (double)(sv.n_bins - 1) ? (int)sv.n_bins - 1 : (int)x);
             atomicAdd(&lds_hist[bin], 1u);

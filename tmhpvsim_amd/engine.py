@@ -138,9 +138,10 @@ class BatchedSim:
         """Device view of one SoA state field ([n], or [n, TMH_SIGMA_CAP] for the sigma arrays)."""
         torch = _torch()
         i = _lib.STATE_FIELDS.index(name)
-        dt = {np.float64: torch.float64, np.int32: torch.int32, np.uint32: torch.int32}[_lib.STATE_DTYPES[name]]
+        dt = {np.float64: torch.float64, np.int32: torch.int32, np.uint32: torch.int32,
+              np.float32: torch.float32}[_lib.STATE_DTYPES[name]]
         esz = 8 if dt == torch.float64 else 4
-        rows = _lib.TMH_SIGMA_CAP if name.startswith("sigma_c") else 1
+        rows = _lib.TMH_SIGMA_CAP if name.startswith("sigma_c") else (2 if name.startswith("fn_") else 1)
         o = int(self._offsets[i])
         v = self.state[o:o + esz * self.n * rows].view(dt)
         return v.view(self.n, rows) if rows > 1 else v
