@@ -154,6 +154,12 @@ size_t tmh_workspace_bytes(uint32_t n_chains, uint32_t n_steps);
 int tmh_engine_create(const tmh_params* params, const tmh_clock* clock, int device,
                       struct tmh_engine** out);
 int tmh_engine_destroy(struct tmh_engine* eng);
+/* Replace the engine's wall clock for later plans (a rolling DST table: the
+ * shift table holds 8 changes, so open-ended runs roll it forward).  Steps keep
+ * their numbering (same utc0); the new clock must describe every step still to
+ * be run plus the one before the first (boundary detection compares with it).
+ * tmh_init keeps using the step-0 time of the creation clock. */
+int tmh_set_clock(struct tmh_engine* eng, const tmh_clock* clock);
 /* the kernel path the engine resolved (TMH_PATH_SEQUENTIAL or TMH_PATH_TIME_PARALLEL) */
 int tmh_engine_path(const struct tmh_engine* eng);
 

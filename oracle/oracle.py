@@ -59,6 +59,8 @@ def lib():
                               p, p, p, p, p, p, p, p]
         L.orc_set_tables.argtypes = [p, p, C.c_uint32]
         L.orc_set_sites.argtypes = [p, p, C.c_uint32]
+        L.orc_injected_streams.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, p, C.c_int]
+        L.orc_set_stats.argtypes = [p, p, p, C.c_uint32, C.c_double, C.c_double, C.c_double]
         _lib = L
     return _lib
 
@@ -107,12 +109,15 @@ def _ptr(a):
 
 
 def run(mp, chain0, n_chains, n_steps, start, tz=None, inj=None, n_threads=1,
-        outputs=("csi", "covered", "pv", "meter", "residual", "pos"), tables=None, sites=None):
+        outputs=("csi", "covered", "pv", "meter", "residual", "pos"), tables=None, sites=None, stats=None):
     """Run the oracle; returns dict of time-major [n_steps, n_chains] arrays + status/init.
 
     tables: optional per-chain shape tables (shapes [n_chains, 6, 4] float64,
     is_t [n_chains, 6] int32); chain c draws its hourly cloud cover from row c.
-    sites: optional per-chain PV sites [n_chains, 8] (or (sites, linke [n_chains, 12]))."""
+    sites: optional per-chain PV sites [n_chains, 8] (or (sites, linke [n_chains, 12])).
+    stats: optional dict(n_bins, lo, hi, amb_eps): per-chain statistics of the good
+    seconds as the GPU's stats mode keeps them -> res["acc"] [n, 4] (sum pv, sum
+    meter, sum residual, max residual), res["hist"] [n, n_bins], res["amb"] [n]."""
     P = make_params(mp, n_threads)
     cal, utc = calendar(start, n_steps, tz)
     out = {}
@@ -140,6 +145,12 @@ def run(mp, chain0, n_chains, n_steps, start, tz=None, inj=None, n_threads=1,
             sli = np.ascontiguousarray(sli, dtype=np.float64)
             assert sli.shape == (n_chains, 12)
         lib().orc_set_sites(_ptr(ssi), _ptr(sli), n_chains)
+    if stats is not None:
+        acc = np.zeros((n_chains, 4))
+        hist = np.zeros((n_chains, int(stats["n_bins"])), dtype=np.uint64)
+        amb = np.zeros(n_chains, dtype=np.uint64)
+        lib().orc_set_stats(_ptr(acc), _ptr(hist), _ptr(amb), int(stats["n_bins"]), float(stats["lo"]),
+                            float(stats["hi"]), float(stats.get("amb_eps", 0.0)))
     try:
         rc = lib().orc_run(C.byref(P), chain0, n_chains, n_steps, _ptr(cal), _ptr(utc), _ptr(inj), stride,
                            _ptr(out["csi"]), _ptr(out["covered"]), _ptr(out["pv"]), _ptr(out["meter"]),
@@ -149,11 +160,22 @@ def run(mp, chain0, n_chains, n_steps, start, tz=None, inj=None, n_threads=1,
             lib().orc_set_tables(None, None, 0)
         if sites is not None:
             lib().orc_set_sites(None, None, 0)
+        if stats is not None:
+            lib().orc_set_stats(None, None, None, 0, 0.0, 1.0, 0.0)
     if rc != 0:
         raise RuntimeError(f"orc_run failed: {rc}")
     res = {k: v for k, v in out.items() if v is not None}
     res["status"], res["init"] = status, init
+    if stats is not None:
+        res["acc"], res["hist"], res["amb"] = acc, hist, amb
     return res
+
+
+def injected_streams(seed, chain0, n_chains, length, n_threads=16):
+    """[n_chains, length] injected uniforms (philox.injected_stream of chains chain0..), in C."""
+    out = np.empty((n_chains, length), dtype=np.float64)
+    lib().orc_injected_streams(int(seed), int(chain0), int(n_chains), int(length), _ptr(out), int(n_threads))
+    return out
 
 
 def ndtri(u):

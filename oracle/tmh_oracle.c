@@ -91,6 +91,24 @@ static double u52(uint32_t lo, uint32_t hi)
     return (double)((v >> 11) | 1ull) * 0x1p-53;
 }
 
+/* injected uniform streams (oracle/philox.py injected_stream, key = (seed, chain),
+ * counter = block number, two 53-bit uniforms per block): out[c * len + k] */
+void orc_injected_streams(uint64_t seed, uint64_t chain0, uint32_t n_chains, uint32_t len, double* out, int n_threads)
+{
+#pragma omp parallel for schedule(static) num_threads(n_threads > 0 ? n_threads : 1)
+    for (uint32_t c = 0; c < n_chains; ++c) {
+        const uint32_t k[2] = {(uint32_t)seed, (uint32_t)(chain0 + c)};
+        double* o = out + (size_t)c * len;
+        for (uint32_t b = 0; 2 * b < len; ++b) {
+            const uint32_t ctr[4] = {b, 0u, 0u, 0u};
+            uint32_t r[4];
+            philox4x32_10(ctr, k, r);
+            o[2 * b] = u52(r[0], r[1]);
+            if (2 * b + 1 < len) o[2 * b + 1] = u52(r[2], r[3]);
+        }
+    }
+}
+
 void orc_philox(const uint32_t* ctr, const uint32_t* key, uint32_t* out)
 {
     philox4x32_10(ctr, key, out);
@@ -724,6 +742,45 @@ void orc_set_sites(const double* sites /* [n][8] */, const double* linke /* [n][
     g_sites_n = n;
 }
 
+/* optional on-host statistics of orc_run (the GPU's stats mode, tmh_stats): per
+ * chain c: acc[c][4] = sum pv, sum meter, sum residual (W s), max residual over
+ * its good seconds; hist[c][n_bins] its residual histogram (edge bins absorb
+ * out-of-range, bin = floor((r - lo) n_bins / (hi - lo))); amb[c] the seconds
+ * whose bin coordinate lies within amb_eps of a bin edge (a tolerance-sized
+ * error may move them) */
+static double* g_acc;
+static uint64_t* g_hist;
+static uint64_t* g_amb;
+static uint32_t g_nbins;
+static double g_lo, g_scale, g_amb_eps;
+
+void orc_set_stats(double* acc, uint64_t* hist, uint64_t* amb, uint32_t n_bins, double lo, double hi, double amb_eps)
+{
+    g_acc = acc;
+    g_hist = hist;
+    g_amb = amb;
+    g_nbins = n_bins;
+    g_lo = lo;
+    g_scale = hist ? n_bins / (hi - lo) : 0.0;
+    g_amb_eps = amb_eps;
+}
+
+static void stats_add(uint32_t c, double pv, double meter, double res)
+{
+    double* a = g_acc + 4 * (size_t)c;
+    a[0] += pv;
+    a[1] += meter;
+    a[2] += res;
+    a[3] = a[3] > res ? a[3] : res;
+    if (g_hist) {
+        const double x = (res - g_lo) * g_scale;
+        const int bin = x < 0.0 ? 0 : (x >= (double)(g_nbins - 1) ? (int)g_nbins - 1 : (int)x);
+        g_hist[(size_t)c * g_nbins + bin] += 1;
+        const double fr = x - floor(x);
+        if (g_amb && x > 0.0 && x < (double)(g_nbins - 1) && (fr < g_amb_eps || fr > 1.0 - g_amb_eps)) g_amb[c] += 1;
+    }
+}
+
 /* -------------------------------------------------------------------- run */
 /* cal: n_steps x 6 int32 = (day of month, hour, minute, second, day of year, leap) local fields.
  * Outputs time-major [step][chain]; any pointer may be NULL.
@@ -769,6 +826,11 @@ int orc_run(const orc_params* P, uint64_t chain0, uint32_t n_chains, uint32_t n_
             ch->tab_t = g_tab_t + 6 * (size_t)c;
         }
         if (inj) { ch->inj = inj + (uint64_t)c * inj_stride; ch->inj_len = inj_stride; }
+        if (g_acc) {
+            double* a = g_acc + 4 * (size_t)c;
+            a[0] = a[1] = a[2] = 0.0;
+            a[3] = -INFINITY;
+        }
         fields_t t0 = {cal[0], cal[1], cal[2], cal[3]};
         chain_init(&X, ch, &t0);
         if (init_out) {
@@ -843,6 +905,7 @@ int orc_run(const orc_params* P, uint64_t chain0, uint32_t n_chains, uint32_t n_
             if (pv_out) pv_out[o] = pv;
             if (meter_out) meter_out[o] = meter;
             if (resid_out) resid_out[o] = meter - pv;
+            if (g_acc && !ch->status) stats_add(c, pv, meter, meter - pv);
         }
         if (status_out) status_out[c] = (uint8_t)ch->status;
         free(ch);

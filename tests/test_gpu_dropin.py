@@ -1,0 +1,106 @@
+"""The drop-in classes (tmhpvsim_amd.ClearskyindexModel / PVModel) on the GPU:
+the reference's own tests restated through them (tests/test_clearskyindexmodel.py:7-13,
+tests/test_pvmodel.py:6-10), a PVModel streamed for a day from now(), a DST
+fall-back day driven with tz-aware times as pvmodel.py:45-48 does, and both
+classes against the C oracle on the same keyed chain (fp64, 1e-12)."""
+import datetime
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from oracle import oracle as O
+from tmhpvsim_amd.params import ModelParams
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def test_reference_clearskyindexmodel_test():
+    """tests/test_clearskyindexmodel.py:7-13: 25 h at 1 s from 2019-09-05 12:00 (naive), 0 < csi < 2."""
+    from tmhpvsim_amd import ClearskyindexModel
+    t0 = datetime.datetime(2019, 9, 5, 12)
+    m = ClearskyindexModel(t0, seed=7)
+    csi = np.array([m.next(t0 + datetime.timedelta(seconds=s)) for s in range(25 * 3600 + 1)])
+    assert ((csi > 0) & (csi < 2)).all()
+    assert m.time.time == t0 + datetime.timedelta(seconds=25 * 3600)
+
+
+def test_reference_pvmodel_test():
+    """tests/test_pvmodel.py:6-10: one day at 1 s, generation >= 0."""
+    from tmhpvsim_amd import PVModel
+    t0 = datetime.datetime(2019, 9, 6)
+    m = PVModel(t0, seed=5)
+    pv = np.array([m.next(t0 + datetime.timedelta(seconds=s)) for s in range(86400)])
+    assert (pv >= 0).all() and pv.max() > 0
+    noon = pv[12 * 3600:12 * 3600 + 600]
+    assert 10.0 < noon.mean() < 250.0            # README.rst:95-100: ~157-174 W around noon
+
+
+def test_pvmodel_default_time_streams_a_day():
+    """PVModel() (time = now, pvmodel.py:32-33) constructs and streams 86,400 s (Europe/Berlin),
+    whatever DST changes lie ahead of now."""
+    from tmhpvsim_amd import PVModel
+    m = PVModel()
+    t0 = m._t0
+    times = pd.date_range(t0, periods=86400, freq="s")
+    pv = np.array([m.next(t) for t in times])
+    assert np.isfinite(pv).all() and (pv >= 0).all()
+
+
+@pytest.mark.parametrize("prec", ["fp64", "fp32"])
+def test_clearskyindexmodel_dst_fall_back_vs_oracle(prec):
+    """The fall-back day (2019-10-27, Europe/Berlin) driven with tz-aware local times as
+    PVModel.populate_cache does (pvmodel.py:45-48): the repeated local hour triggers no
+    _next_hour (clearskyindexmodel.py:123); the chain equals the oracle's keyed chain 0."""
+    from tmhpvsim_amd import ClearskyindexModel
+    times = pd.date_range("2019-10-27 00:00:00", periods=30 * 3600, freq="s", tz="Europe/Berlin").to_pydatetime()
+    m = ClearskyindexModel(times[0], seed=0x5EED, precision=prec)
+    csi = np.array([m.next(t) for t in times])
+    ref = O.run(ModelParams(seed=0x5EED, with_pv=False), 0, 1, len(times), "2019-10-27 00:00:00", tz="Europe/Berlin",
+                outputs=("csi",))
+    tol = 1e-12 if prec == "fp64" else 1e-5
+    np.testing.assert_allclose(csi, ref["csi"][:, 0], rtol=tol)
+
+
+def test_pvmodel_vs_oracle_and_lookahead():
+    """PVModel.next on a day with naive times (read as Europe/Berlin, pvmodel.py:83) equals the
+    oracle's keyed chain 0 (fp64, 1e-12); a second read of a second in the current look-ahead
+    block is allowed, one before it raises KeyError."""
+    from tmhpvsim_amd import PVModel
+    t0 = datetime.datetime(2019, 6, 21, 3)
+    m = PVModel(t0, seed=0xABC)
+    n = 20000
+    pv = np.array([m.next(t0 + datetime.timedelta(seconds=s)) for s in range(n)])
+    ref = O.run(ModelParams(seed=0xABC), 0, 1, n, "2019-06-21 03:00:00", tz="Europe/Berlin", outputs=("pv",))
+    err = np.abs(pv - ref["pv"][:, 0]) / np.maximum(np.abs(ref["pv"][:, 0]), 1.0)
+    assert err.max() <= 1e-12
+    assert m.next(t0 + datetime.timedelta(seconds=n - 1)) == pv[-1]
+    with pytest.raises(KeyError):
+        m.next(t0)
+
+
+def test_clearskyindexmodel_consecutive_seconds_enforced():
+    from tmhpvsim_amd import ClearskyindexModel
+    t0 = datetime.datetime(2019, 9, 5, 12)
+    m = ClearskyindexModel(t0, seed=1)
+    m.next(t0)
+    with pytest.raises(ValueError):
+        m.next(t0 + datetime.timedelta(seconds=5))
+
+
+def test_batched_sim_rolls_its_clock_past_the_horizon():
+    """A BatchedSim run past its horizon installs the next rolling clock (tmh_set_clock): 3 days
+    in 1-day pieces with a 1-day horizon, across the 2019 fall-back, equal one 3-day run."""
+    from tmhpvsim_amd.engine import BatchedSim
+    start = "2019-10-26 00:00:00"
+    a = BatchedSim(64, start, tz="Europe/Berlin", precision="fp32", device="cuda:0", horizon=86400)
+    b = BatchedSim(64, start, tz="Europe/Berlin", precision="fp32", device="cuda:0", horizon=4 * 86400)
+    ra = [a.run(86400, trace=("csi", "pv", "covered")) for _ in range(3)]
+    rb = b.run(3 * 86400, trace=("csi", "pv", "covered"))
+    for f in ("csi", "pv", "covered"):
+        x, y = torch.cat([r[f] for r in ra]), rb[f]
+        if f != "covered":
+            x, y = torch.nan_to_num(x, nan=-1.0), torch.nan_to_num(y, nan=-1.0)
+        assert torch.equal(x, y), f
+    assert a.clock.step0 == 2 * 86400

@@ -5,7 +5,9 @@ Bars (DESIGN.md "Parity"):
   * discrete Markov state (covered bit, uniforms consumed, fault status): bit-exact;
   * fp64 kernel: every continuous output within 1e-12 relative (PV / residual
     relative to max(|ref|, 1 W));
-  * fp32 kernel: within 1e-5 relative (same floor);
+  * fp32 kernel: within 1e-5 relative (same floor), pointwise, no outlier allowance
+    (the seconds in a guard band of the PV chain's discontinuities are recomputed
+    in fp64 by fixup_kernel);
   * reference fixtures (injected uniforms): CSI within 1e-12 relative.
 """
 import numpy as np
@@ -114,12 +116,7 @@ def test_keyed_vs_oracle(start, tz, steps, variant, prec):
     for f in ("csi", "pv", "meter", "residual"):
         assert np.array_equal(np.isnan(_np(out[f])), np.isnan(ref[f])), f
         err = _err(f, got, rf)
-        if prec == "fp32" and f in ("pv", "residual"):
-            # fp32 may flip the DISC kt <= 0.6 branch or the inverter p_dc < Pso cut on a
-            # handful of seconds; allow <= 1e-5 of points past tol, none past 1e-2 W/W
-            assert (err > tol).mean() <= 1e-5 and err.max() <= 1e-2, (f, _where(err, tol))
-        else:
-            assert err.max() <= tol, (f, _where(err, tol), got["pv"][np.unravel_index(np.argmax(err), err.shape)])
+        assert err.max() <= tol, (f, _where(err, tol), got["pv"][np.unravel_index(np.argmax(err), err.shape)])
 
 
 @pytest.mark.parametrize("path", ["sequential", "time_parallel"])
@@ -172,7 +169,7 @@ def _ptr_of(t):
     return C.c_void_p(t.data_ptr())
 
 
-def _check_vs_oracle(out, ref, prec, outlier_frac=1e-5):
+def _check_vs_oracle(out, ref, prec):
     np.testing.assert_array_equal(_np(out["covered"]), ref["covered"])
     ok = ref["status"] == 0
     tol = 1e-12 if prec == "fp64" else 1e-5
@@ -181,10 +178,7 @@ def _check_vs_oracle(out, ref, prec, outlier_frac=1e-5):
     for f in ("csi", "pv", "meter", "residual"):
         assert np.array_equal(np.isnan(_np(out[f])), np.isnan(ref[f])), f
         err = _err(f, got, rf)
-        if prec == "fp32" and f in ("pv", "residual"):   # see test_keyed_vs_oracle
-            assert (err > tol).mean() <= outlier_frac and err.max() <= 1e-2, (f, _where(err, tol))
-        else:
-            assert err.max() <= tol, (f, _where(err, tol))
+        assert err.max() <= tol, (f, _where(err, tol))
 
 
 @pytest.mark.parametrize("path,prec,linke", [("time_parallel", "fp64", False), ("time_parallel", "fp32", True),
@@ -203,9 +197,7 @@ def test_site_grid_vs_oracle(path, prec, linke):
     sim = _sim(n, start, tz="Europe/Berlin", mp=mp, prec=prec, horizon=steps, kernel_path=path, sites=(sites, lk))
     out = sim.run(steps, window=5000)
     np.testing.assert_array_equal(sim.status(), ref["status"])
-    # fp32: DISC at low sun (airmass 5-12, kt > 0.6) amplifies the fp32 rounding of the csi
-    # itself ~100x (d ln pv / d ln csi); on this grid ~1e-5 of the points land in 1e-5..3e-5
-    _check_vs_oracle(out, ref, prec, outlier_frac=1e-4)
+    _check_vs_oracle(out, ref, prec)
     pv = ref["pv"][:, ref["status"] == 0]
     first = np.argmax(pv > 0, axis=0)
     assert first.max() - first.min() > 60 * 60      # sunrise spreads over the grid's longitudes / latitudes

@@ -64,7 +64,7 @@ EXPORTS = ["tmh_abi_version", "tmh_last_error", "tmh_state_bytes", "tmh_state_of
            "tmh_scratch_bytes", "tmh_workspace_bytes", "tmh_engine_create", "tmh_engine_destroy", "tmh_engine_path",
            "tmh_init", "tmh_run", "tmh_plan", "tmh_step", "tmh_probe", "tmh_profile_enable", "tmh_profile_read",
            "tmh_set_shape_tables", "tmh_set_sites", "tmh_walk", "tmh_expand",
-           "tmh_walk_part", "tmh_expand_part"]
+           "tmh_walk_part", "tmh_expand_part", "tmh_set_clock"]
 K_EXPAND, K_SEGMENTS, K_CANDIDATES, K_STEP = 0, 1, 2, 3
 WALK_DRAWS, WALK_SEGMENTS = 1, 2
 EXPAND_KERNEL, EXPAND_COMMIT = 1, 2
@@ -105,6 +105,8 @@ def load():
     L.tmh_engine_path.argtypes = [p]
     L.tmh_engine_create.argtypes = [C.POINTER(Params), C.POINTER(Clock), C.c_int, C.POINTER(p)]
     L.tmh_engine_destroy.argtypes = [p]
+    if hasattr(L, "tmh_set_clock"):
+        L.tmh_set_clock.argtypes = [p, C.POINTER(Clock)]
     L.tmh_init.argtypes = [p, p, u64, u32, C.POINTER(UStream), p]
     L.tmh_run.argtypes = [p, p, u64, u32, i64, u32, C.POINTER(UStream), C.POINTER(Trace), C.POINTER(Stats), p, sz, p]
     L.tmh_step.argtypes = [p, p, u64, u32, i64, u32, C.POINTER(UStream), C.POINTER(Trace), C.POINTER(Stats), p, p,
@@ -125,7 +127,7 @@ def load():
     for name in ("tmh_state_offsets", "tmh_engine_create", "tmh_engine_destroy", "tmh_engine_path", "tmh_init",
                  "tmh_run", "tmh_step", "tmh_plan", "tmh_probe", "tmh_profile_enable", "tmh_profile_read",
                  "tmh_set_shape_tables", "tmh_set_sites", "tmh_walk", "tmh_expand", "tmh_walk_part",
-                 "tmh_expand_part"):
+                 "tmh_expand_part", "tmh_set_clock"):
         if hasattr(L, name):
             getattr(L, name).restype = C.c_int
     if L.tmh_abi_version() != TMH_ABI_VERSION:

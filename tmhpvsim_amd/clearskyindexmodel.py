@@ -60,7 +60,12 @@ def _draw_seed():
 
 
 class _StreamedChain:
-    """One chain on the GPU, consumed second by second from look-ahead blocks."""
+    """One chain on the GPU, consumed second by second from look-ahead blocks.
+
+    The engine's clock rolls forward with the blocks (BatchedSim installs a new
+    DST table when a block runs past the current one), so a stream has no end.
+    The current and the previous block stay readable, like the tail of the
+    reference's cache that populate_cache keeps (pvmodel.py:39-43)."""
 
     def __init__(self, time, params, tz, block, precision, device, fields):
         from .engine import BatchedSim
@@ -69,31 +74,31 @@ class _StreamedChain:
         self._block = int(block)
         self._fields = fields
         self.sim = BatchedSim(1, time, tz=tz, params=params, precision=precision, device=device,
-                              horizon=10 ** 9)
+                              horizon=max(self._block, 400 * 86400))
         st = int(self.sim.status()[0])
         if st == 1:
             raise NameError("name 'x' is not defined")        # clearskyindexmodel.py:80
         if st == 2:
             raise AssertionError()                            # cloud_cover_binary.py:91
-        self._buf = {}
-        self._lo = 0          # first step held in _buf
-        self._hi = 0          # one past the last step held
+        self._bufs = []       # [(first step, {field: np.ndarray})], at most two blocks
+        self._hi = 0          # one past the last step computed
 
     def _fill(self, upto):
         while self._hi <= upto:
             out = self.sim.run(self._block, trace=self._fields)
-            self._buf = {k: v[:, 0].cpu().numpy() for k, v in out.items()}
-            self._lo, self._hi = self._hi, self._hi + self._block
+            self._bufs = self._bufs[-1:] + [(self._hi, {k: v[:, 0].cpu().numpy() for k, v in out.items()})]
+            self._hi += self._block
 
     def value(self, step, field):
-        if step < self._lo:
-            raise KeyError(f"second {step} before the look-ahead window (only forward access is supported)")
         self._fill(step)
-        i = step - self._lo
-        cov = self._buf.get("covered")
-        if cov is not None and cov[i] == 255:
-            raise AssertionError()                             # CloudCoverBinary could not place a cloud
-        return float(self._buf[field][i])
+        for lo, buf in self._bufs:
+            if lo <= step < lo + self._block:
+                i = step - lo
+                cov = buf.get("covered")
+                if cov is not None and cov[i] == 255:
+                    raise AssertionError()                     # CloudCoverBinary could not place a cloud
+                return float(buf[field][i])
+        raise KeyError(f"second {step} is before the look-ahead window (only forward access is supported)")
 
 
 class ClearskyindexModel:

@@ -1931,6 +1931,7 @@ struct tmh_engine {
     GParams gp;
     int device;
     int path;          // resolved kernel path: 1 sequential, 2 time-parallel
+    int64_t local_step0 = 0;   // local wall-clock seconds of step 0 (the constructors' time), kept across tmh_set_clock
     uint32_t n_tab = 0;     // rows of the per-chain shape tables (0: none)
     uint32_t n_sites = 0;   // rows of the per-chain sites (0: the engine's one site)
     // kernel timing (tmh_profile_*): event pairs per kernel, read and recycled
@@ -1973,6 +1974,13 @@ struct tmh_engine {
         for (hipEvent_t e : pool) (void)hipEventDestroy(e);
     }
 };
+
+static bool whole_minutes(const tmh_clock& ck)
+{
+    bool m = ((ck.local0 - ck.utc0) % 60) == 0;
+    for (int i = 0; i < ck.n_shifts; ++i) m = m && (ck.shift_delta[i] % 60) == 0;
+    return m;
+}
 
 extern "C" {
 
@@ -2022,9 +2030,7 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
     if (clock->n_shifts < 0 || clock->n_shifts > 8) return fail(TMH_E_INVAL, "bad n_shifts %d", clock->n_shifts);
     // the time-parallel path needs every draw keyed by step, the reference's
     // memoryless (faithful) hourly draw, and whole-minute UTC offsets
-    bool minutes = ((clock->local0 - clock->utc0) % 60) == 0;
-    for (int i = 0; i < clock->n_shifts; ++i) minutes = minutes && (clock->shift_delta[i] % 60) == 0;
-    const bool tp_ok = p->rng_mode == TMH_RNG_KEYED && minutes;
+    const bool tp_ok = p->rng_mode == TMH_RNG_KEYED && whole_minutes(*clock);
     int path = p->kernel_path == TMH_PATH_AUTO ? (tp_ok ? TMH_PATH_TIME_PARALLEL : TMH_PATH_SEQUENTIAL)
                                                : p->kernel_path;
     if (path == TMH_PATH_TIME_PARALLEL && !tp_ok)
@@ -2107,7 +2113,21 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
     d.markov = p->cc_mode == TMH_CC_MARKOV;
     e->device = device;
     e->path = path;
+    e->local_step0 = clock->local0;
+    for (int i = 0; i < clock->n_shifts; ++i)
+        if (clock->shift_step[i] <= 0) e->local_step0 += clock->shift_delta[i];
     *out = e;
+    return TMH_OK;
+}
+
+int tmh_set_clock(struct tmh_engine* eng, const tmh_clock* clock)
+{
+    if (!eng || !clock) return fail(TMH_E_INVAL, "NULL engine/clock");
+    if (clock->n_shifts < 0 || clock->n_shifts > 8) return fail(TMH_E_INVAL, "bad n_shifts %d", clock->n_shifts);
+    if (clock->utc0 != eng->gp.clock.utc0) return fail(TMH_E_INVAL, "tmh_set_clock: utc0 differs (steps renumbered)");
+    if (eng->path == TMH_PATH_TIME_PARALLEL && !whole_minutes(*clock))
+        return fail(TMH_E_INVAL, "tmh_set_clock: the time-parallel path needs whole-minute offsets");
+    eng->gp.clock = *clock;
     return TMH_OK;
 }
 
@@ -2192,8 +2212,7 @@ int tmh_init(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_ch
         return fail(TMH_E_INVAL, "injected mode needs a stream with stride >= len");
     if (int rc = check_tables(eng, n_chains)) return rc;
     if (int rc = hip_check(hipSetDevice(eng->device), "hipSetDevice")) return rc;
-    const tmh_clock& ck = eng->gp.clock;
-    int64_t sod = ck.local0 % 86400;
+    int64_t sod = eng->local_step0 % 86400;   // the constructor time (step 0)
     if (sod < 0) sod += 86400;
     const double hf = ((int)((sod / 60) % 60) + (int)(sod % 60) / 60.0) / 60.0;
     StateView v = make_view(state, n_chains);

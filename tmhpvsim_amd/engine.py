@@ -16,6 +16,7 @@ from .clock import make_clock
 from .params import ModelParams, RNG_INJECTED
 
 TRACE_FIELDS = ("csi", "covered", "pv", "meter", "residual")
+ROLL_MAX = 731 * 86400   # steps per rolling clock (<= 6 DST changes in two years)
 DEFAULT_HIST = dict(n_bins=4096, lo=-300.0, hi=9000.0)
 
 
@@ -41,7 +42,8 @@ class BatchedSim:
     precision : "fp32" (per-second CSI/PV math in fp32; Markov state fp64) or "fp64"
     chain0 : global id of the first chain (keyed RNG -> partition-independent results)
     injected : optional device tensor [n_chains, L] of uniforms (RNG_INJECTED mode)
-    horizon : maximum number of steps this object will run (sizes the DST table)
+    horizon : steps covered by one wall clock (its DST table holds 8 changes); a run
+        past it installs the next rolling clock (tmh_set_clock), so runs are unbounded
     shape_tables : optional per-chain hourly cloud-cover tables (shapes [n, 6, 4],
         is_t [n, 6]; e.g. params.site_shape_tables) in place of params.shapes —
         one table per site of a lat/lon sweep (tmh_set_shape_tables)
@@ -65,6 +67,7 @@ class BatchedSim:
         if self.device.type != "cuda":
             raise ValueError("BatchedSim runs on a GPU device (there is no CPU path)")
         self.horizon = int(horizon)
+        self._start, self._tz = start, tz
         self.clock = make_clock(start, self.horizon, tz)
         kp = {"auto": _lib.PATH_AUTO, "sequential": _lib.PATH_SEQUENTIAL,
               "time_parallel": _lib.PATH_TIME_PARALLEL}[kernel_path]
@@ -172,17 +175,21 @@ class BatchedSim:
         """Advance n_steps seconds.  Returns {field: tensor[n_steps, n_chains]} for `trace`."""
         torch = _torch()
         n_steps = int(n_steps)
-        if self.step + n_steps > self.horizon:
-            raise ValueError(f"run beyond the horizon ({self.horizon} steps) given at construction")
         trace = tuple(trace or ())
+        if n_steps > ROLL_MAX:   # one rolling clock covers at most ROLL_MAX steps: run in pieces (same bits)
+            res = out if out is not None else self._alloc(n_steps, trace)
+            done = 0
+            while done < n_steps:
+                k = min(ROLL_MAX, n_steps - done)
+                self.run(k, trace, window, {f: res[f][done:done + k] for f in trace})
+                done += k
+            return res
+        if self.step + n_steps > self.clock.end:
+            self._roll(n_steps)
         for f in trace:
             if f not in TRACE_FIELDS:
                 raise ValueError(f"unknown trace field {f!r}")
-        res = out if out is not None else {}
-        for f in trace:
-            if f not in res:
-                dt = torch.uint8 if f == "covered" else self.real
-                res[f] = torch.empty(n_steps, self.n, dtype=dt, device=self.device)
+        res = out if out is not None else self._alloc(n_steps, trace)
         st = self._stats_struct()
         win = max(1, min(int(window), n_steps))
         if self.path == "time_parallel" and n_steps > win:
@@ -204,6 +211,16 @@ class BatchedSim:
                 done += k
         self.step += n_steps
         return res
+
+    def _alloc(self, n_steps, trace):
+        torch = _torch()
+        return {f: torch.empty(n_steps, self.n, dtype=torch.uint8 if f == "covered" else self.real, device=self.device)
+                for f in trace}
+
+    def _roll(self, n_steps):
+        """The next rolling wall clock, from the current step (tmh_set_clock)."""
+        self.clock = make_clock(self._start, max(int(n_steps), min(self.horizon, ROLL_MAX)), self._tz, step0=self.step)
+        _lib.check(self.L.tmh_set_clock(self._eng, C.byref(self.clock.as_struct())))
 
     def _run_pipelined(self, n_steps, win, trace, res, st):
         """Windows of the time-parallel path, pipelined: the segment walk of window
