@@ -69,6 +69,9 @@ def parse():
                          "default: normal for c2, where construction shares the walk stream, else high)")
     ap.add_argument("--expand-priority", default="normal", choices=["high", "normal"],
                     help="HIP stream priority of the expansion stream (pipelined batches)")
+    ap.add_argument("--schedule", default="gated", choices=["gated", "stagger"],
+                    help="pipelined one-window batches: 'gated' releases the expansion of batch k, the walk of "
+                         "k + 1 and the construction of k + 2 together when walk k ends; 'stagger' is round 1's")
     ap.add_argument("--pipeline", type=int, default=None,
                     help="batches in flight on separate HIP streams (1 = no overlap): the segment walks of the "
                          "next batches (latency-bound, one wave per SIMD) run beside this batch's expansion")
@@ -294,6 +297,66 @@ def main():
             cx.expanded = torch.cuda.Event()
         cx.expanded.record(cx.wstream)
 
+    # gated schedule: one walk stream and one construction stream for all batches.
+    # When the walk of batch k ends, three streams are released together: the
+    # expansion of k, the walk of k + 1 and the construction of k + 2.  Their
+    # workgroups are then dispatched interleaved, so the walk (one long-lived wave
+    # per SIMD) and the construction kernels are resident beside the expansion
+    # instead of queueing behind its 10,800 workgroups (a kernel launched while an
+    # expansion fills the CUs waits for its tail: the walks then ran three at a time,
+    # between expansions, rocprofv3 kernel trace r02).
+    wst = torch.cuda.Stream(dev, priority=prio_hi if args.walk_priority == "high" else prio_lo)
+    wst_p = C.c_void_p(wst.cuda_stream)
+    bst = torch.cuda.Stream(dev)
+    bst_p = C.c_void_p(bst.cuda_stream)
+
+    def g_build(j, gate):
+        cx = ctxs[j % len(ctxs)]
+        cx.chain0 = (rank + j * world) * n
+        if gate is not None:
+            bst.wait_event(gate)
+        if cx.expanded is not None:                        # the context's previous batch is committed
+            bst.wait_event(cx.expanded)
+        _lib.check(L.tmh_init(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, None, bst_p))
+        _lib.check(L.tmh_plan(sim._eng, 0, secs, C.c_void_p(cx.plan.data_ptr()), bst_p))
+        _lib.check(L.tmh_walk_part(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs,
+                                   C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
+                                   cx.scratch.numel(), None, 0, _lib.WALK_DRAWS, bst_p))
+        cx.done.record(bst)
+
+    def g_walk(j):
+        cx = ctxs[j % len(ctxs)]
+        wst.wait_event(cx.done)
+        _lib.check(L.tmh_walk_part(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs,
+                                   C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
+                                   cx.scratch.numel(), None, 0, _lib.WALK_SEGMENTS, wst_p))
+        cx.walked.record(wst)
+
+    def g_expand(j):
+        cx = ctxs[j % len(ctxs)]
+        estream.wait_event(cx.walked)
+        args_ = (sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs, None, C.byref(cx.tr),
+                 C.byref(cx.st) if cx.st is not None else None, C.c_void_p(cx.plan.data_ptr()),
+                 C.c_void_p(cx.scratch.data_ptr()), cx.scratch.numel())
+        _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_KERNEL, eptr))
+        _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_COMMIT, eptr))
+        if cx.expanded is None:
+            cx.expanded = torch.cuda.Event()
+        cx.expanded.record(estream)
+
+    def run_gated(k0, cnt):
+        end = k0 + cnt
+        for j in range(k0, min(k0 + 2, end)):
+            g_build(j, None)
+        g_walk(k0)
+        for k in range(k0, end):
+            gate = ctxs[k % len(ctxs)].walked
+            if k + 2 < end:
+                g_build(k + 2, gate)
+            if k + 1 < end:
+                g_walk(k + 1)
+            g_expand(k)
+
     def run_batches(k0, cnt):
         """Batches k0 .. k0 + cnt - 1.  One-window batches are software-pipelined:
         construction + plan and the expansions run in order on one stream, the
@@ -304,6 +367,9 @@ def main():
         if nwin > 1 or not args.stagger:
             for k in range(k0, k0 + cnt):
                 one_step(k)
+            return
+        if args.schedule == "gated" and len(ctxs) >= 3:
+            run_gated(k0, cnt)
             return
         D = len(ctxs)
         ahead = D - 1
@@ -394,7 +460,8 @@ def main():
                                + f"{args.start[:10]}, {args.mode} mode ({'meter+pv+residual fp32 trace' if args.mode == 'trace' else 'on-GPU stats'})",
                    "chains_per_gpu": n, "seconds": secs, "parallelism": f"chains sharded over {world} GPU(s)",
                    "batches_in_flight": len(ctxs), "staggered": bool(args.stagger and nwin == 1),
-                   "construction_on": args.build_on, "walk_priority": args.walk_priority},
+                   "construction_on": args.build_on, "walk_priority": args.walk_priority,
+                   "schedule": args.schedule if (args.stagger and nwin == 1 and len(ctxs) >= 3) else None},
         "roofline": ({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": achieved / HBM_PEAK_GBS, "traffic": traffic(args, n, secs),
                       "kernel": "expand_kernel (P2, " + sim.path + ")", "kernel_ms": kmean,

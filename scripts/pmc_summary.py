@@ -7,7 +7,7 @@ import glob
 import re
 import sys
 
-KERNELS = ["expand_kernel<float>", "expand_kernel<double>", "segments_kernel", "minute_draws_kernel",
+KERNELS = ["expand_kernel<float>", "expand_kernel<double>", "segments_kernel", "minute_table_kernel", "fixup_kernel",
            "init_kernel", "geom_kernel", "event_draws_kernel", "events_kernel", "desc_kernel", "commit_kernel",
            "chain_kernel"]
 

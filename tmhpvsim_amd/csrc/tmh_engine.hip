@@ -1021,12 +1021,18 @@ constexpr int RCH_FIXED = 4;   // chunks always processed (L <= 64 for 99.7 % of
 #ifndef TMH_SEG_WAVES
 #define TMH_SEG_WAVES 1
 #endif
+#ifndef TMH_SEG_PRIO   // wave issue priority of the walk (s_setprio) over the expansion beside it
+#define TMH_SEG_PRIO 0
+#endif
 __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
                                                           int64_t W0, uint32_t nsteps, tmh_clock ck,
                                                           const int2* __restrict__ events,
                                                           const uint32_t* __restrict__ n_events, SegView sg,
                                                           PrevView prev)
 {
+#if TMH_SEG_PRIO
+    __builtin_amdgcn_s_setprio(TMH_SEG_PRIO);
+#endif
     const int lane = threadIdx.x & 63, p = lane & 15, row0 = lane & ~15;
     const uint32_t c = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
     const bool live = c < n;
@@ -1360,11 +1366,13 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
 // one trace row's store: a buffer resource on the wave-uniform row base (SGPRs)
 // plus the lane's 32-bit byte offset, non-temporal (the trace is written once);
 // no per-lane 64-bit address arithmetic.  0x00020000: gfx9 raw-buffer dword 3.
+// num_records = the row's valid bytes: lanes past the last chain are dropped by
+// the buffer range check, so the stores need no exec mask
 template <typename R>
-__device__ __forceinline__ void row_store(void* base, size_t row_off, uint32_t lane_off, R v)
+__device__ __forceinline__ void row_store(void* base, size_t row_off, uint32_t lane_off, R v, uint32_t row_bytes)
 {
     const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(base) + row_off, 0, -1, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(base) + row_off, 0, (int)row_bytes, 0x00020000);
     if constexpr (sizeof(R) == 8)
     {
         typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -1380,6 +1388,9 @@ __device__ __forceinline__ void row_store(void* base, size_t row_off, uint32_t l
 // sampler pairs and does no fp64 work in fp32 mode.
 #ifndef TMH_HELD_LDS
 #define TMH_HELD_LDS 1
+#endif
+#ifndef TMH_COVER_LDS   // covered bits + minute draws staged in LDS at the block start
+#define TMH_COVER_LDS 1
 #endif
 #ifndef TMH_PVF_VGPR   // leading PVF fields pinned in VGPRs in the fp32 expansion
 #define TMH_PVF_VGPR 24
@@ -1460,6 +1471,57 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
         if (alive && b > 0) samplers_at<R>(d, sg, n, c, s, mc, st);
         to_real(fs, s);
     }
+#if TMH_COVER_LDS
+    // The block's covered bits and its minute draws staged in LDS before the loop:
+    // the per-second loop then issues no vector loads, so no s_waitcnt vmcnt in it
+    // waits behind the trace stores (gfx9's vmcnt counts loads and stores alike;
+    // per-second record loads cost 42 % of the waves' cycles in such waits, PMC
+    // SQ_WAIT_ANY).  Word-major: lane-consecutive dwords, no bank conflicts.
+    __shared__ uint32_t cov_lds[4][256];
+    __shared__ R min_lds[4][256];   // minute boundaries mA, mA + 1 of the block: cloudy, clear noise
+    const int32_t s0i = (int32_t)(W0 + j0), s1i = (int32_t)(W0 + j1);
+    const int32_t mA = (int32_t)j0 <= (int32_t)fm ? 0 : ((int32_t)j0 - (int32_t)fm + 59) / 60;
+    {
+        uint32_t cw[4] = {0u, 0u, 0u, 0u};
+        if (alive) {   // segment containing the block start: first record with next-call step > start
+            int lo = 0, hi = (int)sg.count[c] - 1;
+            const int last = hi;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (rec[mid].y > s0i) hi = mid;
+                else lo = mid + 1;
+            }
+            // covered iff step < x of the segment holding it: [start, min(x, y)) per segment
+            int2 r = rec[lo];
+            int32_t a = s0i;
+            for (;;) {
+                const int32_t e = min(min(r.x, r.y), s1i);
+                if (e > a) {
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) {
+                        const int32_t wl = max(a - s0i - 32 * w, 0), wh = min(e - s0i - 32 * w, 32);
+                        if (wh > wl) cw[w] |= (wh - wl == 32 ? ~0u : ((1u << (wh - wl)) - 1u)) << wl;
+                    }
+                }
+                if (r.y >= s1i || lo >= last) break;
+                a = max(a, r.y);
+                r = rec[++lo];
+            }
+            jr = (uint32_t)lo;   // the segment of the block's last step (fixup_kernel walks back from it)
+        }
+#pragma unroll
+        for (int w = 0; w < 4; ++w) cov_lds[w][threadIdx.x] = cw[w];
+        const R* mt = reinterpret_cast<const R*>(sg.mtab);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int32_t m = mA + k;
+            const bool in = live && (int32_t)fm + 60 * m < (int32_t)j1;
+            min_lds[2 * k][threadIdx.x] = in ? mt[(size_t)(2 * m) * n + c] : R(0);
+            min_lds[2 * k + 1][threadIdx.x] = in ? mt[(size_t)(2 * m + 1) * n + c] : R(0);
+        }
+    }
+    uint32_t cov_w = 0;
+#else
     if (alive) {   // segment containing the block start: first record with next-call step > start
         const int64_t s0 = W0 + j0;
         int lo = 0, hi = (int)sg.count[c] - 1;
@@ -1472,6 +1534,7 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
         seg = rec[jr];
         seg_nx = rec[min(jr + 1, sg.cap - 1)];
     }
+#endif
     const double* evd = sg.evd + c;
     U4 pair{0, 0, 0, 0};
     bool have_pair = false;
@@ -1522,12 +1585,32 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
                 }
             }
             if (fl & FL_MIN) {                         // _next_min: from the minute table
-                const R* mt = reinterpret_cast<const R*>(sg.mtab) + (size_t)(2 * (((int32_t)j - (int32_t)fm) / 60)) * n + c;
+                const int32_t mi = ((int32_t)j - (int32_t)fm) / 60;
                 fs.b[S_CLOUDY_NOISE] = fs.a[S_CLOUDY_NOISE];
-                fs.a[S_CLOUDY_NOISE] = mt[0];
                 fs.b[S_CLEAR_NOISE] = fs.a[S_CLEAR_NOISE];
+#if TMH_COVER_LDS
+                const int32_t k = mi - mA;   // wave-uniform
+                const int32_t kk = min(k, 1);
+                R ncl = min_lds[2 * kk][threadIdx.x], ncr = min_lds[2 * kk + 1][threadIdx.x];
+                if (k >= 2) {   // a third boundary in the block (its first within 8 s of the start): rare
+                    const R* mt = reinterpret_cast<const R*>(sg.mtab) + (size_t)(2 * mi) * n + c;
+                    ncl = mt[0];
+                    ncr = mt[n];
+                    __builtin_amdgcn_s_waitcnt(0);   // wait here, not at the join every minute
+                }
+                fs.a[S_CLOUDY_NOISE] = ncl;
+                fs.a[S_CLEAR_NOISE] = ncr;
+#else
+                const R* mt = reinterpret_cast<const R*>(sg.mtab) + (size_t)(2 * mi) * n + c;
+                fs.a[S_CLOUDY_NOISE] = mt[0];
                 fs.a[S_CLEAR_NOISE] = mt[n];
+#endif
             }
+#if TMH_COVER_LDS
+            const uint32_t jb = j - j0;   // wave-uniform
+            if ((jb & 31) == 0) cov_w = cov_lds[jb >> 5][threadIdx.x];
+            const bool covered = (cov_w >> (jb & 31)) & 1u;
+#else
             const int32_t stepi = (int32_t)step;   // steps < 2^31 (tmh_step checks the window)
             if (stepi >= seg.y) {   // next_cloud happened at seg.y
                 seg = seg_nx;
@@ -1536,6 +1619,7 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
                 seg_nx = rec[min(jr + 1, sg.cap - 1)];
             }
             const bool covered = stepi < seg.x;
+#endif
             cov = covered ? 1 : 0;
             if (!(step & 1) || !have_pair) {   // one Philox block per step pair (uniform branch)
 #ifdef TMH_DIAG_NO_RNG   // diagnostic builds only (scripts/diag_variants.sh): cost breakdown
@@ -1571,13 +1655,13 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
             emit<R, OUT>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok, held);
 #else
         if constexpr (OUT == OUT_TRACE3) {   // row pointers are wave-uniform: 32-bit lane offsets only
-            if (live) {                        // (SGPR row base + zero-extended lane byte offset: no 64-bit VALU adds)
-                const size_t ro = (size_t)j * tr.ld * sizeof(R);
-                const uint32_t lo = c * (uint32_t)sizeof(R);
-                row_store(tr.pv, ro, lo, pv);
-                row_store(tr.meter, ro, lo, meter);
-                row_store(tr.residual, ro, lo, res);
-            }
+            // (SGPR row base + zero-extended lane byte offset: no 64-bit VALU adds; dead lanes
+            // fall outside the buffer's range)
+            const size_t ro = (size_t)j * tr.ld * sizeof(R);
+            const uint32_t lo = c * (uint32_t)sizeof(R), rb = n * (uint32_t)sizeof(R);
+            row_store(tr.pv, ro, lo, pv, rb);
+            row_store(tr.meter, ro, lo, meter, rb);
+            row_store(tr.residual, ro, lo, res, rb);
         } else if (live) {
             emit<R, OUT>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok, held);
         }

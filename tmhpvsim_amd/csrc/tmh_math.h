@@ -28,14 +28,29 @@ __device__ __forceinline__ void key_bump(uint32_t& k0, uint32_t& k1)
     asm volatile("s_add_u32 %0, %0, 0x9e3779b9\n\ts_add_u32 %1, %1, 0xbb67ae85" : "+s"(k0), "+s"(k1) : : "scc");
 }
 
+#ifndef TMH_PHILOX_OPAQUE
+#define TMH_PHILOX_OPAQUE 1
+#endif
 __device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                             uint32_t k0, uint32_t k1)
 {
     k0 = __builtin_amdgcn_readfirstlane(k0);
     k1 = __builtin_amdgcn_readfirstlane(k1);
+#if TMH_PHILOX_OPAQUE
+    // round key r = key + r (W0, W1): one s_add with a literal each, from a base the
+    // compiler must treat as fresh per call (so it neither hoists twenty loop-invariant
+    // round keys into SGPRs nor copies a bumped register it still needs)
+    asm volatile("" : "+s"(k0), "+s"(k1));
+    const uint32_t kb0 = k0, kb1 = k1;
+#endif
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
+#if TMH_PHILOX_OPAQUE
+        k0 = kb0 + (uint32_t)r * 0x9E3779B9u;
+        k1 = kb1 + (uint32_t)r * 0xBB67AE85u;
+#else
         if (r) key_bump(k0, k1);
+#endif
         // one v_mad_u64_u32 per product (both halves) instead of mul_lo + mul_hi:
         // about 25 % less issue time per block on gfx950 (scripts/micro/philox_bench.hip)
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
@@ -108,43 +123,67 @@ __device__ __noinline__ double ndtri(double p)
 // kernels that call it per second keep their register budget
 __device__ __noinline__ double ndtri_fast(double p) { return normcdfinv(p); }
 
+// Giles' single-precision erfinv ("Approximating the erfinv function", GPU
+// Computing Gems, 2011) as p(w), w = -log((1 - x)(1 + x)), erfinv(x) = p x:
+// central polynomial in w - 2.5 for w < 5 (99.66 % of draws) ...
+__device__ __forceinline__ float erfinv_central(float w0)
+{
+    const float v = w0 - 2.5f;
+    float p = 2.81022636e-08f;
+    p = fmaf(p, v, 3.43273939e-07f);
+    p = fmaf(p, v, -3.5233877e-06f);
+    p = fmaf(p, v, -4.39150654e-06f);
+    p = fmaf(p, v, 0.00021858087f);
+    p = fmaf(p, v, -0.00125372503f);
+    p = fmaf(p, v, -0.00417768164f);
+    p = fmaf(p, v, 0.246640727f);
+    return fmaf(p, v, 1.50140941f);
+}
+
+// ... his tail polynomial in sqrt(w) - 3 for 5 <= w < 16, and for 16 <= w <= 21.5
+// (t down to 2^-33, the smallest 32-bit midpoint uniform) a quintic in sqrt(w) - 4.3
+// fitted here (scripts/fit_ndtri_tail.py: 1.7e-7 relative; Giles' tail is 4e-4 off
+// there).  Straight-line code: no nested branch (the library quantile's nest of
+// exec-mask branches cost the per-second loop ~20 scalar instructions a step).
+__device__ __forceinline__ float erfinv_tail(float w0)
+{
+    const float s = __builtin_amdgcn_sqrtf(w0);
+    const float v = s - 3.0f;
+    float p = -0.000200214257f;
+    p = fmaf(p, v, 0.000100950558f);
+    p = fmaf(p, v, 0.00134934322f);
+    p = fmaf(p, v, -0.00367342844f);
+    p = fmaf(p, v, 0.00573950773f);
+    p = fmaf(p, v, -0.0076224613f);
+    p = fmaf(p, v, 0.00943887047f);
+    p = fmaf(p, v, 1.00167406f);
+    p = fmaf(p, v, 2.83297682f);
+    const float e = s - 4.3f;
+    float q = -5.854465416632593e-05f;
+    q = fmaf(q, e, 0.00019957200856879354f);
+    q = fmaf(q, e, -0.000567059323657304f);
+    q = fmaf(q, e, 0.000624575128313154f);
+    q = fmaf(q, e, 1.010045051574707f);
+    q = fmaf(q, e, 4.14272403717041f);
+    return w0 < 16.0f ? p : q;
+}
+
 // standard normal quantile from a fp64 uniform in fp32 arithmetic:
-// ndtri(u) = sqrt(2) erfinv(2u - 1) with Giles' single-precision erfinv
-// ("Approximating the erfinv function", GPU Computing Gems, 2011), whose
-// log argument (1 - x)(1 + x) = 4u(1 - u) is formed in fp64 so the tails keep
-// full relative precision.  Central branch for w < 5 (99.6 % of draws), tail
-// polynomial up to w = 16; beyond (p < 2e-7 per draw) the fp32 library quantile.
+// ndtri(u) = sqrt(2) erfinv(2u - 1), the log argument (1 - x)(1 + x) = 4u(1 - u)
+// formed in fp64 so the tails keep full relative precision.  53-bit uniforms reach
+// past w = 21.5 (p < 5e-10 per draw): the fp32 library quantile there.
 __device__ __forceinline__ float ndtri_f(double u)
 {
     const float x = (float)(2.0 * u - 1.0);
     const float w0 = -__logf((float)(4.0 * u * (1.0 - u)));
-    float p;
-    if (w0 < 5.0f) {
-        const float w = w0 - 2.5f;
-        p = 2.81022636e-08f;
-        p = fmaf(p, w, 3.43273939e-07f);
-        p = fmaf(p, w, -3.5233877e-06f);
-        p = fmaf(p, w, -4.39150654e-06f);
-        p = fmaf(p, w, 0.00021858087f);
-        p = fmaf(p, w, -0.00125372503f);
-        p = fmaf(p, w, -0.00417768164f);
-        p = fmaf(p, w, 0.246640727f);
-        p = fmaf(p, w, 1.50140941f);
-    } else if (w0 < 16.0f) {
-        const float w = sqrtf(w0) - 3.0f;
-        p = -0.000200214257f;
-        p = fmaf(p, w, 0.000100950558f);
-        p = fmaf(p, w, 0.00134934322f);
-        p = fmaf(p, w, -0.00367342844f);
-        p = fmaf(p, w, 0.00573950773f);
-        p = fmaf(p, w, -0.0076224613f);
-        p = fmaf(p, w, 0.00943887047f);
-        p = fmaf(p, w, 1.00167406f);
-        p = fmaf(p, w, 2.83297682f);
-    } else {
-        const double t = u < 0.5 ? u : 1.0 - u;
-        const float z = normcdfinvf((float)t);
-        return u < 0.5 ? z : -z;
+    float p = erfinv_central(w0);
+    if (w0 >= 5.0f) {
+        if (w0 > 21.5f) {
+            const double t = u < 0.5 ? u : 1.0 - u;
+            const float z = normcdfinvf((float)t);
+            return u < 0.5 ? z : -z;
+        }
+        p = erfinv_tail(w0);
     }
     return 1.41421356237309505f * (p * x);
 }
@@ -160,33 +199,8 @@ __device__ __forceinline__ float ndtri_w(uint32_t w)
     const float x = fmaf((float)(int32_t)(w ^ 0x80000000u), 0x1p-31f, 0x1p-32f);
     // -log((1 - x)(1 + x)) = -log(4 t (1 - t)); the argument is >= 2^-31: no denormal path needed
     const float w0 = -0.693147180559945309f * __builtin_amdgcn_logf(fmaf(-4.0f * t, t, 4.0f * t));
-    float p;
-    if (w0 < 5.0f) {
-        const float v = w0 - 2.5f;
-        p = 2.81022636e-08f;
-        p = fmaf(p, v, 3.43273939e-07f);
-        p = fmaf(p, v, -3.5233877e-06f);
-        p = fmaf(p, v, -4.39150654e-06f);
-        p = fmaf(p, v, 0.00021858087f);
-        p = fmaf(p, v, -0.00125372503f);
-        p = fmaf(p, v, -0.00417768164f);
-        p = fmaf(p, v, 0.246640727f);
-        p = fmaf(p, v, 1.50140941f);
-    } else if (w0 < 16.0f) {
-        const float v = sqrtf(w0) - 3.0f;
-        p = -0.000200214257f;
-        p = fmaf(p, v, 0.000100950558f);
-        p = fmaf(p, v, 0.00134934322f);
-        p = fmaf(p, v, -0.00367342844f);
-        p = fmaf(p, v, 0.00573950773f);
-        p = fmaf(p, v, -0.0076224613f);
-        p = fmaf(p, v, 0.00943887047f);
-        p = fmaf(p, v, 1.00167406f);
-        p = fmaf(p, v, 2.83297682f);
-    } else {   // p < 2e-7 per draw
-        const float z = normcdfinvf(t);
-        return w < 0x80000000u ? z : -z;
-    }
+    float p = erfinv_central(w0);
+    if (w0 >= 5.0f) p = erfinv_tail(w0);   // 0.34 % of draws; w0 <= 21.5 for 32-bit words
     return 1.41421356237309505f * (p * x);
 }
 
