@@ -1003,7 +1003,7 @@ __device__ __forceinline__ double bperm_f64(int src_lane, double v)
 }
 
 #ifndef TMH_RCH
-#define TMH_RCH 8
+#define TMH_RCH 4
 #endif
 constexpr int RCH = TMH_RCH;   // register chunks of 16 entries: sigma entries 0..127 (all but ~1e-5 of calls)
 constexpr int RCH_FIXED = 4;   // chunks always processed (L <= 64 for 99.7 % of calls)
@@ -1267,9 +1267,13 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
             sl_last = gsl[last];
         }
         const double nclr = f * (ncl + sc_last) - sl_last;
+        // entry 16 RCH - 1 (register chunk RCH - 1, lane 15) for lane 0 of the first global chunk:
+        // the DPP runs with the whole row active (under a p == 0 branch lane 15 would be
+        // masked off and the read would return the DPP's old value)
+        const double carry_g = dpp_row_f64<0x121>(0.0, vc[RCH - 1]);
         for (int ch = top; ch >= RCH; --ch) {   // rare, descending: reads before writes
             const int k = ch * 16 + p;
-            const double prev = (ch == RCH && p == 0) ? dpp_row_f64<0x121>(0.0, vc[RCH - 1]) : gsc[k - 1];
+            const double prev = (ch == RCH && p == 0) ? carry_g : gsc[k - 1];
             const double nsc = ncl + prev;
             gsc[k] = nsc;
             gsl[k] = f * nsc;
@@ -1363,24 +1367,21 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
 }
 
 // ------------------------------------------------------------ P2: expand
-// one trace row's store: a buffer resource on the wave-uniform row base (SGPRs)
-// plus the lane's 32-bit byte offset, non-temporal (the trace is written once);
-// no per-lane 64-bit address arithmetic.  0x00020000: gfx9 raw-buffer dword 3.
-// num_records = the row's valid bytes: lanes past the last chain are dropped by
-// the buffer range check, so the stores need no exec mask
+// one trace store: a buffer resource on a wave-uniform base (SGPRs) plus the lane's
+// 32-bit byte offset, non-temporal (the trace is written once); no per-lane 64-bit
+// address arithmetic.  0x00020000: gfx9 raw-buffer dword 3.  Offsets past
+// num_records are dropped by the range check (lanes past the last chain)
 template <typename R>
-__device__ __forceinline__ void row_store(void* base, size_t row_off, uint32_t lane_off, R v, uint32_t row_bytes)
+__device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t rs, uint32_t off, R v)
 {
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(base) + row_off, 0, (int)row_bytes, 0x00020000);
     if constexpr (sizeof(R) == 8)
     {
         typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
         const uint64_t u = (uint64_t)__double_as_longlong(v);
-        __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)u, (uint32_t)(u >> 32)}, rs, (int)lane_off, 0, 2 /* nt */);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)u, (uint32_t)(u >> 32)}, rs, (int)off, 0, 2 /* nt */);
     }
     else
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (int)lane_off, 0, 2 /* nt */);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (int)off, 0, 2 /* nt */);
 }
 
 // One work-item per (chain, block of 128 seconds).  The boundary draws come
@@ -1389,14 +1390,11 @@ __device__ __forceinline__ void row_store(void* base, size_t row_off, uint32_t l
 #ifndef TMH_HELD_LDS
 #define TMH_HELD_LDS 1
 #endif
-#ifndef TMH_COVER_LDS   // covered bits + minute draws staged in LDS at the block start
-#define TMH_COVER_LDS 1
+#ifndef TMH_EXP_CHAIN_FAST
+#define TMH_EXP_CHAIN_FAST 0
 #endif
 #ifndef TMH_PVF_VGPR   // leading PVF fields pinned in VGPRs in the fp32 expansion
-#define TMH_PVF_VGPR 24
-#endif
-#ifndef TMH_ROW_PREFETCH
-#define TMH_ROW_PREFETCH 0
+#define TMH_PVF_VGPR 8
 #endif
 #ifndef TMH_DIAG_EXP_LDS   // diagnostic: extra LDS per expand workgroup (caps its occupancy)
 #define TMH_DIAG_EXP_LDS 0
@@ -1422,8 +1420,14 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
                                                      StatsView sv)
 {
     extern __shared__ uint32_t lds_hist[];
+#if TMH_EXP_CHAIN_FAST   // 1-D grid, chain block fastest: the workgroups writing one trace row run together
+    const uint32_t ncb = (n + 255) / 256;
+    const uint32_t b = blockIdx.x / ncb;
+    const uint32_t c = (blockIdx.x - b * ncb) * blockDim.x + threadIdx.x;
+#else
     const uint32_t c = blockIdx.y * blockDim.x + threadIdx.x;   // grid: x = time block, y = chain block
     const uint32_t b = blockIdx.x;
+#endif
     const bool live = c < n;
     if (sv.hist) {
         for (uint32_t i = threadIdx.x; i < sv.n_bins; i += blockDim.x) lds_hist[i] = 0;
@@ -1445,7 +1449,6 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
     Acc acc{0.0, 0.0, 0.0, -INFINITY};
     bool alive = false;
     int32_t fault = INT_MAX;
-    int2 seg = make_int2(0, 0), seg_nx = make_int2(0, 0);   // current record and the next, loaded ahead
     const int2* rec = sg.rec + (size_t)(live ? c : 0) * sg.cap;
     uint32_t jr = 0, evi = 0;
     FSamp<R> fs;
@@ -1471,7 +1474,6 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
         if (alive && b > 0) samplers_at<R>(d, sg, n, c, s, mc, st);
         to_real(fs, s);
     }
-#if TMH_COVER_LDS
     // The block's covered bits and its minute draws staged in LDS before the loop:
     // the per-second loop then issues no vector loads, so no s_waitcnt vmcnt in it
     // waits behind the trace stores (gfx9's vmcnt counts loads and stores alike;
@@ -1521,58 +1523,43 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
         }
     }
     uint32_t cov_w = 0;
-#else
-    if (alive) {   // segment containing the block start: first record with next-call step > start
-        const int64_t s0 = W0 + j0;
-        int lo = 0, hi = (int)sg.count[c] - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if ((int64_t)rec[mid].y > s0) hi = mid;
-            else lo = mid + 1;
-        }
-        jr = (uint32_t)lo;
-        seg = rec[jr];
-        seg_nx = rec[min(jr + 1, sg.cap - 1)];
-    }
-#endif
     const double* evd = sg.evd + c;
-    U4 pair{0, 0, 0, 0};
-    bool have_pair = false;
-    // the step's geometry row (wave-uniform, scalar loads) is fetched one step
-    // ahead, so its latency hides behind the previous step's arithmetic
-    auto load_row = [&](uint32_t j, R* r) {
-#pragma unroll
-        for (int i = 0; i < row_w<R>(); ++i)
-            r[i] = sizeof(R) == 8 ? (R)tab64[(size_t)j * ROW + i] : (R)tab32[(size_t)j * ROW32 + i];
-    };
-#if TMH_ROW_PREFETCH
-    R row_nx[row_w<R>()];
-    load_row(j0, row_nx);
-#endif
 #if TMH_HELD_LDS   // the guard-band seconds of the lane's block, a bit each, in LDS: no register carried through the loop
     __shared__ uint4 held_lds[256];
     held_lds[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
 #else
     bool held_any = false;   // fp32: some second of this block lies in a guard band (pv_power_f)
 #endif
-    for (uint32_t j = j0; j < j1; ++j) {
-        const int64_t step = W0 + j;
+    // Trace stores: one buffer resource per output for the block's rows (built here,
+    // not per store) and one running per-lane byte offset; lanes past the last chain
+    // start at 2^31, out of the resource's range, so the stores need no exec mask.
+    // (The host keeps a block's rows under 2 GiB: tmh_expand checks the trace's ld.)
+    constexpr int RW = sizeof(R) == 8 ? ROW : ROW32;   // geometry row: wave-uniform, scalar loads
+    const R* rowp = (sizeof(R) == 8 ? reinterpret_cast<const R*>(tab64) : reinterpret_cast<const R*>(tab32)) +
+                    (size_t)j0 * RW;
+    __amdgpu_buffer_rsrc_t rs_pv, rs_m, rs_r;
+    uint32_t voff = live ? c * (uint32_t)sizeof(R) : 0x80000000u;
+    const uint32_t rowb = (uint32_t)(tr.ld * sizeof(R));
+    if constexpr (OUT == OUT_TRACE3) {
+        const size_t bo = (size_t)j0 * tr.ld * sizeof(R);
+        const int nb = (int)((j1 - j0) * rowb);
+        rs_pv = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(tr.pv) + bo, 0, nb, 0x00020000);
+        rs_m = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(tr.meter) + bo, 0, nb, 0x00020000);
+        rs_r = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(tr.residual) + bo, 0, nb, 0x00020000);
+    }
+    const int32_t fault_eff = alive ? fault : 0;   // ok = j < fault_eff: one compare, no branch
+    // One second.  Every lane computes it; a lane whose chain is faulted (or not
+    // alive) emits NaN / no statistics.  un, um: the step's Philox words (noise, meter).
+    auto second = [&](uint32_t j, uint32_t un, uint32_t um) {
         R row[row_w<R>()];
-#if TMH_ROW_PREFETCH
 #pragma unroll
-        for (int i = 0; i < row_w<R>(); ++i) row[i] = row_nx[i];
-        if (j + 1 < j1) load_row(j + 1, row_nx);
-#else
-        load_row(j, row);
-#endif
-        const uint32_t fl = sizeof(R) == 8 ? (uint32_t)tab64[(size_t)j * ROW + G_FLAGS] : __float_as_uint(row[G_FLAGS + G32]);
-        R csi = R(NAN), pv = R(NAN), meter = R(NAN), res = R(NAN);
-        uint8_t cov = 255;
-        bool held = false;   // fp32: PV in a guard band, recomputed in fp64 by fixup_kernel
-        const bool ok = alive && (int32_t)j < fault;
-        if (ok) {
-            if (fl & (FL_DAY | FL_HOUR)) {            // _next_day, _next_hour
-                const size_t eo = (size_t)evi * 4 * n;
+        for (int i = 0; i < row_w<R>(); ++i) row[i] = rowp[i];
+        rowp += RW;
+        const uint32_t fl = sizeof(R) == 8 ? (uint32_t)(double)rowp[G_FLAGS - RW] : __float_as_uint(row[G_FLAGS + G32]);
+        const bool ok = (int32_t)j < fault_eff;
+        if (fl & (FL_DAY | FL_HOUR)) {            // _next_day, _next_hour (rare: loads waited here)
+            const size_t eo = (size_t)evi * 4 * n;
+            if (live) {
                 if (fl & FL_DAY) {
                     fs.b[S_CLEAR_DAY] = fs.a[S_CLEAR_DAY];
                     fs.a[S_CLEAR_DAY] = (R)evd[eo + 2 * (size_t)n];
@@ -1584,88 +1571,81 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
                     fs.a[S_CLEAR_DAY] = (R)evd[eo + 3 * (size_t)n];
                 }
             }
-            if (fl & FL_MIN) {                         // _next_min: from the minute table
-                const int32_t mi = ((int32_t)j - (int32_t)fm) / 60;
-                fs.b[S_CLOUDY_NOISE] = fs.a[S_CLOUDY_NOISE];
-                fs.b[S_CLEAR_NOISE] = fs.a[S_CLEAR_NOISE];
-#if TMH_COVER_LDS
-                const int32_t k = mi - mA;   // wave-uniform
-                const int32_t kk = min(k, 1);
-                R ncl = min_lds[2 * kk][threadIdx.x], ncr = min_lds[2 * kk + 1][threadIdx.x];
-                if (k >= 2) {   // a third boundary in the block (its first within 8 s of the start): rare
+            __builtin_amdgcn_s_waitcnt(0);
+            ++evi;
+        }
+        if (fl & FL_MIN) {                         // _next_min: staged minute draws
+            const int32_t mi = ((int32_t)j - (int32_t)fm) / 60;
+            fs.b[S_CLOUDY_NOISE] = fs.a[S_CLOUDY_NOISE];
+            fs.b[S_CLEAR_NOISE] = fs.a[S_CLEAR_NOISE];
+            const int32_t k = mi - mA;   // wave-uniform
+            const int32_t kk = min(k, 1);
+            R ncl = min_lds[2 * kk][threadIdx.x], ncr = min_lds[2 * kk + 1][threadIdx.x];
+            if (k >= 2) {   // a third boundary in the block (its first within 8 s of the start): rare
+                if (live) {
                     const R* mt = reinterpret_cast<const R*>(sg.mtab) + (size_t)(2 * mi) * n + c;
                     ncl = mt[0];
                     ncr = mt[n];
-                    __builtin_amdgcn_s_waitcnt(0);   // wait here, not at the join every minute
                 }
-                fs.a[S_CLOUDY_NOISE] = ncl;
-                fs.a[S_CLEAR_NOISE] = ncr;
-#else
-                const R* mt = reinterpret_cast<const R*>(sg.mtab) + (size_t)(2 * mi) * n + c;
-                fs.a[S_CLOUDY_NOISE] = mt[0];
-                fs.a[S_CLEAR_NOISE] = mt[n];
-#endif
+                __builtin_amdgcn_s_waitcnt(0);   // wait here, not at the join every minute
             }
-#if TMH_COVER_LDS
-            const uint32_t jb = j - j0;   // wave-uniform
-            if ((jb & 31) == 0) cov_w = cov_lds[jb >> 5][threadIdx.x];
-            const bool covered = (cov_w >> (jb & 31)) & 1u;
-#else
-            const int32_t stepi = (int32_t)step;   // steps < 2^31 (tmh_step checks the window)
-            if (stepi >= seg.y) {   // next_cloud happened at seg.y
-                seg = seg_nx;
-                ++jr;
-                while (stepi >= seg.y) seg = rec[++jr];   // zero-length segments (rare)
-                seg_nx = rec[min(jr + 1, sg.cap - 1)];
-            }
-            const bool covered = stepi < seg.x;
-#endif
-            cov = covered ? 1 : 0;
-            if (!(step & 1) || !have_pair) {   // one Philox block per step pair (uniform branch)
-#ifdef TMH_DIAG_NO_RNG   // diagnostic builds only (scripts/diag_variants.sh): cost breakdown
-                const uint32_t hsh = (uint32_t)chain * 0x9E3779B9u ^ (uint32_t)step * 0x85EBCA6Bu;
-                pair = U4{hsh, hsh >> 3, hsh ^ 0x5555u, hsh >> 5};
-#else
-                pair = keyed_block(kp.seed, chain, (uint64_t)step >> 1, TAG_STEP2, 0);
-#endif
-                have_pair = true;
-            }
-            const bool odd = step & 1;
-            uint32_t flp = fl;
-            if constexpr (SITES) {   // this chain's own site: geometry per chain-second
-                const bool night = lane_row<R>(ls, sun + (size_t)j * SUN_W, kp.module, row);
-                flp = night ? (fl | FL_NIGHT) : (fl & ~(uint32_t)FL_NIGHT);
-            }
-            second_body<R>(kp, pkv, row, flp, fs, covered, noise_z<R>(odd ? pair.z : pair.x), meter_w<R>(odd ? pair.w : pair.y),
-                           csi, pv, meter, res, held);
-            if constexpr (sizeof(R) == 4) {
-#if TMH_HELD_LDS
-                if (held) {   // (j - j0) is wave-uniform: the word and the bit are scalars
-                    uint32_t* hw = reinterpret_cast<uint32_t*>(&held_lds[threadIdx.x]) + ((j - j0) >> 5);
-                    *hw |= 1u << ((j - j0) & 31);
-                }
-#else
-                held_any |= held;   // guard band of a PV discontinuity: fixup_kernel redoes this block's such seconds in fp64
-#endif
-            }
+            fs.a[S_CLOUDY_NOISE] = ncl;
+            fs.a[S_CLEAR_NOISE] = ncr;
         }
-        if (fl & (FL_DAY | FL_HOUR)) ++evi;
+        const uint32_t jb = j - j0;   // wave-uniform
+        if ((jb & 31) == 0) cov_w = cov_lds[jb >> 5][threadIdx.x];
+        const bool covered = (cov_w >> (jb & 31)) & 1u;
+        uint32_t flp = fl;
+        if constexpr (SITES) {   // this chain's own site: geometry per chain-second
+            const bool night = lane_row<R>(ls, sun + (size_t)j * SUN_W, kp.module, row);
+            flp = night ? (fl | FL_NIGHT) : (fl & ~(uint32_t)FL_NIGHT);
+        }
+        R csi, pv, meter, res;
+        bool held = false;   // fp32: PV in a guard band, recomputed in fp64 by fixup_kernel
+        second_body<R>(kp, pkv, row, flp, fs, covered, noise_z<R>(un), meter_w<R>(um), csi, pv, meter, res, held);
+        held = held && ok;
+        if constexpr (sizeof(R) == 4) {
+#if TMH_HELD_LDS
+            if (held) {   // jb is wave-uniform: the word and the bit are scalars
+                uint32_t* hw = reinterpret_cast<uint32_t*>(&held_lds[threadIdx.x]) + (jb >> 5);
+                *hw |= 1u << (jb & 31);
+            }
+#else
+            held_any |= held;   // guard band of a PV discontinuity: fixup_kernel redoes this block's such seconds in fp64
+#endif
+        }
+        csi = ok ? csi : R(NAN);
+        pv = ok ? pv : R(NAN);
+        meter = ok ? meter : R(NAN);
+        res = ok ? res : R(NAN);
+        const uint8_t cov = ok ? (covered ? 1 : 0) : 255;
 #ifdef TMH_DIAG_NO_STORE
         if (live && csi == R(-12345))
             emit<R, OUT>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok, held);
 #else
-        if constexpr (OUT == OUT_TRACE3) {   // row pointers are wave-uniform: 32-bit lane offsets only
-            // (SGPR row base + zero-extended lane byte offset: no 64-bit VALU adds; dead lanes
-            // fall outside the buffer's range)
-            const size_t ro = (size_t)j * tr.ld * sizeof(R);
-            const uint32_t lo = c * (uint32_t)sizeof(R), rb = n * (uint32_t)sizeof(R);
-            row_store(tr.pv, ro, lo, pv, rb);
-            row_store(tr.meter, ro, lo, meter, rb);
-            row_store(tr.residual, ro, lo, res, rb);
+        if constexpr (OUT == OUT_TRACE3) {
+            row_store(rs_pv, voff, pv);
+            row_store(rs_m, voff, meter);
+            row_store(rs_r, voff, res);
+            voff += rowb;
         } else if (live) {
             emit<R, OUT>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok, held);
         }
 #endif
+    };
+    // one Philox block per step pair: (x, y) for the even step, (z, w) for the odd one
+    if (((W0 + j0) & 1) == 0 && ((j1 - j0) & 1) == 0) {
+        for (uint32_t j = j0; j < j1; j += 2) {
+            const U4 pr = keyed_block(kp.seed, chain, (uint64_t)(W0 + j) >> 1, TAG_STEP2, 0);
+            second(j, pr.x, pr.y);
+            second(j + 1, pr.z, pr.w);
+        }
+    } else {   // odd window start or length: one block per step (rare)
+        for (uint32_t j = j0; j < j1; ++j) {
+            const U4 pr = keyed_block(kp.seed, chain, (uint64_t)(W0 + j) >> 1, TAG_STEP2, 0);
+            const bool odd = (W0 + j) & 1;
+            second(j, odd ? pr.z : pr.x, odd ? pr.w : pr.y);
+        }
     }
     if constexpr (sizeof(R) == 4) {
 #if TMH_HELD_LDS
@@ -2430,12 +2410,19 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
                                    n_chains, step0, n_steps, fmh, pv.tab64, pv.events, pv.n_events, sg);
         }
     }
+#if TMH_EXP_CHAIN_FAST
+    dim3 grid2(nblk_of(n_steps) * cb);
+#else
     dim3 grid2(nblk_of(n_steps), cb);
+#endif
     const bool no_stats = !sv.hist && !sv.acc;
     const int out = (no_stats && tv.pv && tv.meter && tv.residual && !tv.csi && !tv.covered) ? OUT_TRACE3
                     : (!tv.pv && !tv.meter && !tv.residual && !tv.csi && !tv.covered) ? OUT_STATS
                                                                                       : OUT_ANY;
-#define LAUNCH(R, O, S)                                                                                              \
+    if (out == OUT_TRACE3 && tv.ld * (f64 ? 8u : 4u) * BLOCK_STEPS >= (1ull << 31))   // one block's rows: one buffer range
+        return fail(TMH_E_INVAL, "trace ld %llu too large (a 128-step block of rows must stay under 2 GiB)",
+                    (unsigned long long)tv.ld);
+#define LAUNCH(R, O, S)                                                                                            \
     hipLaunchKernelGGL((expand_kernel<R, O, S>), grid2, dim3(256), lds + TMH_DIAG_EXP_LDS, s, eng->kp, eng->dp, v, chain0, n_chains,      \
                        step0, n_steps, utc0, pv.tab64, pv.tab32, pv.sun, pv.events, pv.n_events, pv.desc, sg, tv, sv)
     if (eng->kp.sites) {   // per-chain sites: one instantiation per precision, any output
