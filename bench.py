@@ -14,12 +14,16 @@ independent).  value = chain-seconds of all ranks / max rank tim
 
 Roofline: the dominant kernel (expand_kernel, P2 of the time-parallel path) is
 timed with HIP events the library records on the stream it runs on
-(tmh_profile_enable / tmh_profile_read); achieved = 12 B x chains x seconds per
-launch / mean launch time, against 8 TB/s.  `traffic` = HBM bytes per launch of
-that kernel from the rocprofv3 PMC passes (scripts/pmc.sh, FETCH_SIZE x 2 +
-WRITE_SIZE, MI355X_MICROARCH.md), read from profiles/pmc_traffic.json when it
-was measured on this same workload, else null.  cpu_baseline: the C oracle (oracle/tmh_oracle.c,
-"port") on a bounded sample of the same workload on this host, rank 0, N = 1.
+(tmh_profile_enable / tmh_profile_read).  Trace mode is HBM-bound: achieved =
+12 B x chains x seconds per launch / mean launch time, against 8 TB/s.  Stats
+mode writes no trace and is VALU-bound: achieved = the launch's
+VALU lane-ops (rocprofv3 SQ_INSTS_VALU x 64, profiles/pmc_kernels.json, measured
+on the same workload) / mean launch time, against 256 CU x 4 SIMD x 32 lanes x
+2.4 GHz.  `traffic` = HBM bytes per launch from the same PMC record (FETCH_SIZE x
+2 + WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction), null when no record
+matches.  cpu_baseline: the C oracle (oracle/tmh_oracle.c, "port") on a bounded
+sample of the same workload on this host, rank 0, N = 1: all threads of the
+box's share (<= 16) and one thread.
 """
 from __future__ import annotations
 
@@ -35,6 +39,9 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 TRACE_BYTES = 12               # meter + pv + residual, fp32 (24 in fp64)
+# VALU issue peak: 256 CUs x 4 SIMD-32 x 32 lanes per cycle x 2.4 GHz (a wave64
+# instruction issues over 2 cycles, MI355X_MICROARCH.md), in lane-ops/s
+VALU_PEAK_TLANE = 256 * 4 * 32 * 2.4e9 / 1e12
 
 
 def parse():
@@ -92,37 +99,55 @@ def parse():
 
 
 def cpu_baseline(args, kw):
-    """The C oracle on a bounded sample of the same workload (same site(s)/day/modes, fp64)."""
+    """The C oracle on a bounded sample of the same workload (same site(s)/day/modes, fp64):
+    OpenMP over the box's CPU share (<= 16 threads) and one thread on a smaller sample."""
     from oracle import oracle as O
     from tmhpvsim_amd.params import CC_MARKOV, ModelParams
-    threads = max(1, min(16, os.cpu_count() or 1))
+    nproc = os.cpu_count() or 1
+    threads = max(1, min(16, nproc))
     c5 = args.workload == "c5"
     mp = ModelParams(cc_mode=CC_MARKOV if args.cc == "markov" else 0)
-    n = args.cpu_sample_chains if not c5 else min(args.cpu_sample_chains // 16, args.chains)
     secs = min(args.seconds, 86400)
-    extra = {}
-    if c5:   # the first n sites of the sweep, their tables; geometry per chain-second like the GPU path
-        extra = dict(tables=tuple(x[:n] for x in kw["shape_tables"]), sites=kw["sites"][:n])
+
+    def timed(n, nt):
+        extra = {}
+        if c5:   # the first n sites of the sweep, their tables; geometry per chain-second like the GPU path
+            extra = dict(tables=tuple(x[:n] for x in kw["shape_tables"]), sites=kw["sites"][:n])
+        t = time.perf_counter()
+        O.run(mp, 10 ** 9, n, secs, args.start, tz="Europe/Berlin", n_threads=nt, outputs=("residual",), **extra)
+        return time.perf_counter() - t
+
     O.run(mp, 0, 2, 600, args.start, tz="Europe/Berlin", n_threads=1)   # load + warm
-    t = time.perf_counter()
-    O.run(mp, 10 ** 9, n, secs, args.start, tz="Europe/Berlin", n_threads=threads, outputs=("residual",), **extra)
-    dt = time.perf_counter() - t
+    n = args.cpu_sample_chains if not c5 else min(args.cpu_sample_chains // 16, args.chains)
+    dt = timed(n, threads)
+    n1 = max(1, n // 16)
+    dt1 = timed(n1, 1)
+    what = 'C5 sites/tables, ' + args.cc if c5 else 'C2 site/day'
     return {"value": n * secs / dt, "unit": "chain-seconds/s", "cores": threads, "kind": "port",
-"sample": f"{n} chains x {secs} s ({'C5 sites/tables, ' + args.cc if c5 else 'C2 site/day'}, fp64 C oracle, "
-                      f"{threads} OpenMP threads, {dt:.1f} s wall)"}
+            "sample": f"{n} chains x {secs} s ({what}, fp64 C oracle, {threads} OpenMP threads of nproc={nproc}, "
+                      f"{dt:.1f} s wall)",
+            "single_thread": {"value": n1 * secs / dt1, "cores": 1,
+                              "sample": f"{n1} chains x {secs} s, 1 thread, {dt1:.1f} s wall"},
+            "reference_python_per_core": {"value": 4.0e4, "source": "BASELINE.md (timed in the build container; "
+                                                                    "the reference cannot run on the GPU box)"}}
 
 
-def traffic(args, n, secs):
-    """HBM bytes per expand_kernel launch from the committed PMC summary, when it
-    was measured on this workload (scripts/pmc.sh + scripts/pmc_summary.py)."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def pmc_record(args, n, launch_secs):
+    """The committed PMC record of the dominant kernel on this workload
+    (profiles/pmc_kernels.json, written by scripts/pmc_summary.py from the
+    rocprofv3 --pmc passes of scripts/pmc_workload.sh): per-launch VALU / SALU
+    wave-instructions and HBM bytes.  None when that workload was not measured."""
+    path = os.path.join(ROOT, "profiles", "pmc_kernels.json")
     try:
-        d = json.load(open(path))
-    except (OSError, ValueError):
+        recs = json.load(open(path))["records"]
+    except (OSError, ValueError, KeyError):
         return None
-    if (d.get("chains"), d.get("seconds"), d.get("precision"), d.get("mode")) != (n, secs, args.precision, args.mode):
-        return None
-    return d.get("traffic_bytes_per_launch")
+    want = dict(workload=args.workload, chains=n, launch_seconds=launch_secs, precision=args.precision,
+                mode=args.mode, cc=args.cc)
+    for r in recs:
+        if all(r.get(k) == v for k, v in want.items()):
+            return r
+    return None
 
 
 def main():
@@ -411,8 +436,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run_batches(args.warmup, args.steps)
-    if args.mode == "stats":
-        exchange()
+    tot = exchange() if args.mode == "stats" else None
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -445,9 +469,44 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kmean = float(t[0]), float(t[1])
     chain_seconds = world * n * secs * args.steps
-    value = chain_seconds / elapsed
+    # stats mode: the chain-seconds actually simulated = the histogram's count (a chain
+    # that faults, e.g. the reference's AssertionError in markov mode, freezes and
+    # records nothing more; edge bins absorb out-of-range residuals)
+    live = int(tot["hist"].sum()) if tot is not None else None
+    value = (live if live is not None else chain_seconds) / elapsed
     TB = TRACE_BYTES * (2 if args.precision == "fp64" else 1)
     achieved = TB * n * secs / (kmean / 1e3) / 1e9
+    launch_secs = min(win, secs)
+    rec = pmc_record(args, n, launch_secs)
+    kms_launch = kmean / nwin                              # one expand launch (one window)
+
+    def valu(ms):
+        if rec is None or not ms or ms != ms:
+            return None
+        a = rec["valu_insts_per_launch"] * 64 / (ms / 1e3) / 1e12
+        return {"achieved": a, "peak": VALU_PEAK_TLANE, "unit": "T lane-ops/s", "frac": a / VALU_PEAK_TLANE,
+                "valu_per_chain_second": rec["valu_insts_per_launch"] * 64 / (n * launch_secs),
+                "salu_per_chain_second": rec["salu_insts_per_launch"] * 64 / (n * launch_secs)}
+
+    if args.mode == "trace":
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": rec["traffic_bytes_per_launch"] if rec else None,
+                "kernel": "expand_kernel (P2, " + sim.path + ")", "kernel_ms": kmean,
+                "bytes_per_launch": TB * n * secs,
+                # the same launch with no other batch in flight (one extra batch after the timed region)
+                "alone": {"kernel_ms": alone_ms, "achieved": TB * n * secs / (alone_ms / 1e3) / 1e9,
+                          "frac": TB * n * secs / (alone_ms / 1e3) / 1e9 / HBM_PEAK_GBS},
+                "valu": valu(kms_launch)}
+    else:
+        v = valu(kms_launch) or {}
+        roof = {"bound": "valu", "achieved": v.get("achieved"), "peak": VALU_PEAK_TLANE, "unit": "T lane-ops/s",
+                "frac": v.get("frac"), "traffic": rec["traffic_bytes_per_launch"] if rec else None,
+                "kernel": "expand_kernel (P2, " + sim.path + ")", "kernel_ms": kms_launch,
+                "launches_per_batch": nwin, "chain_seconds_per_launch": n * launch_secs,
+                "valu_per_chain_second": v.get("valu_per_chain_second"),
+                "salu_per_chain_second": v.get("salu_per_chain_second"),
+                "source": "VALU lane-ops = SQ_INSTS_VALU x 64 per launch (profiles/pmc_kernels.json) / HIP-event "
+                          "launch time" if rec else "no PMC record for this workload in profiles/pmc_kernels.json"}
     line = {
         "metric": "simulated chain-seconds/sec (node) at 1/2/4/8 GPUs + % HBM roofline",
         "value": value, "unit": "chain-seconds/s", "n_gpus": world, "steps": args.steps,
@@ -462,17 +521,8 @@ def main():
                    "batches_in_flight": len(ctxs), "staggered": bool(args.stagger and nwin == 1),
                    "construction_on": args.build_on, "walk_priority": args.walk_priority,
                    "schedule": args.schedule if (args.stagger and nwin == 1 and len(ctxs) >= 3) else None},
-        "roofline": ({"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic(args, n, secs),
-                      "kernel": "expand_kernel (P2, " + sim.path + ")", "kernel_ms": kmean,
-                      "bytes_per_launch": TB * n * secs,
-                      # the same launch with no other batch in flight (one extra batch after the timed region)
-                      "alone": {"kernel_ms": alone_ms, "achieved": TB * n * secs / (alone_ms / 1e3) / 1e9,
-                                "frac": TB * n * secs / (alone_ms / 1e3) / 1e9 / HBM_PEAK_GBS}}
-                     if args.mode == "trace" else
-                     {"bound": "valu", "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None,
-                      "kernel": "expand_kernel (P2, " + sim.path + ")", "kernel_ms": kmean,
-                      "note": "stats mode stores no trace; VALU counters under profiles/"}),
+        "roofline": roof,
+        "chain_seconds_total": chain_seconds, "chain_seconds_live": live,
         "phases_ms": phases,
         # whole-pipeline rate: trace bytes of all batches / wall time (kernels overlap across batches)
         "effective_trace_gbs": (TB * n * secs / (elapsed / args.steps) / 1e9) if args.mode == "trace" else None,

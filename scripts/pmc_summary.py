@@ -1,59 +1,100 @@
-"""Summarise rocprofv3 --pmc passes (scripts/pmc.sh) per kernel: mean per dispatch.
-FETCH_SIZE/WRITE_SIZE are in KB (rocprofv3 derived counters); on gfx950 FETCH_SIZE
-reads half the bytes of wide streaming loads (MI355X_MICROARCH.md, HBM)."""
+"""Summarise rocprofv3 --pmc passes (scripts/pmc.sh, scripts/pmc_workload.sh) per
+kernel: mean per dispatch.  FETCH_SIZE/WRITE_SIZE are in KiB (rocprofv3 derived
+counters); on gfx950 FETCH_SIZE reads half the bytes of wide streaming loads
+(MI355X_MICROARCH.md, HBM), so it is doubled before it is called traffic.
+
+  python3 scripts/pmc_summary.py DIR                  print the per-kernel means
+  python3 scripts/pmc_summary.py DIR --record K=V ... upsert the dominant expand
+        kernel's record into profiles/pmc_kernels.json (keys: workload, chains,
+        launch_seconds, precision, mode, cc), which bench.py reads
+"""
 import collections
 import csv
 import glob
+import json
+import os
 import re
 import sys
 
-KERNELS = ["expand_kernel<float>", "expand_kernel<double>", "segments_kernel", "minute_table_kernel", "fixup_kernel",
-           "init_kernel", "geom_kernel", "event_draws_kernel", "events_kernel", "desc_kernel", "commit_kernel",
-           "chain_kernel"]
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def key(name):
-    for k in KERNELS:
-        if k.split("<")[0] in name and (("<" not in k) or k.split("<")[1][:-1] in name):
-            return k
-    return None
+def short(name):
+    """'void (anonymous namespace)::expand_kernel<float, 1, false>(...)' -> 'expand_kernel<float, 1, false>'"""
+    n = name.replace("void ", "").replace("(anonymous namespace)::", "").replace("tmh::", "")
+    depth, out = 0, []
+    for ch in n:
+        if ch == "(" and depth == 0:
+            break
+        depth += ch == "<"
+        depth -= ch == ">"
+        out.append(ch)
+    return re.sub(r"\s+", " ", "".join(out)).strip()
 
 
-def main(d):
+def main(d, quiet=False):
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(lambda: collections.defaultdict(set))
-    for f in glob.glob(f"{d}/p*/*counter_collection.csv"):
+    for f in glob.glob(f"{d}/p*/*counter_collection.csv") + glob.glob(f"{d}/p*/*/*counter_collection.csv"):
         for r in csv.DictReader(open(f)):
-            k = key(r["Kernel_Name"])
-            if k:
-                agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
-                disp[k][r["Counter_Name"]].add((f, r["Dispatch_Id"]))
+            k = short(r["Kernel_Name"])
+            agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            disp[k][r["Counter_Name"]].add((f, r["Dispatch_Id"]))
     out = {}
-    for k, d2 in agg.items():
+    for k, d2 in sorted(agg.items()):
         out[k] = {c: v / len(disp[k][c]) for c, v in d2.items()}
-        print(k)
-        print("   " + ", ".join(f"{c}={v:.4g}" for c, v in sorted(out[k].items())))
+        out[k]["_dispatches"] = max(len(s) for s in disp[k].values())
+        if not quiet:
+            print(k)
+            print("   " + ", ".join(f"{c}={v:.4g}" for c, v in sorted(out[k].items())))
     return out
 
 
-if __name__ == "__main__":
-    main(sys.argv[1])
-
-
-def write_traffic(d, chains, seconds, precision="fp32", mode="trace", kernel="expand_kernel<float>", out=None):
-    """profiles/pmc_traffic.json: HBM bytes per launch of the bench's dominant kernel.
-    FETCH_SIZE / WRITE_SIZE are KiB; FETCH_SIZE is doubled (gfx950 reports half the
-    bytes of wide streaming reads, MI355X_MICROARCH.md § HBM)."""
-    import json
-    import os
-    s = main(d)[kernel]
-    fetch = s["FETCH_SIZE"] * 1024 * 2
-    write = s["WRITE_SIZE"] * 1024
-    rec = {"kernel": kernel, "chains": chains, "seconds": seconds, "precision": precision, "mode": mode,
-           "fetch_bytes_corrected": fetch, "fetch_size_kib_raw": s["FETCH_SIZE"], "write_bytes": write,
-           "traffic_bytes_per_launch": fetch + write, "algorithmic_bytes_per_launch": 12 * chains * seconds,
-           "source": os.path.basename(os.path.normpath(d))}
-    out = out or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
-                              "pmc_traffic.json")
-    json.dump(rec, open(out, "w"), indent=1)
+def record(d, **key):
+    """profiles/pmc_kernels.json: the expand kernel's per-launch counters on one workload."""
+    s = main(d, quiet=True)
+    exp = [k for k in s if k.startswith("expand_kernel<")]
+    if not exp:
+        raise SystemExit(f"no expand_kernel dispatch in {d}")
+    k = max(exp, key=lambda k: s[k].get("SQ_WAVES", 0) * s[k]["_dispatches"])
+    c = s[k]
+    rec = dict(key)
+    rec.update(kernel=k, dispatches=c["_dispatches"], source=os.path.basename(os.path.normpath(d)))
+    for name, cn in (("valu_insts_per_launch", "SQ_INSTS_VALU"), ("salu_insts_per_launch", "SQ_INSTS_SALU"),
+                     ("trans_f32_insts_per_launch", "SQ_INSTS_VALU_TRANS_F32"), ("waves_per_launch", "SQ_WAVES"),
+                     ("wave_cycles", "SQ_WAVE_CYCLES"), ("wait_any", "SQ_WAIT_ANY"),
+                     ("wait_inst_any", "SQ_WAIT_INST_ANY"), ("active_inst_any", "SQ_ACTIVE_INST_ANY"),
+                     ("active_inst_valu", "SQ_ACTIVE_INST_VALU")):
+        if cn in c:
+            rec[name] = c[cn]
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        rec["fetch_bytes_corrected"] = c["FETCH_SIZE"] * 1024 * 2
+        rec["write_bytes"] = c["WRITE_SIZE"] * 1024
+        rec["traffic_bytes_per_launch"] = rec["fetch_bytes_corrected"] + rec["write_bytes"]
+    path = os.path.join(ROOT, "profiles", "pmc_kernels.json")
+    try:
+        db = json.load(open(path))
+    except (OSError, ValueError):
+        db = {"note": "per-launch PMC means of the dominant expand kernel per bench workload "
+                      "(scripts/pmc_workload.sh); SQ_* are wave-instruction counts summed over the chip",
+              "records": []}
+    ident = ("workload", "chains", "launch_seconds", "precision", "mode", "cc")
+    db["records"] = [r for r in db["records"] if any(r.get(i) != rec.get(i) for i in ident)] + [rec]
+    json.dump(db, open(path, "w"), indent=1)
     return rec
+
+
+def _val(v):
+    try:
+        return int(v)
+    except ValueError:
+        return v
+
+
+if __name__ == "__main__":
+    if "--record" in sys.argv:
+        i = sys.argv.index("--record")
+        kv = dict(a.split("=", 1) for a in sys.argv[i + 1:])
+        print(json.dumps(record(sys.argv[1], **{k: _val(v) for k, v in kv.items()}), indent=1))
+    else:
+        main(sys.argv[1])
