@@ -50,7 +50,9 @@ extern "C" {
 #define TMH_CHAIN_ASSERT_BINARY 2   /* cloud_cover_binary.py:90-98 (assert not recurse) */
 #define TMH_CHAIN_SIGMA_OVERFLOW 3  /* sigma arrays exceed TMH_SIGMA_CAP (no reference analogue) */
 #define TMH_CHAIN_U_EXHAUSTED 4     /* injected uniform stream ran out */
-#define TMH_CHAIN_SEGMENT_OVERFLOW 5 /* > n_steps/8 + 64 cloud segments in one window (time-parallel path) */
+#define TMH_CHAIN_SEGMENT_OVERFLOW 5 /* > n_steps/64 + 256 + 2,048 cloud segments in one window, or the
+                                         window's shared overflow pool (n/16 + 8 chunks of 256) is full
+                                         (time-parallel path) */
 #define TMH_CHAIN_GUARD_OVERFLOW 6   /* fp32 guard-band records of the batch exceeded their room (never observed; time-parallel path) */
 
 /* ---- modes ---- */
@@ -150,6 +152,11 @@ int tmh_state_offsets(uint32_t n_chains, uint64_t* offsets);
 size_t tmh_plan_bytes(uint32_t n_steps);
 size_t tmh_scratch_bytes(uint32_t n_chains, uint32_t n_steps);
 size_t tmh_workspace_bytes(uint32_t n_chains, uint32_t n_steps);
+/* Tests only: segment records kept per chain (a multiple of 16; 0 = the default
+ * n_steps/64 + 256) and the overflow pool's chunks (0 = n_chains/16 + 8), for
+ * every later tmh_scratch_bytes / launch in this process.  Exercises the
+ * overflow path, which the default sizes reach only on the windiest days. */
+int tmh_test_set_segment_capacity(uint32_t cap, uint32_t pool_chunks);
 
 int tmh_engine_create(const tmh_params* params, const tmh_clock* clock, int device,
                       struct tmh_engine** out);
@@ -172,7 +179,9 @@ int tmh_engine_path(const struct tmh_engine* eng);
  * (then tmh_params.shape_is_t).  Row i serves the chain at index i of the
  * tmh_init / tmh_run batch (chain0 + i), so n_chains must cover the batch.
  * The buffers are read by every later launch and must outlive them; shapes ==
- * NULL restores the single table.  Both cc modes and both kernel paths. */
+ * NULL restores the single table; shapes must be 16-byte aligned (the markov
+ * kernel stages each workgroup's rows in LDS with 16-B loads; TMH_E_INVAL
+ * otherwise).  Both cc modes and both kernel paths. */
 int tmh_set_shape_tables(struct tmh_engine* eng, const double* shapes, const int32_t* is_t,
                          uint32_t n_chains);
 

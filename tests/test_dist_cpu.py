@@ -8,7 +8,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from tmhpvsim_amd.dist import all_reduce_stats, shard
+from tmhpvsim_amd.dist import all_reduce_stats, shard, simulate_stats
 
 
 def _free_port():
@@ -82,3 +82,55 @@ def test_all_reduce_stats_single_process_is_identity():
     assert torch.equal(out["hist"], t["hist"])
     assert float(out["peak_residual"]) == float(t["peak_residual"])
     assert float(out["energy_pv"]) == float(t["energy_pv"])
+
+
+# ---- simulate_stats end to end on CPU: each rank's shard simulated by the C oracle
+# (test infrastructure standing in for the GPU runner), reduced over gloo; the node
+# totals must equal one unsharded run (histogram bit for bit)
+SIM = dict(start="2019-09-05 09:00:00", n_steps=7200, tz="Europe/Berlin")
+
+
+def oracle_shard(chain0, n, start, n_steps, tz, params, precision, window, n_bins, lo, hi, device):
+    from oracle import oracle as O
+    from tmhpvsim_amd.params import ModelParams
+    ref = O.run(params or ModelParams(), chain0, n, n_steps, start, tz=tz, outputs=(),
+                stats=dict(n_bins=n_bins, lo=lo, hi=hi))
+    ok = ref["status"] == 0
+    acc = torch.as_tensor(ref["acc"])
+    tot = dict(energy_pv=acc[ok, 0].sum(), energy_meter=acc[ok, 1].sum(), energy_residual=acc[ok, 2].sum(),
+               peak_residual=acc[ok, 3].max(), hist=torch.as_tensor(ref["hist"].astype(np.int64).sum(0)))
+    return tot, ref["status"]
+
+
+def _sim_worker(rank, world, port, n_total, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tot, bad = simulate_stats(n_total, runner=oracle_shard, **SIM)
+        q.put((rank, {k: v.numpy().copy() for k, v in tot.items()}, bad))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_simulate_stats_sharded_equals_unsharded():
+    world, n_total = 2, 101          # odd: the shards differ in size
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sim_worker, args=(r, world, port, n_total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (t, b) for r, t, b in (q.get(timeout=300) for _ in procs)}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    one, bad1 = simulate_stats(n_total, runner=oracle_shard, **SIM)       # world 1: no process group
+    assert int(one["hist"].sum()) > 0
+    for r in range(world):
+        got, bad = res[r]
+        assert bad == bad1
+        np.testing.assert_array_equal(got["hist"], one["hist"].numpy())   # bit for bit
+        assert float(got["peak_residual"]) == float(one["peak_residual"])
+        for k in ("energy_pv", "energy_meter", "energy_residual"):       # fp64 sums in another order
+            assert float(got[k]) == pytest.approx(float(one[k]), rel=1e-12)

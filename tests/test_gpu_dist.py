@@ -1,0 +1,42 @@
+"""The multi-GPU stats path on the one test GPU: two ranks (gloo, both on cuda:0) run
+tmhpvsim_amd.dist.simulate_stats on their chain shards through the product path and
+all-reduce; the node totals equal one unsharded run (histogram bit for bit: keyed
+Philox makes every chain independent of the partition)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_simulate_stats_two_ranks_equal_one(tmp_path):
+    from tmhpvsim_amd.dist import simulate_stats
+    n_total, n_steps, world = 777, 6 * 3600, 2          # 3 day-windows of 7,200 s, odd shard sizes
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(world))
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "_dist_gpu_worker.py"), str(n_total), str(n_steps),
+                               str(tmp_path)], env=dict(env, RANK=str(r), LOCAL_RANK=str(r))) for r in range(world)]
+    for p in procs:
+        assert p.wait(timeout=240) == 0
+    one, bad1 = simulate_stats(n_total, "2019-09-05 06:00:00", n_steps, tz="Europe/Berlin", device="cuda:0",
+                               window=7200)
+    want = {k: v.cpu().numpy() for k, v in one.items()}
+    assert want["hist"].sum() > 0 and want["energy_pv"] > 0
+    for r in range(world):
+        got = np.load(tmp_path / f"rank{r}.npz")
+        assert int(got["bad"]) == bad1
+        np.testing.assert_array_equal(got["hist"], want["hist"])
+        assert float(got["peak_residual"]) == float(want["peak_residual"])
+        for k in ("energy_pv", "energy_meter", "energy_residual"):
+            assert float(got[k]) == pytest.approx(float(want[k]), rel=1e-12)

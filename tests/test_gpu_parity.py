@@ -410,3 +410,38 @@ def test_c2_full_size_properties():
         ref = O.run(ModelParams(), c, 1, steps, start, tz=tz)
         np.testing.assert_array_equal(_np(out["covered"][:, cols[c]]), ref["covered"][:, 0])
         assert _rel(_np(out["csi"][:, cols[c]]), ref["csi"][:, 0]).max() <= 1e-5
+
+
+def test_segment_overflow_pool():
+    """Segment records past a chain's row go to the shared overflow pool (the windy
+    tail of cloud_cover_binary.py:80-107's call count): with the row cut to 16
+    records every chain spills ~24 chunks' worth, and the outputs stay bit-identical;
+    with a pool too small for them, the chains that got no chunk end with
+    TMH_CHAIN_SEGMENT_OVERFLOW (5) and every other chain is unchanged."""
+    from tmhpvsim_amd import _lib
+    L = _lib.load()
+    n, steps, start = 256, 86400, "2019-09-05 00:00:00"
+
+    def run():
+        s = _sim(n, start, tz="Europe/Berlin", prec="fp32", kernel_path="time_parallel", horizon=steps)
+        out = s.run(steps, trace=("covered", "pv"))
+        torch.cuda.synchronize()
+        return s.status(), _np(out["covered"]), _np(out["pv"])
+
+    st0, cov0, pv0 = run()
+    try:
+        _lib.check(L.tmh_test_set_segment_capacity(16, 4 * n))
+        st1, cov1, pv1 = run()
+        _lib.check(L.tmh_test_set_segment_capacity(16, 40))
+        st2, cov2, pv2 = run()
+    finally:
+        L.tmh_test_set_segment_capacity(0, 0)
+    np.testing.assert_array_equal(st1, st0)
+    np.testing.assert_array_equal(cov1, cov0)
+    np.testing.assert_array_equal(pv1, pv0)
+    hit = (st2 == 5)
+    assert 0 < hit.sum() < n
+    keep = ~hit
+    np.testing.assert_array_equal(st2[keep], st0[keep])
+    np.testing.assert_array_equal(cov2[:, keep], cov0[:, keep])
+    np.testing.assert_array_equal(pv2[:, keep], pv0[:, keep])

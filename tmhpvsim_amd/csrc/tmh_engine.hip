@@ -59,9 +59,20 @@ struct BlockDesc {                 // as of the step before the block start; -1 
     int32_t h2;                    // event index of the third-last hour boundary
 };
 
+// Segment records: a chain's first `cap` records sit in its row of `rec`; records
+// past that go to 256-record chunks of a shared overflow pool, allocated by the
+// walk (atomic counter) and listed per chain in `ovf` (OVF_SLOTS chunks).  cap is
+// sized to ~4x the mean calls per window (~387 a day), so the pool
+// serves the windy tail; only a chain past cap + 256 OVF_SLOTS records, or a
+// full pool, ends with TMH_CHAIN_SEGMENT_OVERFLOW.
+constexpr int OVF_SLOTS = 8, OVF_CHUNK = 256;
 struct SegView {                   // P1 -> P2 scratch
     int2* rec;                     // [n][cap] (first uncovered step, next call step), global steps
-    uint32_t cap;
+    uint32_t cap;                  // a multiple of 16 (the walk flushes records in groups of 16)
+    int32_t* ovf;                  // [n][OVF_SLOTS] pool chunk of the chain's records cap + 256 k ..
+    int2* pool;                    // [pool_cap][OVF_CHUNK]
+    uint32_t pool_cap;
+    uint32_t* pool_n;              // chunks handed out (zeroed by the draws phase)
     uint32_t* count;               // [n]
     int32_t* fault;                // [n] window-relative fault step (INT_MAX = none)
     uint32_t* status;              // [n] status after the window
@@ -99,6 +110,15 @@ struct PrevView {
     const uint32_t* status;
     const double* end_p1;   // [4][n]: cc before/after, ws before/after
 };
+
+// record i of chain c (its row, or its overflow chunks)
+__device__ __forceinline__ int2 rec_at(const SegView& sg, uint32_t c, uint32_t i)
+{
+    if (i < sg.cap) return sg.rec[(size_t)c * sg.cap + i];
+    const uint32_t o = i - sg.cap;
+    const int32_t ch = sg.ovf[(size_t)c * OVF_SLOTS + o / OVF_CHUNK];
+    return sg.pool[(size_t)ch * OVF_CHUNK + o % OVF_CHUNK];
+}
 
 
 // ------------------------------------------------------------ state I/O
@@ -482,21 +502,72 @@ __global__ __launch_bounds__(256) void event_draws_kernel(DrawParams dp, uint64_
 // window's hour events in order and fills evd[e][0] for the time-parallel
 // kernels.  The state is the last drawn cc, i.e. sa[S_CC] (init and every
 // _next_hour push the markov state), so nothing extra is carried over.
-__global__ __launch_bounds__(256) void markov_cc_kernel(KParams kp, StateView st, uint64_t chain0, uint32_t n,
+//
+// Per-chain tables (C5's lat/lon sweep): the workgroup's 256 rows of shape
+// parameters ([256][6][4] fp64 + [256][6] Student-t flags, 54 KB, one contiguous
+// range of the caller's table) are staged in LDS once with coalesced 16-B loads,
+// so each hourly draw reads its bin's four parameters from LDS instead of a
+// scattered 32-B global read per chain-hour.  The bin select (np.searchsorted on
+// the shared right edges, :309) is branch-free per lane, and the two quantile
+// families are taken as wave-uniform branches on a wave64 ballot of the lanes'
+// Student-t flags (bin 2 of the reference's table, cloud_cover_hourly.py:314),
+// so a wave whose lanes all sit in AL bins never enters stdtrit.
+constexpr int MK_BLOCK = 256;
+__global__ __launch_bounds__(MK_BLOCK) void markov_cc_kernel(KParams kp, StateView st, uint64_t chain0, uint32_t n,
                                                         uint32_t nsteps, const int2* __restrict__ events,
                                                         const uint32_t* __restrict__ n_events, double* evd,
                                                         PrevView prev)
 {
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ double2 tab_s[MK_BLOCK * 12];   // [chain][bin][4] fp64, as double2 pairs
+    __shared__ int32_t tabt_s[MK_BLOCK * 6];
+    const uint32_t cb0 = blockIdx.x * MK_BLOCK;
+    const uint32_t nb = min((uint32_t)MK_BLOCK, n - cb0);
+    if (kp.tab) {   // the block's rows are one contiguous range: coalesced 16-B loads
+        const double2* src = reinterpret_cast<const double2*>(kp.tab + (size_t)cb0 * 24);
+        for (uint32_t i = threadIdx.x; i < nb * 12; i += MK_BLOCK) tab_s[i] = src[i];
+        for (uint32_t i = threadIdx.x; i < nb * 6; i += MK_BLOCK)
+            tabt_s[i] = kp.tab_t ? kp.tab_t[(size_t)cb0 * 6 + i] : kp.is_t[i % 6];
+    }
+    __syncthreads();
+    const uint32_t c = cb0 + threadIdx.x;
     if (c >= n) return;
     const uint64_t chain = chain0 + c;
     const uint32_t ne = min(*n_events, ev_cap_dev(nsteps));
+    const double* row = kp.tab ? reinterpret_cast<const double*>(tab_s) + threadIdx.x * 24 : nullptr;
+    const int32_t* rowt = tabt_s + threadIdx.x * 6;
     double state = prev.status ? prev.end_p1[(size_t)n + c] : st.mstate[c];   // the last hourly draw
     for (uint32_t e = 0; e < ne; ++e) {
         const int2 ev = events[e];
         if (!(ev.y & FL_HOUR)) continue;
-        const U4 u = keyed_block(kp.seed, chain, (uint64_t)ev.x, TAG_BOUNDARY, 1);
-        state = draw_cc_from(kp, c, state, u52(u.x, u.y));
+        const U4 u4 = keyed_block(kp.seed, chain, (uint64_t)ev.x, TAG_BOUNDARY, 1);
+        const double u = u52(u4.x, u4.y);
+        int bin = 5;   // np.searchsorted(bins, state): the first bin whose right edge is >= state
+#pragma unroll
+        for (int k = 4; k >= 0; --k) bin = kp.edges[k] < state ? bin : k;
+        double loc, scale, kappa, df;
+        int is_t;
+        if (row) {
+            const double* sh = row + 4 * bin;
+            loc = sh[0];
+            scale = sh[1];
+            kappa = sh[2];
+            df = sh[3];
+            is_t = rowt[bin];
+        } else {
+            loc = kp.shapes[bin][0];
+            scale = kp.shapes[bin][1];
+            kappa = kp.shapes[bin][2];
+            df = kp.shapes[bin][3];
+            is_t = kp.is_t[bin];
+        }
+        const uint64_t tl = __builtin_amdgcn_ballot_w64(is_t != 0);
+        const uint64_t al = __builtin_amdgcn_ballot_w64(is_t == 0);
+        double v = 0.0;
+        if (tl && is_t) v = stdtrit(df, u);
+        if (al && !is_t) v = al_ppf(u, kappa);
+        v = v * scale + loc;                              // scipy rvs: vals * scale + loc
+        const double x = state + v;
+        state = x < 0.0 ? 0.0 : (x > 1.0 ? 1.0 : x);      // np.clip(., 0, 1)
         evd[(size_t)e * 4 * n + c] = state;
     }
 }
@@ -703,10 +774,9 @@ __device__ __forceinline__ bool redo_second(const KParams& kp, const DrawParams&
     sx.b[S_CLEAR_NOISE] = st.sb[S_CLEAR_NOISE][c];
     sx.a[S_CLEAR_NOISE] = st.sa[S_CLEAR_NOISE][c];
     exact_noise_at(d, dp, st, sg, n, c, chain0, W0, first_minute(utc0, W0), events, tab64, sx);
-    const int2* rec = sg.rec + (size_t)c * sg.cap;   // the segment holding the step: first next-call step > step,
-    uint32_t k = jr_end;                             // at or before the one of the block's last step
-    while (k > 0 && (int64_t)rec[k - 1].y > step) --k;
-    const bool covered = step < (int64_t)rec[k].x;
+    uint32_t k = jr_end;   // the segment holding the step: first next-call step > step, at or before the block's last
+    while (k > 0 && (int64_t)rec_at(sg, c, k - 1).y > step) --k;
+    const bool covered = step < (int64_t)rec_at(sg, c, k).x;
     const U4 pb = keyed_block(kp.seed, chain0 + c, (uint64_t)step >> 1, TAG_STEP2, 0);
     const bool odd = step & 1;
     LaneSite ls{};
@@ -951,6 +1021,7 @@ __global__ __launch_bounds__(256) void candidates_kernel(DrawParams dp, StateVie
 {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t k = blockIdx.y;
+    if (c == 0 && k == 0) *sg.pool_n = 0;   // the walk that follows hands out the overflow chunks
     if (c >= n || (prev.status ? prev.status[c] : st.status[c]) != 0) return;
     const U4 b = keyed_block(dp.seed, chain0 + c, (uint64_t)(st.ncalls[c] + k), TAG_CLOUD, 0);
     sg.cand[(size_t)k * n + c] = pow_d(dp.alpha + dp.delta * u52(b.x, b.y), dp.expo);
@@ -1076,13 +1147,17 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
     int2* rec = sg.rec + (size_t)cs * sg.cap;
     int rb_x = 0, rb_y = 0;       // record buffer: lane p = record rbase + p
     uint32_t rbase = 0;
+    int32_t chunk = 0;            // the overflow chunk of records >= cap (row-uniform)
+    auto group_at = [&](uint32_t b) {   // where the record group starting at b goes
+        return b < sg.cap ? rec + b : sg.pool + (size_t)chunk * OVF_CHUNK + (b - sg.cap) % OVF_CHUNK;
+    };
     auto put_rec = [&](uint32_t i, int x, int y) {
         const uint32_t slot = i - rbase;
         const bool mine = (uint32_t)p == slot;
         rb_x = mine ? x : rb_x;
         rb_y = mine ? y : rb_y;
         if (slot == 15) {
-            rec[rbase + p] = make_int2(rb_x, rb_y);
+            group_at(rbase)[p] = make_int2(rb_x, rb_y);
             rbase += 16;
         }
     };
@@ -1308,11 +1383,23 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
         clr = nclr;
         s_start = e;
         e = s_start + ceil_thr(cl + clr) - 1;
-        if (nrec >= sg.cap) {
-            status = TMH_CHAIN_SEGMENT_OVERFLOW;
-            fault = (int32_t)(s_start - W0);
-            active = false;
-            continue;
+        if (nrec >= sg.cap && (nrec - sg.cap) % OVF_CHUNK == 0) {   // a new overflow chunk (windy tail)
+            const uint32_t k = (nrec - sg.cap) / OVF_CHUNK;
+            int got = -1;
+            if (k < OVF_SLOTS) {
+                int v = 0;
+                if (p == 0) v = (int)atomicAdd(sg.pool_n, 1u);
+                got = __builtin_amdgcn_ds_bpermute(row0 << 2, v);   // the whole row is active here
+                if ((uint32_t)got >= sg.pool_cap) got = -1;
+                else if (p == 0) sg.ovf[(size_t)c * OVF_SLOTS + k] = got;
+            }
+            if (got < 0) {
+                status = TMH_CHAIN_SEGMENT_OVERFLOW;
+                fault = (int32_t)(s_start - W0);
+                active = false;
+                continue;
+            }
+            chunk = got;
         }
         put_rec(nrec, (int)(s_start + ceil_thr(cl) - 1), (int)e);
         ++nrec;
@@ -1324,7 +1411,7 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
         for (int i = 0; i < 8; ++i) g_p1diag[w * 8 + i] = dg[i];
     }
 #endif
-    if (live && (uint32_t)p < nrec - rbase) rec[rbase + p] = make_int2(rb_x, rb_y);   // partial record group
+    if (live && (uint32_t)p < nrec - rbase) group_at(rbase)[p] = make_int2(rb_x, rb_y);   // partial record group
     if (!live) return;
     if (status == 0) {
         while (next_ev <= W1 - 1) {   // remaining boundaries of the window
@@ -1402,8 +1489,8 @@ __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t rs, uint32_t of
 #ifndef TMH_EXP_WAVES   // min waves per SIMD of the fp32 single-site expansion: 7 = at most 72 VGPRs (alone -4 % vs 6, no VGPR spills)
 #define TMH_EXP_WAVES 7
 #endif
-#ifndef TMH_EXP_WAVES_STATS   // the same for the statistics / other outputs (C3, C4): 6 = 80 VGPRs
-#define TMH_EXP_WAVES_STATS 6
+#ifndef TMH_EXP_WAVES_STATS   // the same for the statistics / other outputs (C3, C4): 5 = 96 VGPRs (their 16-KB LDS histogram + 12 KB staging allow 5 workgroups per CU anyway)
+#define TMH_EXP_WAVES_STATS 5
 #endif
 template <typename R, int OUT, bool SITES>
 #ifndef TMH_SITES_WAVES   // min waves per SIMD of the per-chain-site expansion: 2 (a few spills) is 35 % faster than 1
@@ -1449,7 +1536,6 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
     Acc acc{0.0, 0.0, 0.0, -INFINITY};
     bool alive = false;
     int32_t fault = INT_MAX;
-    const int2* rec = sg.rec + (size_t)(live ? c : 0) * sg.cap;
     uint32_t jr = 0, evi = 0;
     FSamp<R> fs;
     const MinuteCtx mc{dp, chain, W0, fm, events, (int)min(*n_events, ev_cap_dev(nsteps)), tab64};
@@ -1490,11 +1576,11 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
             const int last = hi;
             while (lo < hi) {
                 const int mid = (lo + hi) >> 1;
-                if (rec[mid].y > s0i) hi = mid;
+                if (rec_at(sg, c, mid).y > s0i) hi = mid;
                 else lo = mid + 1;
             }
             // covered iff step < x of the segment holding it: [start, min(x, y)) per segment
-            int2 r = rec[lo];
+            int2 r = rec_at(sg, c, lo);
             int32_t a = s0i;
             for (;;) {
                 const int32_t e = min(min(r.x, r.y), s1i);
@@ -1507,7 +1593,7 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
                 }
                 if (r.y >= s1i || lo >= last) break;
                 a = max(a, r.y);
-                r = rec[++lo];
+                r = rec_at(sg, c, ++lo);
             }
             jr = (uint32_t)lo;   // the segment of the block's last step (fixup_kernel walks back from it)
         }
@@ -1928,7 +2014,11 @@ size_t plan_layout(uint32_t n_steps, void* base, PlanView* v)
     return o;
 }
 
-uint32_t seg_cap(uint32_t n_steps) { return n_steps / 8 + 64; }
+// ~4.2x the mean next_cloud calls of a window (~387 a day, max 806 in 16,384
+// chain-days measured with the oracle), a multiple of 16; the pool takes the rest
+uint32_t g_cap_override = 0, g_pool_override = 0;   // tmh_test_set_segment_capacity (tests only)
+uint32_t seg_cap(uint32_t n_steps) { return g_cap_override ? g_cap_override : (n_steps / 64 + 256 + 15) & ~15u; }
+uint32_t pool_chunks(uint32_t n) { return g_pool_override ? g_pool_override : n / 16 + 8; }
 // (chain, block)s with a guard-band second of the fp32 PV chain: ~1e-5 of the
 // chain-seconds are such seconds, ~1.3e-3 of the blocks; room for 1/16
 uint32_t fix_cap(uint32_t n, uint32_t n_steps) { return (uint32_t)((uint64_t)n * nblk_of(n_steps) / 16) + 1024; }
@@ -1944,6 +2034,15 @@ size_t scratch_layout(uint32_t n, uint32_t n_steps, void* base, SegView* v)
         v->rec = (int2*)(b + o);
     }
     o += align_up((size_t)n * seg_cap(n_steps) * 8);
+    if (v) {
+        v->ovf = (int32_t*)(b + o);
+        v->pool_cap = pool_chunks(n);
+    }
+    o += align_up((size_t)n * OVF_SLOTS * 4);
+    if (v) v->pool = (int2*)(b + o);
+    o += align_up((size_t)pool_chunks(n) * OVF_CHUNK * 8);
+    if (v) v->pool_n = (uint32_t*)(b + o);
+    o += ALIGN;
     if (v) v->count = (uint32_t*)(b + o);
     o += align_up((size_t)n * 4);
     if (v) v->fault = (int32_t*)(b + o);
@@ -2207,6 +2306,7 @@ int tmh_set_shape_tables(struct tmh_engine* eng, const double* shapes, const int
 {
     if (!eng) return fail(TMH_E_INVAL, "NULL engine");
     if (shapes && n_chains == 0) return fail(TMH_E_INVAL, "per-chain shape tables with n_chains 0");
+    if ((uintptr_t)shapes & 15) return fail(TMH_E_INVAL, "shape tables must be 16-byte aligned (staged as 16-B loads)");
     eng->kp.tab = eng->dp.tab = shapes;
     eng->kp.tab_t = eng->dp.tab_t = shapes ? is_t : nullptr;
     eng->n_tab = shapes ? n_chains : 0;
@@ -2238,6 +2338,14 @@ int tmh_diag_p1(uint64_t* out, uint32_t n)   // diagnostic build only
     return hip_check(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_p1diag), (size_t)n * 8), "diag copy");
 }
 #endif
+
+int tmh_test_set_segment_capacity(uint32_t cap, uint32_t pool_chunks)
+{
+    if (cap % 16) return fail(TMH_E_INVAL, "segment capacity %u is not a multiple of 16", cap);
+    g_cap_override = cap;
+    g_pool_override = pool_chunks;
+    return TMH_OK;
+}
 
 int tmh_profile_enable(struct tmh_engine* eng, int on)
 {
@@ -2410,15 +2518,15 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
                                    n_chains, step0, n_steps, fmh, pv.tab64, pv.events, pv.n_events, sg);
         }
     }
-#if TMH_EXP_CHAIN_FAST
-    dim3 grid2(nblk_of(n_steps) * cb);
-#else
-    dim3 grid2(nblk_of(n_steps), cb);
-#endif
     const bool no_stats = !sv.hist && !sv.acc;
     const int out = (no_stats && tv.pv && tv.meter && tv.residual && !tv.csi && !tv.covered) ? OUT_TRACE3
                     : (!tv.pv && !tv.meter && !tv.residual && !tv.csi && !tv.covered) ? OUT_STATS
                                                                                       : OUT_ANY;
+#if TMH_EXP_CHAIN_FAST
+    dim3 grid2(sg.nblk * cb);
+#else
+    dim3 grid2(sg.nblk, cb);
+#endif
     if (out == OUT_TRACE3 && tv.ld * (f64 ? 8u : 4u) * BLOCK_STEPS >= (1ull << 31))   // one block's rows: one buffer range
         return fail(TMH_E_INVAL, "trace ld %llu too large (a 128-step block of rows must stay under 2 GiB)",
                     (unsigned long long)tv.ld);

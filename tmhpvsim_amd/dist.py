@@ -46,18 +46,34 @@ def all_reduce_stats(tot: dict, group=None) -> dict:
 
 
 def simulate_stats(n_total, start, n_steps, tz=None, params=None, precision="fp32", window=86400,
-                   n_bins=4096, lo=-300.0, hi=9000.0, group=None, device=None):
-    """Node-wide stats run (C3/C4): this rank's shard of `n_total` chains, reduced over `group`."""
+                   n_bins=4096, lo=-300.0, hi=9000.0, group=None, device=None, runner=None):
+    """Node-wide stats run (C3/C4): this rank's shard of `n_total` chains, reduced over `group`.
+
+    Returns (totals, faulted): the all-reduced totals (histogram and energies
+    summed, peak a max; every rank gets them) and the node's count of faulted
+    chains.  `runner(chain0, n, **spec) -> (totals, status)` simulates one shard;
+    the default runs it on this rank's GPU (`BatchedSim`, stats mode, no trace).
+    """
+    import torch
     import torch.distributed as dist
-    from .engine import BatchedSim
 
     world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
     rank = dist.get_rank(group) if world > 1 else 0
     chain0, n = shard(n_total, rank, world)
+    spec = dict(start=start, n_steps=n_steps, tz=tz, params=params, precision=precision, window=window,
+                n_bins=n_bins, lo=lo, hi=hi, device=device)
+    tot, status = (runner or _gpu_shard)(chain0, n, **spec)
+    tot = all_reduce_stats(tot, group=group)
+    bad = torch.tensor([int((status != 0).sum())], dtype=torch.int64, device=tot["energy_pv"].device)
+    if world > 1:
+        dist.all_reduce(bad, op=dist.ReduceOp.SUM, group=group)
+    return tot, int(bad[0])
+
+
+def _gpu_shard(chain0, n, start, n_steps, tz, params, precision, window, n_bins, lo, hi, device):
+    from .engine import BatchedSim
     sim = BatchedSim(n, start, tz=tz, params=params, precision=precision, chain0=chain0, device=device,
                      horizon=n_steps)
     sim.enable_stats(n_bins=n_bins, lo=lo, hi=hi)
     sim.run(n_steps, trace=(), window=window)
-    tot = all_reduce_stats(sim.stats_totals(), group=group)
-    bad = int((sim.status() != 0).sum())
-    return tot, bad
+    return sim.stats_totals(), sim.status()
