@@ -1076,8 +1076,43 @@ __device__ __forceinline__ double bperm_f64(int src_lane, double v)
 #ifndef TMH_RCH
 #define TMH_RCH 4
 #endif
+#ifndef TMH_DOOM_SKIP   // skip provably rejected tries (bit-exact, GPU-tested; measured: walk +1-3 %, off)
+#define TMH_DOOM_SKIP 0
+#endif
+
+// True if, for the row's sigma arrays (lane-distributed: entry k = chunk k / 16,
+// lane k % 16), no cloud length a candidate can take (x / ws, x in the
+// power law's [xmin, xmax], cloud_cover_binary.py:35-40) makes any entry
+// possible (:83-87).  In real arithmetic entry k is possible for
+// ncl in (sl_k / f - sc_k, 5400 / (1 + f) - sc_k); the tests below keep a
+// relative margin of 1e-6, far above the few-ulp difference between these and
+// the fp64 predicate, so "doomed" never holds while some candidate could pass.
+// Entries past the register chunks (L > 16 RCH): not doomed (no shortcut).
+template <int NCH>
+__device__ __forceinline__ bool row_doomed(const double (&vc)[NCH], const double (&vl)[NCH], int L, int p, int row0,
+                                           double f, double ws, const DrawParams& dp)
+{
+    constexpr double m = 1e-6;
+    const double rws = 1.0 / ws;
+    const double cmin = dp.x_lo * rws * (1.0 - m), cmax = dp.x_hi * rws * (1.0 + m);
+    bool hope = L > 16 * NCH;
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+        const int k = ch * 16 + p;
+        const double sc = vc[ch], sl = vl[ch];
+        const bool h1 = sl * (1.0 + f) < 5400.0 * f * (1.0 + m);   // sl / f < 5400 / (1 + f)
+        const bool h2 = sl < f * (cmax + sc) * (1.0 + m);          // some ncl <= cmax passes nsl > sl
+        const bool h3 = (cmin + sc) * (1.0 + f) < 5400.0 * (1.0 + m);   // some ncl >= cmin passes tot < 5400
+        hope |= (k < L) & h1 & h2 & h3;
+    }
+    const uint64_t bal = __builtin_amdgcn_ballot_w64(hope);
+    return ((bal >> row0) & 0xFFFFull) == 0;
+}
 constexpr int RCH = TMH_RCH;   // register chunks of 16 entries: sigma entries 0..127 (all but ~1e-5 of calls)
-constexpr int RCH_FIXED = 4;   // chunks always processed (L <= 64 for 99.7 % of calls)
+#ifndef TMH_RCH_FIXED
+#define TMH_RCH_FIXED 4
+#endif
+constexpr int RCH_FIXED = TMH_RCH_FIXED;   // chunks always processed; chunk ch >= RCH_FIXED only when some row needs it
 
 // P1: segment walk.  Four chains per wavefront, one per row of 16 lanes; entry
 // k of a chain's sigma arrays lives in chunk k / 16, lane k % 16 of its row
@@ -1091,6 +1126,9 @@ constexpr int RCH_FIXED = 4;   // chunks always processed (L <= 64 for 99.7 % of
 // binary state.
 #ifndef TMH_SEG_WAVES
 #define TMH_SEG_WAVES 1
+#endif
+#ifndef TMH_RETRY_BATCH   // retry candidates 16 at a time across the row (measured: walk +3 %, off)
+#define TMH_RETRY_BATCH 0
 #endif
 #ifndef TMH_SEG_PRIO   // wave issue priority of the walk (s_setprio) over the expansion beside it
 #define TMH_SEG_PRIO 0
@@ -1255,13 +1293,35 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
         // ---- next_cloud: tries (cloud_cover_binary.py:82-98)
         int tries = 0, last = -1;
         double ncl = 0.0;
+#if TMH_RETRY_BATCH
+        // Retry candidates, 16 at a time: lane p of the row draws try tb + p's cloud
+        // length (keyed by the call and the try, so any lane can) and divides it by
+        // the row's wind speed; a retry then costs one bpermute instead of a
+        // Philox block, a pow and a division on all 16 lanes.  ~2 % of the calls
+        // reject 20 candidates in a row (reset_sigma), ~8 % at least one.
+        double nb = 0.0;
+        int tb = -16;
+#endif
         for (;;) {
+#if TMH_RETRY_BATCH
+            if (tries == 0 && x0 >= 0.0) ncl = x0 / ws;
+            else {
+                if (tries - tb >= 16) {   // row-uniform
+                    tb = tries;
+                    const int t = tries + p;
+                    nb = pow_d(dp.alpha + dp.delta * keyed_u(dp.seed, chain, ncall, TAG_CLOUD, (uint32_t)(t >> 1), t & 1),
+                               dp.expo) / ws;
+                }
+                ncl = bperm_f64(row0 | (tries - tb), nb);
+            }
+#else
             double x;
             if (tries == 0 && x0 >= 0.0) x = x0;
             else x = pow_d(dp.alpha + dp.delta * keyed_u(dp.seed, chain, ncall, TAG_CLOUD, (uint32_t)(tries >> 1),
                                                         tries & 1),
                            dp.expo);
             ncl = x / ws;
+#endif
             double bd = INFINITY;
             int bk = INT_MAX;
             auto scan = [&](int k, double sc, double sl) {   // :83-88, branch-free
@@ -1278,10 +1338,9 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
             // issue, bounds this loop); 4..7 only when some row has L > 64
 #pragma unroll
             for (int ch = 0; ch < RCH_FIXED; ++ch) scan(ch * 16 + p, vc[ch], vl[ch]);
-            if (Lmax > 16 * RCH_FIXED) {
 #pragma unroll
-                for (int ch = RCH_FIXED; ch < RCH; ++ch) scan(ch * 16 + p, vc[ch], vl[ch]);
-            }
+            for (int ch = RCH_FIXED; ch < RCH; ++ch)
+                if (Lmax > 16 * ch) scan(ch * 16 + p, vc[ch], vl[ch]);   // wave-uniform
             for (int ch = RCH; ch * 16 < L; ++ch) {   // rare: entries 128..
                 const int k = ch * 16 + p;
                 if (k < L) scan(k, gsc[k], gsl[k]);
@@ -1292,11 +1351,24 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
                 break;
             }
             ++tries;
-            if (tries == 20) {   // reset_sigma (cloud_cover_binary.py:76-78); 300 (k+1) is exact
-                const int nl = (int)(h * 12);
-                vc[0] = 300.0 * (p + 1);
-                vl[0] = f * vc[0];
-                L = nl;
+            for (;;) {
+                if (tries == 20) {   // reset_sigma (cloud_cover_binary.py:76-78); 300 (k+1) is exact
+                    const int nl = (int)(h * 12);
+                    vc[0] = 300.0 * (p + 1);
+                    vl[0] = f * vc[0];
+                    L = nl;
+                }
+#if TMH_DOOM_SKIP
+                // try 0 failed (or the sigma arrays were just reset): if no cloud length
+                // the candidates can take makes any entry possible, every try up to the
+                // reset (or the assert) is rejected -- skip them.  Tries are keyed by
+                // (call, try), so skipping changes no later draw.
+                if ((tries == 1 || tries == 20) && row_doomed(vc, vl, L, p, row0, f, ws, dp)) {
+                    tries = tries == 1 ? 20 : 40;
+                    continue;
+                }
+#endif
+                break;
             }
             if (tries == 40) break;
         }
@@ -1327,9 +1399,9 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
                 a = lc == ch ? vc[ch] : a;
                 b = lc == ch ? vl[ch] : b;
             }
-            if (topmax >= RCH_FIXED) {
 #pragma unroll
-                for (int ch = RCH_FIXED; ch < RCH; ++ch) {
+            for (int ch = RCH_FIXED; ch < RCH; ++ch) {
+                if (topmax >= ch) {   // wave-uniform
                     a = lc == ch ? vc[ch] : a;
                     b = lc == ch ? vl[ch] : b;
                 }
@@ -1354,9 +1426,9 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
             gsl[k] = f * nsc;
         }
         // rows with a lower top rewrite entries >= their new L: harmless
-        if (topmax >= RCH_FIXED) {
 #pragma unroll
-            for (int ch = RCH - 1; ch >= RCH_FIXED; --ch) {
+        for (int ch = RCH - 1; ch >= RCH_FIXED; --ch) {
+            if (topmax >= ch) {   // wave-uniform
                 const double sh = dpp_row_f64<0x111>(0.0, vc[ch]);
                 const double carry = dpp_row_f64<0x121>(0.0, vc[ch - 1]);
                 const double prev = p == 0 ? carry : sh;
@@ -2266,6 +2338,11 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
     d.delta = k.delta;
     d.expo = k.expo;
     d.sqrt09 = k.sqrt09;
+    {   // the candidates' cloud-length range (x at u = 1 and u = 0), for the walk's doomed-call test
+        const double xa = pow(k.alpha, k.expo), xb = pow(k.alpha + k.delta, k.expo);
+        d.x_lo = std::min(xa, xb);
+        d.x_hi = std::max(xa, xb);
+    }
     int fb = 0;   // bin of a fresh generator: searchsorted(edges, 1.0)
     while (fb < 5 && p->edges[fb] < 1.0) ++fb;
     d.fb_is_t = p->shape_is_t[fb];

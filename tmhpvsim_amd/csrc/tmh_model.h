@@ -372,6 +372,7 @@ __device__ uint32_t next_cloud_fresh(const KParams& kp, double* sc, double* sl, 
 struct DrawParams {
     uint64_t seed;
     double alpha, delta, expo, sqrt09;
+    double x_lo, x_hi;               // range of pow(alpha + delta u, expo) over u in [0, 1] (100 m, 1e6 m)
     double fb_k, fb_scale, fb_loc;   // the bin a fresh generator (state 1.0) draws from
     int32_t fb_is_t, fb_bin;
     const double* tab;               // per-chain shape tables (KParams::tab)
