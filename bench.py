@@ -79,6 +79,23 @@ def parse():
     ap.add_argument("--schedule", default="gated", choices=["gated", "stagger"],
                     help="pipelined one-window batches: 'gated' releases the expansion of batch k, the walk of "
                          "k + 1 and the construction of k + 2 together when walk k ends; 'stagger' is round 1's")
+    ap.add_argument("--walks", type=int, default=1,
+                    help="gated schedule: segment walks in flight on their own streams (each batch's walk "
+                         "overlaps the next one's; use with --walk-cpr > 1 so they share the CUs' walk slots)")
+    ap.add_argument("--walk-cpr", type=int, default=1,
+                    help="chains per walk row (tmh_set_walk_chains_per_row): the walk launches n / cpr rows "
+                         "that take the next chain when theirs is done")
+    ap.add_argument("--build-ahead", type=int, default=None,
+                    help="gated schedule: when the walk of batch k ends, the construction of batch k + A is "
+                         "released (default A = walks + 1; needs --pipeline >= A + 1)")
+    ap.add_argument("--build-priority", default="normal", choices=["high", "normal"],
+                    help="gated schedule: HIP stream priority of the construction stream")
+    ap.add_argument("--minutes-ahead", type=int, default=None,
+                    help="gated schedule: build each batch's minute table with its construction (1) instead of "
+                         "before its expansion on the expansion stream (0); default 1 when --walks > 1")
+    ap.add_argument("--commit-stream", type=int, default=None,
+                    help="gated schedule: each batch's fixup + commit on a stream of their own beside the next "
+                         "expansion (1) or after its expansion on the expansion stream (0); default 1 when --walks > 1")
     ap.add_argument("--pipeline", type=int, default=None,
                     help="batches in flight on separate HIP streams (1 = no overlap): the segment walks of the "
                          "next batches (latency-bound, one wave per SIMD) run beside this batch's expansion")
@@ -86,7 +103,12 @@ def parse():
     c5, c4 = a.workload == "c5", a.workload == "c4"
     a.chains = a.chains or {"c2": 4096, "c3": 1048576, "c4": 16384, "c5": 65536}[a.workload]
     a.seconds = a.seconds or {"c2": 86400, "c3": 86400, "c4": 365 * 86400, "c5": 604800}[a.workload]
-    a.pipeline = a.pipeline or (1 if a.workload == "c3" else 3)
+    a.build_ahead = a.build_ahead or max(1, a.walks) + 1
+    a.pipeline = a.pipeline or (1 if a.workload == "c3" else a.build_ahead + 1)
+    if a.minutes_ahead is None:
+        a.minutes_ahead = int(a.walks > 1)
+    if a.commit_stream is None:
+        a.commit_stream = int(a.walks > 1)
     a.mode = a.mode or ("trace" if a.workload == "c2" else "stats")
     a.cc = a.cc or ("markov" if c5 else "faithful")
     a.window = min(a.window or (86400 if (c5 or c4) else a.seconds), a.seconds)
@@ -189,6 +211,8 @@ def main():
     sim = BatchedSim(n, args.start, tz="Europe/Berlin", params=ModelParams(cc_mode=CC_MARKOV if args.cc == "markov" else 0),
                      precision=args.precision, chain0=rank * n, device=dev, horizon=secs, kernel_path=args.path, **kw)
     real = sim.real
+    if args.walk_cpr != 1:
+        _lib.check(L.tmh_set_walk_chains_per_row(sim._eng, args.walk_cpr))
 
     nwin = (secs + win - 1) // win
     prio_lo, prio_hi = torch.cuda.Stream.priority_range()
@@ -330,10 +354,16 @@ def main():
     # instead of queueing behind its 10,800 workgroups (a kernel launched while an
     # expansion fills the CUs waits for its tail: the walks then ran three at a time,
     # between expansions, rocprofv3 kernel trace r02).
-    wst = torch.cuda.Stream(dev, priority=prio_hi if args.walk_priority == "high" else prio_lo)
-    wst_p = C.c_void_p(wst.cuda_stream)
-    bst = torch.cuda.Stream(dev)
+    W = max(1, args.walks)
+    wsts = [torch.cuda.Stream(dev, priority=prio_hi if args.walk_priority == "high" else prio_lo) for _ in range(W)]
+    bst = torch.cuda.Stream(dev, priority=prio_hi if args.build_priority == "high" else prio_lo)
     bst_p = C.c_void_p(bst.cuda_stream)
+    A = args.build_ahead
+
+    def expand_args(cx):
+        return (sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs, None, C.byref(cx.tr),
+                C.byref(cx.st) if cx.st is not None else None, C.c_void_p(cx.plan.data_ptr()),
+                C.c_void_p(cx.scratch.data_ptr()), cx.scratch.numel())
 
     def g_build(j, gate):
         cx = ctxs[j % len(ctxs)]
@@ -347,39 +377,53 @@ def main():
         _lib.check(L.tmh_walk_part(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs,
                                    C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
                                    cx.scratch.numel(), None, 0, _lib.WALK_DRAWS, bst_p))
+        if args.minutes_ahead:   # the minute table needs the draws, not the walk
+            _lib.check(L.tmh_expand_part(*expand_args(cx), _lib.EXPAND_MINUTES, bst_p))
         cx.done.record(bst)
 
     def g_walk(j):
         cx = ctxs[j % len(ctxs)]
+        wst = wsts[j % W]
         wst.wait_event(cx.done)
         _lib.check(L.tmh_walk_part(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs,
                                    C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
-                                   cx.scratch.numel(), None, 0, _lib.WALK_SEGMENTS, wst_p))
+                                   cx.scratch.numel(), None, 0, _lib.WALK_SEGMENTS, C.c_void_p(wst.cuda_stream)))
         cx.walked.record(wst)
+
+    cst = torch.cuda.Stream(dev)
 
     def g_expand(j):
         cx = ctxs[j % len(ctxs)]
         estream.wait_event(cx.walked)
-        args_ = (sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs, None, C.byref(cx.tr),
-                 C.byref(cx.st) if cx.st is not None else None, C.c_void_p(cx.plan.data_ptr()),
-                 C.c_void_p(cx.scratch.data_ptr()), cx.scratch.numel())
-        _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_KERNEL, eptr))
-        _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_COMMIT, eptr))
+        args_ = expand_args(cx)
+        _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_KERNEL | (_lib.EXPAND_NO_MINUTES if args.minutes_ahead else 0),
+                                     eptr))
         if cx.expanded is None:
             cx.expanded = torch.cuda.Event()
-        cx.expanded.record(estream)
+        if args.commit_stream:   # fixup + commit beside the next expansion
+            cx.kernel_done.record(estream)
+            cst.wait_event(cx.kernel_done)
+            _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_COMMIT, C.c_void_p(cst.cuda_stream)))
+            cx.expanded.record(cst)
+        else:
+            _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_COMMIT, eptr))
+            cx.expanded.record(estream)
 
     def run_gated(k0, cnt):
+        """W walks in flight (W + 2 contexts): when the walk of batch k ends, the
+        expansion of k, the walk of k + W (on k's walk stream) and the construction
+        of k + W + 1 are released together."""
         end = k0 + cnt
-        for j in range(k0, min(k0 + 2, end)):
+        for j in range(k0, min(k0 + A, end)):
             g_build(j, None)
-        g_walk(k0)
+        for j in range(k0, min(k0 + W, end)):
+            g_walk(j)
         for k in range(k0, end):
             gate = ctxs[k % len(ctxs)].walked
-            if k + 2 < end:
-                g_build(k + 2, gate)
-            if k + 1 < end:
-                g_walk(k + 1)
+            if k + A < end:
+                g_build(k + A, gate)
+            if k + W < end:
+                g_walk(k + W)
             g_expand(k)
 
     def run_batches(k0, cnt):
@@ -393,7 +437,7 @@ def main():
             for k in range(k0, k0 + cnt):
                 one_step(k)
             return
-        if args.schedule == "gated" and len(ctxs) >= 3:
+        if args.schedule == "gated" and len(ctxs) >= max(A + 1, W + 2):
             run_gated(k0, cnt)
             return
         D = len(ctxs)
@@ -520,7 +564,9 @@ def main():
                    "chains_per_gpu": n, "seconds": secs, "parallelism": f"chains sharded over {world} GPU(s)",
                    "batches_in_flight": len(ctxs), "staggered": bool(args.stagger and nwin == 1),
                    "construction_on": args.build_on, "walk_priority": args.walk_priority,
-                   "schedule": args.schedule if (args.stagger and nwin == 1 and len(ctxs) >= 3) else None},
+                   "schedule": args.schedule if (args.stagger and nwin == 1 and len(ctxs) >= 3) else None,
+                   "walks_in_flight": W, "walk_chains_per_row": args.walk_cpr, "build_ahead": A,
+                   "minutes_ahead": bool(args.minutes_ahead), "commit_stream": bool(args.commit_stream)},
         "roofline": roof,
         "chain_seconds_total": chain_seconds, "chain_seconds_live": live,
         "phases_ms": phases,

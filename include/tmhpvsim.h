@@ -152,6 +152,14 @@ int tmh_state_offsets(uint32_t n_chains, uint64_t* offsets);
 size_t tmh_plan_bytes(uint32_t n_steps);
 size_t tmh_scratch_bytes(uint32_t n_chains, uint32_t n_steps);
 size_t tmh_workspace_bytes(uint32_t n_chains, uint32_t n_steps);
+/* The segment walk's rows (16 lanes each, four per wavefront) per chain: with
+ * chains_per_row = k the walk launches ceil(n / k) rows, each row starting with one
+ * chain and taking the next unstarted chain of the window's queue when its chain
+ * is done.  The walk's duration is set by the longest chain either way; k > 1
+ * shrinks its footprint on the CUs (for callers that run several batches' walks
+ * beside other kernels).  Results do not depend on k.  0 or 1 = one chain per row
+ * (default); at most 64. */
+int tmh_set_walk_chains_per_row(struct tmh_engine* eng, uint32_t chains_per_row);
 /* Tests only: segment records kept per chain (a multiple of 16; 0 = the default
  * n_steps/64 + 256) and the overflow pool's chunks (0 = n_chains/16 + 8), for
  * every later tmh_scratch_bytes / launch in this process.  Exercises the
@@ -265,9 +273,15 @@ int tmh_walk_part(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t
  * latency-bound (a few waves); on a second stream, after an event recorded
  * behind the kernel half, it runs beside the next batch's expansion.  Order:
  * KERNEL then COMMIT on the same buffers; the traces and statistics are final
- * after COMMIT.  tmh_expand == KERNEL | COMMIT. */
+ * after COMMIT.  tmh_expand == KERNEL | COMMIT.  TMH_EXPAND_MINUTES alone = the
+ * window's minute draws only (they need the window-start state -- after tmh_init
+ * or the previous window's COMMIT -- and the walk's draws, not the segment walk),
+ * so a caller can build them ahead on another stream; a later TMH_EXPAND_KERNEL |
+ * TMH_EXPAND_NO_MINUTES on the same buffers then runs the expansion alone. */
 #define TMH_EXPAND_KERNEL 1
 #define TMH_EXPAND_COMMIT 2
+#define TMH_EXPAND_MINUTES 4
+#define TMH_EXPAND_NO_MINUTES 8
 int tmh_expand_part(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, int64_t step0,
                     uint32_t n_steps, const tmh_ustream* inj, const tmh_trace* trace, const tmh_stats* stats,
                     const void* plan, void* scratch, size_t scratch_bytes, int parts, void* stream);

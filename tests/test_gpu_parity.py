@@ -445,3 +445,73 @@ def test_segment_overflow_pool():
     np.testing.assert_array_equal(st2[keep], st0[keep])
     np.testing.assert_array_equal(cov2[:, keep], cov0[:, keep])
     np.testing.assert_array_equal(pv2[:, keep], pv0[:, keep])
+
+
+@pytest.mark.parametrize("window", [86400, 7200])
+def test_walk_chains_per_row_invariance(window):
+    """tmh_set_walk_chains_per_row: rows that take the next chain from the window's
+    queue when theirs is done give bit-identical segment walks (covered bit, PV,
+    status, state) for 1, 3 and 64 chains per row, one window or 12 chained windows."""
+    from tmhpvsim_amd import _lib
+    L = _lib.load()
+    n, steps, start = 700, 86400, "2019-09-05 00:00:00"
+    outs = []
+    for cpr in (1, 3, 64):
+        s = _sim(n, start, tz="Europe/Berlin", prec="fp32", kernel_path="time_parallel", horizon=steps)
+        _lib.check(L.tmh_set_walk_chains_per_row(s._eng, cpr))
+        out = s.run(steps, trace=("covered", "pv"), window=window)
+        torch.cuda.synchronize()
+        outs.append((s.status(), _np(out["covered"]), _np(out["pv"]), s.state_field("ncalls").cpu().numpy()))
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("markov", [False, True])
+def test_parts_minutes_ahead_equal_step(markov):
+    """bench.py's gated order through the C-ABI -- draws, the minute table ahead
+    (TMH_EXPAND_MINUTES), the segment walk with queued rows, the expansion without
+    its minute table (KERNEL | NO_MINUTES), the commit on another stream -- equals
+    tmh_run bit for bit (traces, statistics, state)."""
+    import ctypes as C
+    from tmhpvsim_amd import _lib
+    start, steps, n = "2019-09-05 04:00:00", 9000, 300
+    mp = ModelParams(cc_mode=CC_MARKOV) if markov else ModelParams()
+    a = _sim(n, start, tz="Europe/Berlin", mp=mp, prec="fp32", horizon=steps, kernel_path="time_parallel")
+    b = _sim(n, start, tz="Europe/Berlin", mp=mp, prec="fp32", horizon=steps, kernel_path="time_parallel")
+    a.enable_stats()
+    b.enable_stats()
+    ra = a.run(steps, window=steps)
+    L = b.L
+    out = {f: torch.empty(steps, n, dtype=torch.float32, device="cuda:0") for f in ("csi", "pv", "meter", "residual")}
+    cov = torch.empty(steps, n, dtype=torch.uint8, device="cuda:0")
+    tr = _lib.Trace(out["csi"].data_ptr(), cov.data_ptr(), out["pv"].data_ptr(), out["meter"].data_ptr(),
+                    out["residual"].data_ptr(), n)
+    st = b._stats_struct()
+    plan = torch.empty(L.tmh_plan_bytes(steps), dtype=torch.uint8, device="cuda:0")
+    scr = torch.empty(L.tmh_scratch_bytes(n, steps), dtype=torch.uint8, device="cuda:0")
+    p = lambda t: C.c_void_p(t.data_ptr())
+    s = b._stream()
+    s2 = torch.cuda.Stream()
+    _lib.check(L.tmh_set_walk_chains_per_row(b._eng, 5))
+    args = (b._eng, p(b.state), 0, n, 0, steps, None, C.byref(tr), C.byref(st), p(plan), p(scr), scr.numel())
+    _lib.check(L.tmh_plan(b._eng, 0, steps, p(plan), s))
+    _lib.check(L.tmh_walk_part(b._eng, p(b.state), 0, n, 0, steps, p(plan), p(scr), scr.numel(), None, 0,
+                               _lib.WALK_DRAWS, s))
+    _lib.check(L.tmh_expand_part(*args, _lib.EXPAND_MINUTES, s))
+    _lib.check(L.tmh_walk_part(b._eng, p(b.state), 0, n, 0, steps, p(plan), p(scr), scr.numel(), None, 0,
+                               _lib.WALK_SEGMENTS, s))
+    _lib.check(L.tmh_expand_part(*args, _lib.EXPAND_KERNEL | _lib.EXPAND_NO_MINUTES, s))
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream())      # b._stream() is torch's current stream
+    s2.wait_event(ev)
+    _lib.check(L.tmh_expand_part(*args, _lib.EXPAND_COMMIT, C.c_void_p(s2.cuda_stream)))
+    torch.cuda.synchronize()
+    for f in ("csi", "pv", "meter", "residual"):
+        assert _same(ra[f], out[f]), f
+    assert _same(ra["covered"], cov)
+    np.testing.assert_array_equal(a.status(), b.status())
+    assert torch.equal(a.hist, b.hist)
+    assert torch.equal(a.chain_acc, b.chain_acc)
+    for fld in ("sa_cc", "sigma_len", "ncalls", "sec"):
+        assert _same(a.state_field(fld), b.state_field(fld)), fld

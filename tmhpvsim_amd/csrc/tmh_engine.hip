@@ -73,6 +73,7 @@ struct SegView {                   // P1 -> P2 scratch
     int2* pool;                    // [pool_cap][OVF_CHUNK]
     uint32_t pool_cap;
     uint32_t* pool_n;              // chunks handed out (zeroed by the draws phase)
+    uint32_t* walk_q;              // the walk's chain queue: chains taken past the first `rows` (zeroed likewise)
     uint32_t* count;               // [n]
     int32_t* fault;                // [n] window-relative fault step (INT_MAX = none)
     uint32_t* status;              // [n] status after the window
@@ -1021,7 +1022,10 @@ __global__ __launch_bounds__(256) void candidates_kernel(DrawParams dp, StateVie
 {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t k = blockIdx.y;
-    if (c == 0 && k == 0) *sg.pool_n = 0;   // the walk that follows hands out the overflow chunks
+    if (c == 0 && k == 0) {   // the walk that follows hands out overflow chunks and queued chains
+        *sg.pool_n = 0;
+        *sg.walk_q = 0;
+    }
     if (c >= n || (prev.status ? prev.status[c] : st.status[c]) != 0) return;
     const U4 b = keyed_block(dp.seed, chain0 + c, (uint64_t)(st.ncalls[c] + k), TAG_CLOUD, 0);
     sg.cand[(size_t)k * n + c] = pow_d(dp.alpha + dp.delta * u52(b.x, b.y), dp.expo);
@@ -1133,6 +1137,7 @@ constexpr int RCH_FIXED = TMH_RCH_FIXED;   // chunks always processed; chunk ch 
 #ifndef TMH_SEG_PRIO   // wave issue priority of the walk (s_setprio) over the expansion beside it
 #define TMH_SEG_PRIO 0
 #endif
+template <bool QUEUE>
 __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
                                                           int64_t W0, uint32_t nsteps, tmh_clock ck,
                                                           const int2* __restrict__ events,
@@ -1143,46 +1148,33 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
     __builtin_amdgcn_s_setprio(TMH_SEG_PRIO);
 #endif
     const int lane = threadIdx.x & 63, p = lane & 15, row0 = lane & ~15;
-    const uint32_t c = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
-    const bool live = c < n;
-    const uint32_t cs = live ? c : 0;
-    const uint64_t chain = chain0 + cs;
     const int64_t W1 = W0 + nsteps;
-    uint32_t status = live ? (prev.status ? prev.status[cs] : st.status[cs]) : 0xFFFFFFFFu;
-    double ccb, cca, wsb, wsa;   // window-start cloud-cover and wind pairs
-    if (prev.status) {
-        ccb = prev.end_p1[cs];
-        cca = prev.end_p1[(size_t)n + cs];
-        wsb = prev.end_p1[2 * (size_t)n + cs];
-        wsa = prev.end_p1[3 * (size_t)n + cs];
-    } else {
-        ccb = st.sb[S_CC][cs];
-        cca = st.sa[S_CC][cs];
-        wsb = st.sb[S_WS][cs];
-        wsa = st.sa[S_WS][cs];
-    }
+    const uint32_t nev = min(*n_events, ev_cap_dev(nsteps));
+    const WinClock wck = win_clock(ck, W0);
+    // Rows take chains: row r starts with chain r, and a row whose chain is done
+    // takes the next unstarted one from the window's queue (chains rows.. n - 1), so
+    // with fewer rows than chains the walk's waves stay busy instead of idling
+    // behind the windiest chain of their wave (its duration is the longest chain's
+    // call count either way; its footprint on the CUs shrinks).  Everything below
+    // is the row's current chain, row-uniform.
+    uint32_t c = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    bool live = c < n;
+    uint32_t status = 0xFFFFFFFFu;
+    double ccb = 0.0, cca = 0.0, wsb = 0.0, wsa = 0.0;   // window-start cloud-cover and wind pairs
     int32_t fault = INT_MAX;
     uint32_t nrec = 0;
-    double cl = st.cl[cs], clr = st.clr[cs];
-    int L = st.L[cs];
-    const int32_t sec0 = st.sec[cs];
-    double* gsc = sig_c(st, cs);
-    double* gsl = sig_l(st, cs);
+    double cl = 0.0, clr = 0.0;
+    int L = 0;
+    double* gsc = nullptr;
+    double* gsl = nullptr;
     double vc[RCH], vl[RCH];
-#pragma unroll
-    for (int ch = 0; ch < RCH; ++ch) {
-        const int k = ch * 16 + p;
-        vc[ch] = k < L ? gsc[k] : 0.0;
-        vl[ch] = k < L ? gsl[k] : 0.0;
-    }
-    int64_t s_start = W0 - sec0;   // step at which sec was 1
-    int64_t e = s_start + ceil_thr(cl + clr) - 1;
+    int64_t s_start = 0, e = 0;
     // No global load or store sits on the per-call path: records, boundary
     // events and candidates move through 16-entry lane-distributed buffers
     // (lane p of a row = entry p), flushed / refilled once per 16 uses, and
     // are read back with ds_bpermute.  (A per-call load behind a per-call
     // store makes every call wait for the store's round trip: vmcnt counts both.)
-    int2* rec = sg.rec + (size_t)cs * sg.cap;
+    int2* rec = nullptr;
     int rb_x = 0, rb_y = 0;       // record buffer: lane p = record rbase + p
     uint32_t rbase = 0;
     int32_t chunk = 0;            // the overflow chunk of records >= cap (row-uniform)
@@ -1199,9 +1191,6 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
             rbase += 16;
         }
     };
-    put_rec(0, (int)(s_start + ceil_thr(cl) - 1), (int)e);
-    nrec = 1;
-    const uint32_t nev = min(*n_events, ev_cap_dev(nsteps));
     uint32_t ev = 0, evb = 0;
     int eb_step = INT_MAX, eb_fl = 0;   // event buffer: lane p = event evb + p
     double eb_cc = 0.0, eb_ws = 0.0;
@@ -1212,11 +1201,10 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
             const int2 r = events[i];
             eb_step = r.x;
             eb_fl = r.y;
-            eb_cc = sg.evd[(size_t)i * 4 * n + cs];
-            eb_ws = sg.evd[((size_t)i * 4 + 1) * n + cs];
+            eb_cc = sg.evd[(size_t)i * 4 * n + c];
+            eb_ws = sg.evd[((size_t)i * 4 + 1) * n + c];
         }
     };
-    load_events();
     int64_t next_ev = INT64_MAX;
     int ev_fl = 0;
     double ev_cc = 0.0, ev_ws = 0.0;
@@ -1232,14 +1220,98 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
         ev_cc = bperm_f64(src, eb_cc);
         ev_ws = bperm_f64(src, eb_ws);
     };
-    fetch_event();
-    const uint32_t ncall0 = st.ncalls[cs];
-    uint32_t ncall = ncall0;
-    auto cand_at = [&](uint32_t k) { return k < sg.kcap ? sg.cand[(size_t)k * n + cs] : -1.0; };
+    uint32_t ncall0 = 0, ncall = 0;
+    auto cand_at = [&](uint32_t k) { return k < sg.kcap ? sg.cand[(size_t)k * n + c] : -1.0; };
     uint32_t kb = 0;                                     // candidate buffer: lane p = calls kb + p, kb + 16 + p
-    double cb_a = cand_at(p), cb_b = cand_at(16 + p);
-    const WinClock wck = win_clock(ck, W0);
-    bool active = live && status == 0;
+    double cb_a = 0.0, cb_b = 0.0;
+    bool active = false;
+    auto start_chain = [&]() {   // the row's chain c (< n) at the window start
+        const uint32_t cs = c;
+        status = prev.status ? prev.status[cs] : st.status[cs];
+        if (prev.status) {
+            ccb = prev.end_p1[cs];
+            cca = prev.end_p1[(size_t)n + cs];
+            wsb = prev.end_p1[2 * (size_t)n + cs];
+            wsa = prev.end_p1[3 * (size_t)n + cs];
+        } else {
+            ccb = st.sb[S_CC][cs];
+            cca = st.sa[S_CC][cs];
+            wsb = st.sb[S_WS][cs];
+            wsa = st.sa[S_WS][cs];
+        }
+        fault = INT_MAX;
+        cl = st.cl[cs];
+        clr = st.clr[cs];
+        L = st.L[cs];
+        const int32_t sec0 = st.sec[cs];
+        gsc = sig_c(st, cs);
+        gsl = sig_l(st, cs);
+#pragma unroll
+        for (int ch = 0; ch < RCH; ++ch) {
+            const int k = ch * 16 + p;
+            vc[ch] = k < L ? gsc[k] : 0.0;
+            vl[ch] = k < L ? gsl[k] : 0.0;
+        }
+        s_start = W0 - sec0;   // step at which sec was 1
+        e = s_start + ceil_thr(cl + clr) - 1;
+        rec = sg.rec + (size_t)cs * sg.cap;
+        rb_x = rb_y = 0;
+        rbase = 0;
+        chunk = 0;
+        put_rec(0, (int)(s_start + ceil_thr(cl) - 1), (int)e);
+        nrec = 1;
+        ev = evb = 0;
+        load_events();
+        fetch_event();
+        ncall0 = ncall = st.ncalls[cs];
+        kb = 0;
+        cb_a = cand_at(p);
+        cb_b = cand_at(16 + p);
+        active = status == 0;
+    };
+    auto finish_chain = [&]() {   // the row's chain at the window end: records, state, walk outputs
+        if ((uint32_t)p < nrec - rbase) group_at(rbase)[p] = make_int2(rb_x, rb_y);   // partial record group
+        if (status == 0) {
+            while (next_ev <= W1 - 1) {   // remaining boundaries of the window
+                if (ev_fl & FL_DAY) {
+                    wsb = wsa;
+                    wsa = ev_ws;
+                }
+                if (ev_fl & FL_HOUR) {
+                    ccb = cca;
+                    cca = ev_cc;
+                }
+                ++ev;
+                fetch_event();
+            }
+#pragma unroll
+            for (int ch = 0; ch < RCH; ++ch) {   // register chunks back to the state row
+                const int k = ch * 16 + p;
+                if (k < L) {
+                    gsc[k] = vc[ch];
+                    gsl[k] = vl[ch];
+                }
+            }
+            if (p == 0) {
+                st.sec[c] = (int32_t)(W1 - s_start);   // sec after step W1 - 1
+                st.cl[c] = cl;
+                st.clr[c] = clr;
+                st.L[c] = L;
+                st.ncalls[c] = ncall;
+            }
+        }
+        if (p == 0) {
+            sg.count[c] = nrec;
+            sg.fault[c] = fault;
+            sg.status[c] = status;
+            sg.end_p1[c] = ccb;
+            sg.end_p1[(size_t)n + c] = cca;
+            sg.end_p1[2 * (size_t)n + c] = wsb;
+            sg.end_p1[3 * (size_t)n + c] = wsa;
+        }
+    };
+    const uint32_t rows = gridDim.x * blockDim.x / 16;
+    if (live) start_chain();
 #ifdef TMH_DIAG_P1   // diagnostic build only: cycles per section of the walk (s_memtime)
     uint64_t dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t dt = __builtin_amdgcn_s_memtime();
@@ -1253,6 +1325,16 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
 #define DSTAMP(i)
 #endif
     for (;;) {
+        if constexpr (QUEUE) {
+            while (live && !(active && e < W1)) {   // row-uniform: the row's chain is done, take the next one
+                finish_chain();
+                int v = 0;
+                if (p == 0) v = (int)atomicAdd(sg.walk_q, 1u);
+                c = rows + (uint32_t)__builtin_amdgcn_ds_bpermute(row0 << 2, v);   // the whole row is active here
+                live = c < n;
+                if (live) start_chain();
+            }
+        }
         const bool run = active && e < W1;
         if (__builtin_amdgcn_ballot_w64(run) == 0) break;
         // wave-uniform chunk bound: the loops over register chunks branch on SGPRs only
@@ -1309,7 +1391,7 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
                 if (tries - tb >= 16) {   // row-uniform
                     tb = tries;
                     const int t = tries + p;
-                    nb = pow_d(dp.alpha + dp.delta * keyed_u(dp.seed, chain, ncall, TAG_CLOUD, (uint32_t)(t >> 1), t & 1),
+                    nb = pow_d(dp.alpha + dp.delta * keyed_u(dp.seed, chain0 + c, ncall, TAG_CLOUD, (uint32_t)(t >> 1), t & 1),
                                dp.expo) / ws;
                 }
                 ncl = bperm_f64(row0 | (tries - tb), nb);
@@ -1317,7 +1399,7 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
 #else
             double x;
             if (tries == 0 && x0 >= 0.0) x = x0;
-            else x = pow_d(dp.alpha + dp.delta * keyed_u(dp.seed, chain, ncall, TAG_CLOUD, (uint32_t)(tries >> 1),
+            else x = pow_d(dp.alpha + dp.delta * keyed_u(dp.seed, chain0 + c, ncall, TAG_CLOUD, (uint32_t)(tries >> 1),
                                                         tries & 1),
                            dp.expo);
             ncl = x / ws;
@@ -1477,52 +1559,14 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
         ++nrec;
         DSTAMP(5)
     }
+    if constexpr (!QUEUE)   // one chain per row
+        if (live) finish_chain();
 #ifdef TMH_DIAG_P1
     if (lane == 0) {
         const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
         for (int i = 0; i < 8; ++i) g_p1diag[w * 8 + i] = dg[i];
     }
 #endif
-    if (live && (uint32_t)p < nrec - rbase) group_at(rbase)[p] = make_int2(rb_x, rb_y);   // partial record group
-    if (!live) return;
-    if (status == 0) {
-        while (next_ev <= W1 - 1) {   // remaining boundaries of the window
-            if (ev_fl & FL_DAY) {
-                wsb = wsa;
-                wsa = ev_ws;
-            }
-            if (ev_fl & FL_HOUR) {
-                ccb = cca;
-                cca = ev_cc;
-            }
-            ++ev;
-            fetch_event();
-        }
-#pragma unroll
-        for (int ch = 0; ch < RCH; ++ch) {   // register chunks back to the state row
-            const int k = ch * 16 + p;
-            if (k < L) {
-                gsc[k] = vc[ch];
-                gsl[k] = vl[ch];
-            }
-        }
-        if (p == 0) {
-            st.sec[c] = (int32_t)(W1 - s_start);   // sec after step W1 - 1
-            st.cl[c] = cl;
-            st.clr[c] = clr;
-            st.L[c] = L;
-            st.ncalls[c] = ncall;
-        }
-    }
-    if (p == 0) {
-        sg.count[c] = nrec;
-        sg.fault[c] = fault;
-        sg.status[c] = status;
-        sg.end_p1[c] = ccb;
-        sg.end_p1[(size_t)n + c] = cca;
-        sg.end_p1[2 * (size_t)n + c] = wsb;
-        sg.end_p1[3 * (size_t)n + c] = wsa;
-    }
 }
 
 // ------------------------------------------------------------ P2: expand
@@ -2113,7 +2157,10 @@ size_t scratch_layout(uint32_t n, uint32_t n_steps, void* base, SegView* v)
     o += align_up((size_t)n * OVF_SLOTS * 4);
     if (v) v->pool = (int2*)(b + o);
     o += align_up((size_t)pool_chunks(n) * OVF_CHUNK * 8);
-    if (v) v->pool_n = (uint32_t*)(b + o);
+    if (v) {
+        v->pool_n = (uint32_t*)(b + o);
+        v->walk_q = v->pool_n + 1;
+    }
     o += ALIGN;
     if (v) v->count = (uint32_t*)(b + o);
     o += align_up((size_t)n * 4);
@@ -2169,6 +2216,7 @@ struct tmh_engine {
     int64_t local_step0 = 0;   // local wall-clock seconds of step 0 (the constructors' time), kept across tmh_set_clock
     uint32_t n_tab = 0;     // rows of the per-chain shape tables (0: none)
     uint32_t n_sites = 0;   // rows of the per-chain sites (0: the engine's one site)
+    uint32_t walk_cpr = 1;  // chains per walk row (tmh_set_walk_chains_per_row)
     // kernel timing (tmh_profile_*): event pairs per kernel, read and recycled
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[TMH_K_COUNT];
@@ -2416,6 +2464,14 @@ int tmh_diag_p1(uint64_t* out, uint32_t n)   // diagnostic build only
 }
 #endif
 
+int tmh_set_walk_chains_per_row(struct tmh_engine* eng, uint32_t chains_per_row)
+{
+    if (!eng) return fail(TMH_E_INVAL, "NULL engine");
+    if (chains_per_row > 64) return fail(TMH_E_INVAL, "chains_per_row %u > 64", chains_per_row);
+    eng->walk_cpr = chains_per_row ? chains_per_row : 1;
+    return TMH_OK;
+}
+
 int tmh_test_set_segment_capacity(uint32_t cap, uint32_t pool_chunks)
 {
     if (cap % 16) return fail(TMH_E_INVAL, "segment capacity %u is not a multiple of 16", cap);
@@ -2498,7 +2554,8 @@ int tmh_plan(struct tmh_engine* eng, int64_t step0, uint32_t n_steps, void* plan
     return hip_check(hipGetLastError(), "plan kernels launch");
 }
 
-enum { PH_DRAWS = 1, PH_SEGMENTS = 4, PH_WALK = PH_DRAWS | PH_SEGMENTS, PH_EXPAND = 2, PH_COMMIT = 8, PH_ALL = 15 };
+enum { PH_DRAWS = 1, PH_SEGMENTS = 4, PH_WALK = PH_DRAWS | PH_SEGMENTS, PH_EXPAND = 2, PH_COMMIT = 8, PH_ALL = 15,
+       PH_MINUTES = 16, PH_NO_MINUTES = 32 };
 
 static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_chains, int64_t step0,
                        uint32_t n_steps, const tmh_ustream* inj, const tmh_trace* trace, const tmh_stats* stats,
@@ -2572,13 +2629,17 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     }
     if (phases & PH_SEGMENTS) {
     hipEvent_t t_seg = eng->mark(s);
-    hipLaunchKernelGGL(segments_kernel, dim3((n_chains + 15) / 16), dim3(256), 0, s, eng->dp, v, chain0, n_chains,
-                       step0, n_steps, eng->gp.clock, pv.events, pv.n_events, sg, prev);
+    const uint32_t rows = (uint32_t)(((uint64_t)n_chains + eng->walk_cpr - 1) / eng->walk_cpr);   // 16 per workgroup
+    if (rows < n_chains)   // rows take queued chains
+        hipLaunchKernelGGL(segments_kernel<true>, dim3((rows + 15) / 16), dim3(256), 0, s, eng->dp, v, chain0, n_chains,
+                           step0, n_steps, eng->gp.clock, pv.events, pv.n_events, sg, prev);
+    else
+        hipLaunchKernelGGL(segments_kernel<false>, dim3((rows + 15) / 16), dim3(256), 0, s, eng->dp, v, chain0,
+                           n_chains, step0, n_steps, eng->gp.clock, pv.events, pv.n_events, sg, prev);
     eng->close(TMH_K_SEGMENTS, t_seg, s);
     if (int rc = hip_check(hipGetLastError(), "segments kernel launch")) return rc;
     }
-    if (phases & PH_EXPAND) {
-    hipEvent_t t_exp = eng->mark(s);
+    if ((phases & PH_MINUTES) || ((phases & PH_EXPAND) && !(phases & PH_NO_MINUTES))) {
     {   // the window's minute draws, one work-item each (read by the expansion and the commit)
         const int64_t fmh = first_minute_host(utc0, step0);
         const uint32_t nm = fmh < (int64_t)n_steps ? (uint32_t)((n_steps - 1 - fmh) / 60 + 1) : 0;
@@ -2595,6 +2656,9 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
                                    n_chains, step0, n_steps, fmh, pv.tab64, pv.events, pv.n_events, sg);
         }
     }
+    }
+    if (phases & PH_EXPAND) {
+    hipEvent_t t_exp = eng->mark(s);
     const bool no_stats = !sv.hist && !sv.acc;
     const int out = (no_stats && tv.pv && tv.meter && tv.residual && !tv.csi && !tv.covered) ? OUT_TRACE3
                     : (!tv.pv && !tv.meter && !tv.residual && !tv.csi && !tv.covered) ? OUT_STATS
@@ -2692,10 +2756,12 @@ int tmh_expand_part(struct tmh_engine* eng, void* state, uint64_t chain0, uint32
                     uint32_t n_steps, const tmh_ustream* inj, const tmh_trace* trace, const tmh_stats* stats,
                     const void* plan, void* scratch, size_t scratch_bytes, int parts, void* stream)
 {
-    if (parts & ~(TMH_EXPAND_KERNEL | TMH_EXPAND_COMMIT)) return fail(TMH_E_INVAL, "bad expand parts %d", parts);
+    if (parts & ~(TMH_EXPAND_KERNEL | TMH_EXPAND_COMMIT | TMH_EXPAND_MINUTES | TMH_EXPAND_NO_MINUTES))
+        return fail(TMH_E_INVAL, "bad expand parts %d", parts);
     if (eng && eng->path != TMH_PATH_TIME_PARALLEL && parts != (TMH_EXPAND_KERNEL | TMH_EXPAND_COMMIT))
         return fail(TMH_E_INVAL, "tmh_expand_part in parts needs the time-parallel path");
-    const int ph = ((parts & TMH_EXPAND_KERNEL) ? PH_EXPAND : 0) | ((parts & TMH_EXPAND_COMMIT) ? PH_COMMIT : 0);
+    const int ph = ((parts & TMH_EXPAND_KERNEL) ? PH_EXPAND : 0) | ((parts & TMH_EXPAND_COMMIT) ? PH_COMMIT : 0) |
+                   ((parts & TMH_EXPAND_MINUTES) ? PH_MINUTES : 0) | ((parts & TMH_EXPAND_NO_MINUTES) ? PH_NO_MINUTES : 0);
     return step_phases(eng, state, chain0, n_chains, step0, n_steps, inj, trace, stats, plan, scratch, scratch_bytes,
                        stream, ph);
 }
