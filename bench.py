@@ -96,6 +96,9 @@ def parse():
     ap.add_argument("--commit-stream", type=int, default=None,
                     help="gated schedule: each batch's fixup + commit on a stream of their own beside the next "
                          "expansion (1) or after its expansion on the expansion stream (0); default 1 when --walks > 1")
+    ap.add_argument("--compact", type=int, default=None,
+                    help="multi-window stats workloads: run each window after the first on the chains still "
+                         "live (faulted chains, e.g. C5's markov AssertionError, drop out); default 1 for c5")
     ap.add_argument("--pipeline", type=int, default=None,
                     help="batches in flight on separate HIP streams (1 = no overlap): the segment walks of the "
                          "next batches (latency-bound, one wave per SIMD) run beside this batch's expansion")
@@ -103,6 +106,8 @@ def parse():
     c5, c4 = a.workload == "c5", a.workload == "c4"
     a.chains = a.chains or {"c2": 4096, "c3": 1048576, "c4": 16384, "c5": 65536}[a.workload]
     a.seconds = a.seconds or {"c2": 86400, "c3": 86400, "c4": 365 * 86400, "c5": 604800}[a.workload]
+    if a.compact is None:
+        a.compact = int(c5)
     a.build_ahead = a.build_ahead or max(1, a.walks) + 1
     a.pipeline = a.pipeline or (1 if a.workload == "c3" else a.build_ahead + 1)
     if a.minutes_ahead is None:
@@ -166,8 +171,9 @@ def pmc_record(args, n, launch_secs):
         return None
     want = dict(workload=args.workload, chains=n, launch_seconds=launch_secs, precision=args.precision,
                 mode=args.mode, cc=args.cc)
-    for r in recs:
-        if all(r.get(k) == v for k, v in want.items()):
+    compact = int(bool(args.compact and args.mode == "stats" and args.seconds > launch_secs))
+    for r in recs:   # a compacted run's launches hold fewer chains: its own record
+        if all(r.get(k) == v for k, v in want.items()) and int(r.get("compact", 0)) == compact:
             return r
     return None
 
@@ -232,6 +238,10 @@ def main():
             self.state = torch.zeros(L.tmh_state_bytes(n), dtype=torch.uint8, device=dev)
             self.plan = torch.empty(L.tmh_plan_bytes(win), dtype=torch.uint8, device=dev)
             self.scratch = torch.empty(L.tmh_scratch_bytes(n, win), dtype=torch.uint8, device=dev)
+            if args.compact and args.mode == "stats" and nwin > 1:   # compacted windows: a working state
+                self.work = torch.empty_like(self.state)
+                self.ids = torch.empty(n, dtype=torch.int32, device=dev)
+                self.nlive = torch.zeros(1, dtype=torch.int32, device=dev)
             if nwin > 1:   # second plan + scratch: window w+1's walk beside window w's expansion
                 self.plan2 = torch.empty_like(self.plan)
                 self.scratch2 = torch.empty_like(self.scratch)
@@ -269,6 +279,34 @@ def main():
                                       C.byref(cx.tr), C.byref(cx.st) if cx.st is not None else None,
                                       C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
                                       cx.scratch.numel(), cx.sptr))
+            return
+        if args.compact and args.mode == "stats":   # windows in order, the live chains of each only
+            sp = C.c_void_p(cx.state.data_ptr())
+            for s0 in range(0, secs, win):
+                w = min(win, secs - s0)
+                nl, cur = n, cx.state
+                if s0 > 0:
+                    _lib.check(L.tmh_live_chains(sim._eng, sp, n, None, C.c_void_p(cx.ids.data_ptr()),
+                                                 C.c_void_p(cx.nlive.data_ptr()), cx.sptr))
+                    cx.stream.synchronize()                # n_live was written on the batch's stream
+                    nl = int(cx.nlive.item())
+                    if nl < n:
+                        cur = cx.work
+                        if nl:
+                            _lib.check(L.tmh_state_move(sim._eng, sp, n, C.c_void_p(cx.work.data_ptr()), nl,
+                                                        C.c_void_p(cx.ids.data_ptr()), C.c_void_p(cx.nlive.data_ptr()),
+                                                        nl, 0, cx.sptr))
+                            _lib.check(L.tmh_set_chain_ids(sim._eng, C.c_void_p(cx.ids.data_ptr()), n))
+                if nl:
+                    _lib.check(L.tmh_plan(sim._eng, s0, w, C.c_void_p(cx.plan.data_ptr()), cx.sptr))
+                    _lib.check(L.tmh_step(sim._eng, C.c_void_p(cur.data_ptr()), chain0, nl, s0, w, None,
+                                          C.byref(cx.tr), C.byref(cx.st), C.c_void_p(cx.plan.data_ptr()),
+                                          C.c_void_p(cx.scratch.data_ptr()), cx.scratch.numel(), cx.sptr))
+                if nl and cur is cx.work:
+                    _lib.check(L.tmh_state_move(sim._eng, C.c_void_p(cx.work.data_ptr()), nl, sp, n,
+                                                C.c_void_p(cx.ids.data_ptr()), C.c_void_p(cx.nlive.data_ptr()),
+                                                nl, 1, cx.sptr))
+                _lib.check(L.tmh_set_chain_ids(sim._eng, None, 0))
             return
         # multi-window: the segment walk of window w+1 (high-priority stream) beside the
         # expansion of window w; plans and draws on the expansion's stream (as BatchedSim.run)
@@ -566,7 +604,8 @@ def main():
                    "construction_on": args.build_on, "walk_priority": args.walk_priority,
                    "schedule": args.schedule if (args.stagger and nwin == 1 and len(ctxs) >= 3) else None,
                    "walks_in_flight": W, "walk_chains_per_row": args.walk_cpr, "build_ahead": A,
-                   "minutes_ahead": bool(args.minutes_ahead), "commit_stream": bool(args.commit_stream)},
+                   "minutes_ahead": bool(args.minutes_ahead), "commit_stream": bool(args.commit_stream),
+                   "compacted_windows": bool(args.compact and args.mode == "stats" and nwin > 1)},
         "roofline": roof,
         "chain_seconds_total": chain_seconds, "chain_seconds_live": live,
         "phases_ms": phases,

@@ -160,6 +160,25 @@ size_t tmh_workspace_bytes(uint32_t n_chains, uint32_t n_steps);
  * beside other kernels).  Results do not depend on k.  0 or 1 = one chain per row
  * (default); at most 64. */
 int tmh_set_walk_chains_per_row(struct tmh_engine* eng, uint32_t chains_per_row);
+/* Compaction (batches whose chains fault, e.g. the reference's markov-mode
+ * AssertionError, cloud_cover_binary.py:91): run later windows on the live chains
+ * only.  A launch slot then holds chain ids[slot] of a full batch of n_full chains:
+ * the slot's keyed draws are that chain's (chain0 + ids[slot]), and it reads row
+ * ids[slot] of the per-chain shape tables and sites and accumulates into column
+ * ids[slot] of tmh_stats.chain_acc ([4][n_full]).  State, scratch and traces stay
+ * per slot.  ids == NULL: slot i is chain i (the default).  Results per chain do
+ * not depend on the compaction. */
+int tmh_set_chain_ids(struct tmh_engine* eng, const uint32_t* ids, uint32_t n_full);
+/* the ids (ids_in[slot], or the slot itself when ids_in == NULL) of the slots of
+ * `state` (n_chains slots) whose status is 0, in slot order, into ids_out
+ * (device, n_chains entries); their count into *n_live (device uint32). */
+int tmh_live_chains(struct tmh_engine* eng, const void* state, uint32_t n_chains, const uint32_t* ids_in,
+                    uint32_t* ids_out, uint32_t* n_live, void* stream);
+/* move chains between two state buffers: gather (scatter = 0) dst slot i <- src
+ * slot map[i], scatter (1) dst slot map[i] <- src slot i, for i < min(*count, cap)
+ * (count: device uint32, e.g. tmh_live_chains' n_live). */
+int tmh_state_move(struct tmh_engine* eng, const void* src, uint32_t n_src, void* dst, uint32_t n_dst,
+                   const uint32_t* map, const uint32_t* count, uint32_t cap, int scatter, void* stream);
 /* Tests only: segment records kept per chain (a multiple of 16; 0 = the default
  * n_steps/64 + 256) and the overflow pool's chunks (0 = n_chains/16 + 8), for
  * every later tmh_scratch_bytes / launch in this process.  Exercises the

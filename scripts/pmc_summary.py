@@ -78,7 +78,7 @@ def record(d, **key):
         db = {"note": "per-launch PMC means of the dominant expand kernel per bench workload "
                       "(scripts/pmc_workload.sh); SQ_* are wave-instruction counts summed over the chip",
               "records": []}
-    ident = ("workload", "chains", "launch_seconds", "precision", "mode", "cc")
+    ident = ("workload", "chains", "launch_seconds", "precision", "mode", "cc", "compact")
     db["records"] = [r for r in db["records"] if any(r.get(i) != rec.get(i) for i in ident)] + [rec]
     json.dump(db, open(path, "w"), indent=1)
     return rec

@@ -515,3 +515,34 @@ def test_parts_minutes_ahead_equal_step(markov):
     assert torch.equal(a.chain_acc, b.chain_acc)
     for fld in ("sa_cc", "sigma_len", "ncalls", "sec"):
         assert _same(a.state_field(fld), b.state_field(fld)), fld
+
+
+@pytest.mark.parametrize("path", ["time_parallel", "sequential"])
+def test_compacted_windows_equal_full_batch(path):
+    """BatchedSim.run(compact=True): windows after the first run on the chains still
+    live (markov cc with per-site tables and sites, where the reference's
+    AssertionError ends many chains); per-chain statistics, histogram, status and
+    state are bit-identical to the uncompacted run."""
+    from tmhpvsim_amd.params import site_grid, site_shape_tables
+    n, steps, start = 512, 3 * 86400, "2019-09-05 00:00:00"
+    mp = ModelParams(cc_mode=CC_MARKOV, seed=0xC5)
+    kw = dict(tz="Europe/Berlin", mp=mp, horizon=steps, tables=site_shape_tables(n), sites=site_grid(32, 16),
+              prec="fp32", kernel_path=path)
+    a = _sim(n, start, **kw)
+    b = _sim(n, start, **kw)
+    a.enable_stats()
+    b.enable_stats()
+    a.run(steps, trace=(), window=86400)
+    b.run(steps, trace=(), window=86400, compact=True)
+    torch.cuda.synchronize()
+    sa, sb = a.status(), b.status()
+    assert (sa != 0).sum() > n // 8, "the test needs faulting chains"
+    np.testing.assert_array_equal(sa, sb)
+    assert torch.equal(a.hist, b.hist)
+    assert _same(a.chain_acc, b.chain_acc)
+    for fld in ("sa_cc", "sb_ws", "cloud_length", "sigma_len", "ncalls", "sec", "pos"):
+        assert _same(a.state_field(fld), b.state_field(fld)), fld
+    Ls = a.state_field("sigma_len").long()
+    used = torch.arange(a.state_field("sigma_cloud").shape[1], device="cuda:0")[None, :] < Ls[:, None]
+    for fld in ("sigma_cloud", "sigma_clear"):   # entries past a chain's length are not state
+        assert _same(torch.where(used, a.state_field(fld), 0.0), torch.where(used, b.state_field(fld), 0.0)), fld

@@ -171,8 +171,8 @@ __device__ __forceinline__ void init_cc_pair(const KParams& kp, uint32_t c, cons
 {
     Chain ch;
     ch.mstate = 1.0;
-    b = draw_cc(kp, c, ch, u[0]);
-    a = draw_cc(kp, c, ch, u[1]);
+    b = draw_cc(kp, gid(kp.ids, c), ch, u[0]);
+    a = draw_cc(kp, gid(kp.ids, c), ch, u[1]);
 }
 
 __global__ __launch_bounds__(256) void init_variates_kernel(KParams kp, StateView st, uint64_t chain0, uint32_t n,
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) void init_variates_kernel(KParams kp, StateVie
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     const int j = 2 + (int)blockIdx.y;   // variate 2..11
     if (c >= n) return;
-    const uint64_t chain = chain0 + c;
+    const uint64_t chain = chain0 + gid(kp.ids, c);
     const U4 blk = keyed_block(kp.seed, chain, 0, TAG_INIT, (uint32_t)(j >> 1));
     const double u = (j & 1) ? u52(blk.z, blk.w) : u52(blk.x, blk.y);
     double v;
@@ -224,7 +224,7 @@ __global__ __launch_bounds__(256) void init_kernel(KParams kp, StateView st, uin
     Draw<RNG> dr;
     if constexpr (RNG == TMH_RNG_KEYED) {
         dr.seed = kp.seed;
-        dr.chain = chain0 + c;
+        dr.chain = chain0 + gid(kp.ids, c);
     } else {
         dr.u = inj.u + (size_t)c * inj.stride;
         dr.len = inj.len;
@@ -236,8 +236,8 @@ __global__ __launch_bounds__(256) void init_kernel(KParams kp, StateView st, uin
     } else {
         for (int d = 0; d < 12; d += 2) dr.two(ch, 0, TAG_INIT, (uint32_t)(d >> 1), u[d], u[d + 1]);
     }
-    ch.s.b[S_CC] = draw_cc(kp, c, ch, u[0]);
-    ch.s.a[S_CC] = draw_cc(kp, c, ch, u[1]);
+    ch.s.b[S_CC] = draw_cc(kp, gid(kp.ids, c), ch, u[0]);
+    ch.s.a[S_CC] = draw_cc(kp, gid(kp.ids, c), ch, u[1]);
     if constexpr (RNG == TMH_RNG_KEYED) {
         ch.s.b[S_CLEAR_DAY] = pre[2];
         ch.s.a[S_CLEAR_DAY] = pre[3];
@@ -482,7 +482,7 @@ __global__ __launch_bounds__(256) void event_draws_kernel(DrawParams dp, uint64_
     const uint32_t c = blockIdx.y * blockDim.x + threadIdx.x;
     const uint32_t e = blockIdx.x;
     if (c >= n || e >= min(*n_events, ev_cap_dev(nsteps))) return;
-    const uint64_t chain = chain0 + c, step = (uint64_t)events[e].x;
+    const uint64_t chain = chain0 + gid(dp.ids, c), step = (uint64_t)events[e].x;
     const int fl = events[e].y;
     double* o = evd + (size_t)e * 4 * n + c;
     if (fl & FL_DAY) {
@@ -492,7 +492,7 @@ __global__ __launch_bounds__(256) void event_draws_kernel(DrawParams dp, uint64_
     }
     if (fl & FL_HOUR) {
         const U4 u = keyed_block(dp.seed, chain, step, TAG_BOUNDARY, 1);
-        if (!dp.markov) o[0] = cc_faithful(dp, c, u52(u.x, u.y));
+        if (!dp.markov) o[0] = cc_faithful(dp, gid(dp.ids, c), u52(u.x, u.y));
         o[3 * (size_t)n] = normal(u52(u.z, u.w), 0.99, 0.08);
     }
 }
@@ -523,16 +523,23 @@ __global__ __launch_bounds__(MK_BLOCK) void markov_cc_kernel(KParams kp, StateVi
     __shared__ int32_t tabt_s[MK_BLOCK * 6];
     const uint32_t cb0 = blockIdx.x * MK_BLOCK;
     const uint32_t nb = min((uint32_t)MK_BLOCK, n - cb0);
-    if (kp.tab) {   // the block's rows are one contiguous range: coalesced 16-B loads
+    if (kp.tab && !kp.ids) {   // the block's rows are one contiguous range: coalesced 16-B loads
         const double2* src = reinterpret_cast<const double2*>(kp.tab + (size_t)cb0 * 24);
         for (uint32_t i = threadIdx.x; i < nb * 12; i += MK_BLOCK) tab_s[i] = src[i];
         for (uint32_t i = threadIdx.x; i < nb * 6; i += MK_BLOCK)
             tabt_s[i] = kp.tab_t ? kp.tab_t[(size_t)cb0 * 6 + i] : kp.is_t[i % 6];
+    } else if (kp.tab) {   // a compacted batch: each slot's row of its chain (12 x 16 B)
+        for (uint32_t i = threadIdx.x; i < nb * 12; i += MK_BLOCK) {
+            const uint32_t g = kp.ids[cb0 + i / 12];
+            tab_s[i] = reinterpret_cast<const double2*>(kp.tab + (size_t)g * 24)[i % 12];
+        }
+        for (uint32_t i = threadIdx.x; i < nb * 6; i += MK_BLOCK)
+            tabt_s[i] = kp.tab_t ? kp.tab_t[(size_t)kp.ids[cb0 + i / 6] * 6 + i % 6] : kp.is_t[i % 6];
     }
     __syncthreads();
     const uint32_t c = cb0 + threadIdx.x;
     if (c >= n) return;
-    const uint64_t chain = chain0 + c;
+    const uint64_t chain = chain0 + gid(kp.ids, c);
     const uint32_t ne = min(*n_events, ev_cap_dev(nsteps));
     const double* row = kp.tab ? reinterpret_cast<const double*>(tab_s) + threadIdx.x * 24 : nullptr;
     const int32_t* rowt = tabt_s + threadIdx.x * 6;
@@ -638,7 +645,7 @@ __global__ __launch_bounds__(256) void minute_table_kernel(DrawParams dp, StateV
     if (c >= n || jm >= (int64_t)nsteps) return;
     const int ne = (int)min(*n_events, ev_cap_dev(nsteps));
     double cloudy, clear;
-    minute_draws<R>(dp, chain0 + c, W0 + jm, minute_cc(st, sg, n, c, W0, jm, events, ne, tab64), cloudy, clear);
+    minute_draws<R>(dp, chain0 + gid(dp.ids, c), W0 + jm, minute_cc(st, sg, n, c, W0, jm, events, ne, tab64), cloudy, clear);
     R* t = reinterpret_cast<R*>(sg.mtab);
     t[(size_t)(2 * m) * n + c] = (R)cloudy;
     t[(size_t)(2 * m + 1) * n + c] = (R)clear;
@@ -719,7 +726,7 @@ __device__ __forceinline__ void exact_noise_at(const BlockDesc& d, const DrawPar
     if (d.q1 >= 0) {
         const int64_t jm1 = jm0 - 60;
         const int back = (d.h0 >= 0 && (int64_t)events[d.h0].x == W0 + jm0) ? 1 : 0;
-        minute_draws<double>(dp, chain0 + c, W0 + jm1, desc_cc(d, back, st, sg, n, c, tab64[(size_t)jm1 * ROW + G_HOURF]),
+        minute_draws<double>(dp, chain0 + gid(dp.ids, c), W0 + jm1, desc_cc(d, back, st, sg, n, c, tab64[(size_t)jm1 * ROW + G_HOURF]),
                              cl, cr);
         s.b[S_CLOUDY_NOISE] = cl;
         s.b[S_CLEAR_NOISE] = cr;
@@ -727,7 +734,7 @@ __device__ __forceinline__ void exact_noise_at(const BlockDesc& d, const DrawPar
         s.b[S_CLOUDY_NOISE] = s.a[S_CLOUDY_NOISE];
         s.b[S_CLEAR_NOISE] = s.a[S_CLEAR_NOISE];
     }
-    minute_draws<double>(dp, chain0 + c, W0 + jm0, desc_cc(d, 0, st, sg, n, c, tab64[(size_t)jm0 * ROW + G_HOURF]), cl,
+    minute_draws<double>(dp, chain0 + gid(dp.ids, c), W0 + jm0, desc_cc(d, 0, st, sg, n, c, tab64[(size_t)jm0 * ROW + G_HOURF]), cl,
                          cr);
     s.a[S_CLOUDY_NOISE] = cl;
     s.a[S_CLEAR_NOISE] = cr;
@@ -778,12 +785,12 @@ __device__ __forceinline__ bool redo_second(const KParams& kp, const DrawParams&
     uint32_t k = jr_end;   // the segment holding the step: first next-call step > step, at or before the block's last
     while (k > 0 && (int64_t)rec_at(sg, c, k - 1).y > step) --k;
     const bool covered = step < (int64_t)rec_at(sg, c, k).x;
-    const U4 pb = keyed_block(kp.seed, chain0 + c, (uint64_t)step >> 1, TAG_STEP2, 0);
+    const U4 pb = keyed_block(kp.seed, chain0 + gid(kp.ids, c), (uint64_t)step >> 1, TAG_STEP2, 0);
     const bool odd = step & 1;
     LaneSite ls{};
     if constexpr (SITES) {
-        ls.k = site_k(kp.sites + (size_t)c * 8);
-        ls.linke = kp.site_linke ? kp.site_linke + (size_t)c * 12 : nullptr;
+        ls.k = site_k(kp.sites + (size_t)gid(kp.ids, c) * 8);
+        ls.linke = kp.site_linke ? kp.site_linke + (size_t)gid(kp.ids, c) * 12 : nullptr;
         ls.tl_doy = -1;
     }
     bool risky;
@@ -840,12 +847,12 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
     Draw<RNG> dr;
     if constexpr (RNG == TMH_RNG_KEYED) {
         dr.seed = kp.seed;
-        dr.chain = chain0 + c;
+        dr.chain = chain0 + gid(kp.ids, c);
     } else {
         dr.u = inj.u + (size_t)c * inj.stride;
         dr.len = inj.len;
     }
-    const uint64_t chain = chain0 + c;
+    const uint64_t chain = chain0 + gid(kp.ids, c);
     double* sc = live ? sig_c(st, c) : nullptr;
     double* sl = live ? sig_l(st, c) : nullptr;
     FSamp<R> fs;
@@ -861,8 +868,8 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
     Acc acc{0.0, 0.0, 0.0, -INFINITY};
     LaneSite ls{};   // per-chain sites (tmh_set_sites)
     if (kp.sites) {
-        ls.k = site_k(kp.sites + (size_t)(live ? c : 0) * 8);
-        ls.linke = kp.site_linke ? kp.site_linke + (size_t)(live ? c : 0) * 12 : nullptr;
+        ls.k = site_k(kp.sites + (size_t)(live ? gid(kp.ids, c) : 0) * 8);
+        ls.linke = kp.site_linke ? kp.site_linke + (size_t)(live ? gid(kp.ids, c) : 0) * 12 : nullptr;
         ls.tl_doy = -1;
     }
     for (uint32_t j = 0; j < nsteps; ++j) {
@@ -887,7 +894,7 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
                 }
                 if (fl & FL_HOUR) {                    // _next_hour (advances clear_day)
                     dr.two(ch, step, TAG_BOUNDARY, 1, u0, u1);
-                    push(ch.s, S_CC, draw_cc(kp, c, ch, u0));
+                    push(ch.s, S_CC, draw_cc(kp, gid(kp.ids, c), ch, u0));
                     push(ch.s, S_CLEAR_DAY, normal(u1, 0.99, 0.08));
                 }
                 if (fl & FL_MIN) {                     // _next_min
@@ -966,10 +973,12 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
             st.fn[1][c] = fnl;
         }
         if (sv.acc) {
-            sv.acc[c] += acc.pv;
-            sv.acc[(size_t)n + c] += acc.m;
-            sv.acc[2 * (size_t)n + c] += acc.r;
-            sv.acc[3 * (size_t)n + c] = fmax(sv.acc[3 * (size_t)n + c], acc.mx);
+            const uint32_t g = gid(kp.ids, c);
+            const size_t an = kp.ids ? kp.ids_n : n;   // acc rows: the full batch
+            sv.acc[g] += acc.pv;
+            sv.acc[an + g] += acc.m;
+            sv.acc[2 * an + g] += acc.r;
+            sv.acc[3 * an + g] = fmax(sv.acc[3 * an + g], acc.mx);
         }
     }
     if (sv.hist) {
@@ -1027,7 +1036,7 @@ __global__ __launch_bounds__(256) void candidates_kernel(DrawParams dp, StateVie
         *sg.walk_q = 0;
     }
     if (c >= n || (prev.status ? prev.status[c] : st.status[c]) != 0) return;
-    const U4 b = keyed_block(dp.seed, chain0 + c, (uint64_t)(st.ncalls[c] + k), TAG_CLOUD, 0);
+    const U4 b = keyed_block(dp.seed, chain0 + gid(dp.ids, c), (uint64_t)(st.ncalls[c] + k), TAG_CLOUD, 0);
     sg.cand[(size_t)k * n + c] = pow_d(dp.alpha + dp.delta * u52(b.x, b.y), dp.expo);
 }
 
@@ -1391,7 +1400,7 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
                 if (tries - tb >= 16) {   // row-uniform
                     tb = tries;
                     const int t = tries + p;
-                    nb = pow_d(dp.alpha + dp.delta * keyed_u(dp.seed, chain0 + c, ncall, TAG_CLOUD, (uint32_t)(t >> 1), t & 1),
+                    nb = pow_d(dp.alpha + dp.delta * keyed_u(dp.seed, chain0 + gid(dp.ids, c), ncall, TAG_CLOUD, (uint32_t)(t >> 1), t & 1),
                                dp.expo) / ws;
                 }
                 ncl = bperm_f64(row0 | (tries - tb), nb);
@@ -1399,7 +1408,7 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
 #else
             double x;
             if (tries == 0 && x0 >= 0.0) x = x0;
-            else x = pow_d(dp.alpha + dp.delta * keyed_u(dp.seed, chain0 + c, ncall, TAG_CLOUD, (uint32_t)(tries >> 1),
+            else x = pow_d(dp.alpha + dp.delta * keyed_u(dp.seed, chain0 + gid(dp.ids, c), ncall, TAG_CLOUD, (uint32_t)(tries >> 1),
                                                         tries & 1),
                            dp.expo);
             ncl = x / ws;
@@ -1637,7 +1646,7 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
         __syncthreads();
     }
     const uint32_t j0 = b * BLOCK_STEPS, j1 = min(j0 + (uint32_t)BLOCK_STEPS, nsteps);
-    const uint64_t chain = chain0 + c;
+    const uint64_t chain = chain0 + gid(kp.ids, c);
     const int64_t fm = first_minute(utc0, W0);
     // the fp32 PV constants as per-lane registers (VGPRs): held in SGPRs across
     // the loop they are spilled to VGPR lanes and read back by v_readlane each step
@@ -1657,8 +1666,8 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
     const MinuteCtx mc{dp, chain, W0, fm, events, (int)min(*n_events, ev_cap_dev(nsteps)), tab64};
     LaneSite ls{};   // per-chain sites (C5): this chain's site constants
     if constexpr (SITES) {
-        ls.k = site_k(kp.sites + (size_t)(live ? c : 0) * 8);
-        ls.linke = kp.site_linke ? kp.site_linke + (size_t)(live ? c : 0) * 12 : nullptr;
+        ls.k = site_k(kp.sites + (size_t)(live ? gid(kp.ids, c) : 0) * 8);
+        ls.linke = kp.site_linke ? kp.site_linke + (size_t)(live ? gid(kp.ids, c) : 0) * 12 : nullptr;
         ls.tl_doy = -1;
     }
     if (live) {
@@ -1875,6 +1884,76 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
     }
 }
 
+// ------------------------------------------------------------ compaction
+// Batches whose chains fault (the reference's AssertionError in markov mode ends
+// most C5 chains within the week) keep only their live chains in the launches:
+// live_chains_kernel lists the slots with status 0 (in slot order, one
+// workgroup, deterministic), state_move_kernel gathers those slots into a dense
+// working state and scatters them back after the window.  Keyed draws, tables,
+// sites and statistics follow the chain, not the slot (KParams::ids).
+__global__ __launch_bounds__(1024) void live_chains_kernel(StateView st, uint32_t n, const uint32_t* __restrict__ ids_in,
+                                                           uint32_t* __restrict__ ids_out, uint32_t* __restrict__ n_out)
+{
+    __shared__ uint32_t wsum[16];
+    __shared__ uint32_t base;
+    if (threadIdx.x == 0) base = 0;
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (uint32_t c0 = 0; c0 < n; c0 += 1024) {
+        const uint32_t c = c0 + threadIdx.x;
+        const bool live = c < n && st.status[c] == 0;
+        const uint64_t bal = __builtin_amdgcn_ballot_w64(live);
+        const uint32_t below = (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[w] = (uint32_t)__builtin_popcountll(bal);
+        __syncthreads();
+        uint32_t off = base;
+        for (uint32_t k = 0; k < w; ++k) off += wsum[k];
+        if (live) ids_out[off + below] = ids_in ? ids_in[c] : c;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t t = 0;
+            for (uint32_t k = 0; k < 16; ++k) t += wsum[k];
+            base += t;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *n_out = base;
+}
+
+// dst slot i <- src slot map[i] (gather) or dst slot map[i] <- src slot i
+// (scatter), for i < *count; the sigma rows up to the chain's length only
+__global__ __launch_bounds__(256) void state_move_kernel(StateView src, StateView dst, const uint32_t* __restrict__ map,
+                                                         const uint32_t* __restrict__ count, uint32_t cap, int scatter)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= min(*count, cap)) return;
+    const uint32_t a = scatter ? i : map[i], b = scatter ? map[i] : i;   // src slot a -> dst slot b
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        dst.sb[k][b] = src.sb[k][a];
+        dst.sa[k][b] = src.sa[k][a];
+    }
+    dst.cl[b] = src.cl[a];
+    dst.clr[b] = src.clr[a];
+    dst.mstate[b] = src.mstate[a];
+    dst.sec[b] = src.sec[a];
+    const int L = src.L[a];
+    dst.L[b] = L;
+    dst.pos[b] = src.pos[a];
+    dst.status[b] = src.status[a];
+    dst.ncalls[b] = src.ncalls[a];
+    dst.fn[0][b] = src.fn[0][a];
+    dst.fn[1][b] = src.fn[1][a];
+    const double* sc = src.sc + (size_t)a * CAP;
+    const double* sl = src.sl + (size_t)a * CAP;
+    double* dc = dst.sc + (size_t)b * CAP;
+    double* dl = dst.sl + (size_t)b * CAP;
+    for (int k = 0; k < min(L, CAP); ++k) {
+        dc[k] = sc[k];
+        dl[k] = sl[k];
+    }
+}
+
 // fmax into a double in global memory (compare-and-swap; rare: fixup_kernel only)
 __device__ void atomic_fmax(double* p, double v)
 {
@@ -1942,7 +2021,8 @@ __global__ __launch_bounds__(256) void fixup_kernel(KParams kp, DrawParams dp, S
 template <typename R>
 __global__ __launch_bounds__(256) void commit_kernel(StateView st, uint32_t n, SegView sg, StatsView sv, MinuteCtx mc0,
                                                      const uint32_t* __restrict__ n_events,
-                                                     const BlockDesc* __restrict__ desc_end, int markov)
+                                                     const BlockDesc* __restrict__ desc_end, int markov,
+                                                     uint32_t acc_n)
 {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n) return;
@@ -1958,10 +2038,12 @@ __global__ __launch_bounds__(256) void commit_kernel(StateView st, uint32_t n, S
         }
         p += sg.corr[c];                 // fixup_kernel's exact corrections
         r += sg.corr[(size_t)n + c];
-        sv.acc[c] += p;
-        sv.acc[(size_t)n + c] += m;
-        sv.acc[2 * (size_t)n + c] += r;
-        sv.acc[3 * (size_t)n + c] = fmax(sv.acc[3 * (size_t)n + c], mx);
+        const uint32_t g = gid(mc0.dp.ids, c);
+        const size_t an = acc_n ? acc_n : n;   // acc rows: the full batch
+        sv.acc[g] += p;
+        sv.acc[an + g] += m;
+        sv.acc[2 * an + g] += r;
+        sv.acc[3 * an + g] = fmax(sv.acc[3 * an + g], mx);
     }
     if (st.status[c] != 0) return;
     // records lost (never observed: room for ~100x the measured rate): the batch's
@@ -1975,7 +2057,7 @@ __global__ __launch_bounds__(256) void commit_kernel(StateView st, uint32_t n, S
         sp.a[k] = st.sa[k][c];
     }
     MinuteCtx mc = mc0;
-    mc.chain += c;
+    mc.chain += gid(mc.dp.ids, c);
     mc.ne = (int)min(*n_events, sg.evcap);
     if constexpr (sizeof(R) == 4) {   // the fast noise copies from the fp32 table, the fp64 pairs drawn again
         Samp sf = sp;
@@ -2450,6 +2532,7 @@ int tmh_set_sites(struct tmh_engine* eng, const double* sites, const double* lin
 
 static int check_tables(const tmh_engine* eng, uint32_t n_chains)
 {
+    if (eng->kp.ids) n_chains = std::max(n_chains, eng->kp.ids_n);
     if (eng->kp.tab && n_chains > eng->n_tab)
         return fail(TMH_E_INVAL, "batch of %u chains exceeds the %u per-chain shape tables", n_chains, eng->n_tab);
     if (eng->kp.sites && n_chains > eng->n_sites)
@@ -2470,6 +2553,37 @@ int tmh_set_walk_chains_per_row(struct tmh_engine* eng, uint32_t chains_per_row)
     if (chains_per_row > 64) return fail(TMH_E_INVAL, "chains_per_row %u > 64", chains_per_row);
     eng->walk_cpr = chains_per_row ? chains_per_row : 1;
     return TMH_OK;
+}
+
+int tmh_set_chain_ids(struct tmh_engine* eng, const uint32_t* ids, uint32_t n_full)
+{
+    if (!eng) return fail(TMH_E_INVAL, "NULL engine");
+    if (ids && n_full == 0) return fail(TMH_E_INVAL, "chain ids with n_full 0");
+    eng->kp.ids = eng->dp.ids = ids;
+    eng->kp.ids_n = ids ? n_full : 0;
+    return TMH_OK;
+}
+
+int tmh_live_chains(struct tmh_engine* eng, const void* state, uint32_t n_chains, const uint32_t* ids_in,
+                    uint32_t* ids_out, uint32_t* n_live, void* stream)
+{
+    if (!eng || !state || !ids_out || !n_live) return fail(TMH_E_INVAL, "NULL engine/state/ids_out/n_live");
+    if (int rc = hip_check(hipSetDevice(eng->device), "hipSetDevice")) return rc;
+    hipLaunchKernelGGL(live_chains_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream,
+                       make_view(const_cast<void*>(state), n_chains), n_chains, ids_in, ids_out, n_live);
+    return hip_check(hipGetLastError(), "live_chains_kernel launch");
+}
+
+int tmh_state_move(struct tmh_engine* eng, const void* src, uint32_t n_src, void* dst, uint32_t n_dst,
+                   const uint32_t* map, const uint32_t* count, uint32_t cap, int scatter, void* stream)
+{
+    if (!eng || !src || !dst || !map || !count) return fail(TMH_E_INVAL, "NULL engine/src/dst/map/count");
+    if (cap > (scatter ? n_src : n_dst)) return fail(TMH_E_INVAL, "cap %u exceeds the moved-to/from slots", cap);
+    if (cap == 0) return TMH_OK;
+    if (int rc = hip_check(hipSetDevice(eng->device), "hipSetDevice")) return rc;
+    hipLaunchKernelGGL(state_move_kernel, dim3((cap + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       make_view(const_cast<void*>(src), n_src), make_view(dst, n_dst), map, count, cap, scatter);
+    return hip_check(hipGetLastError(), "state_move_kernel launch");
 }
 
 int tmh_test_set_segment_capacity(uint32_t cap, uint32_t pool_chunks)
@@ -2704,10 +2818,10 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     const MinuteCtx mc{eng->dp, chain0, step0, first_minute_host(utc0, step0), pv.events, 0, pv.tab64};
     if (f64)
         hipLaunchKernelGGL(commit_kernel<double>, dim3(cb), dim3(256), 0, s, v, n_chains, sg, sv, mc, pv.n_events,
-                           pv.desc + nblk_of(n_steps), eng->dp.markov);
+                           pv.desc + nblk_of(n_steps), eng->dp.markov, eng->kp.ids ? eng->kp.ids_n : 0u);
     else
         hipLaunchKernelGGL(commit_kernel<float>, dim3(cb), dim3(256), 0, s, v, n_chains, sg, sv, mc, pv.n_events,
-                           pv.desc + nblk_of(n_steps), eng->dp.markov);
+                           pv.desc + nblk_of(n_steps), eng->dp.markov, eng->kp.ids ? eng->kp.ids_n : 0u);
     eng->close(TMH_K_STEP, t_step, s);
     return hip_check(hipGetLastError(), "commit_kernel launch");
 }

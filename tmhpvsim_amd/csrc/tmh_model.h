@@ -38,7 +38,13 @@ struct KParams {
     const int32_t* tab_t;                       // per-chain Student-t flags [n][6] (NULL: is_t)
     const double* sites;                        // per-chain PV sites [n][8] (NULL: the plan's site)
     const double* site_linke;                   // per-chain monthly Linke turbidity [n][12] (NULL: params)
+    const uint32_t* ids;                        // slot -> chain (tmh_set_chain_ids; NULL: slot c is chain c)
+    uint32_t ids_n, pad_;                       // chains of the full batch (row count of tables, sites, acc)
 };
+
+// The chain in launch slot c (a compacted batch runs only its live chains; its
+// keyed draws, tables, sites and statistics stay those of the original chain).
+__device__ __forceinline__ uint32_t gid(const uint32_t* ids, uint32_t c) { return ids ? ids[c] : c; }
 
 struct GParams {
     double site[8];
@@ -377,6 +383,7 @@ struct DrawParams {
     int32_t fb_is_t, fb_bin;
     const double* tab;               // per-chain shape tables (KParams::tab)
     const int32_t* tab_t;
+    const uint32_t* ids;             // KParams::ids
     int32_t markov, pad;             // cc_mode markov: hourly draws come from markov_cc_kernel
 };
 
