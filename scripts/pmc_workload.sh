@@ -7,6 +7,8 @@ set -u
 ROOT="${GRAFT_REPO_ROOT:-/root/repo}"
 TAG=$1 WL=$2 CH=$3 LS=$4 PREC=$5 MODE=$6 CC=$7
 shift 7
+EXTRA=""
+while [ $# -gt 0 ] && [ "$1" != "--" ]; do EXTRA="$EXTRA $1"; shift; done   # extra record keys k=v
 [ "${1:-}" = "--" ] && shift
 ARGS="$*"
 export TMPDIR=/tmp
@@ -25,7 +27,7 @@ for counters in \
 done
 cd "$ROOT"
 python3 scripts/pmc_summary.py "$OUT" > "$OUT/summary.txt" 2>&1
-python3 scripts/pmc_summary.py "$OUT" --record workload=$WL chains=$CH launch_seconds=$LS precision=$PREC mode=$MODE cc=$CC \
+python3 scripts/pmc_summary.py "$OUT" --record workload=$WL chains=$CH launch_seconds=$LS precision=$PREC mode=$MODE cc=$CC $EXTRA \
     > "$OUT/record.json" || exit 1
 cp profiles/pmc_kernels.json gpurun_out/pmc_kernels.json
 cat "$OUT/record.json"
