@@ -47,8 +47,8 @@ VALU_PEAK_TLANE = 256 * 4 * 32 * 2.4e9 / 1e12
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
-                    help="c2: the headline (BASELINE.json configs[1]); c3: 1,048,576 chains x 1 day, stats, one "
-                         "batch in flight (126 GB of scratch); c4: 16,384 chains x the year 2019 "
+                    help="c2: the headline (BASELINE.json configs[1]); c3: 1,048,576 chains x 1 day, stats, two "
+                         "batches in flight (74 GB of scratch each); c4: 16,384 chains x the year 2019 "
                          "(Europe/Berlin wall clock, stats, day windows); c5: the lat/lon sweep (65,536 sites x 1 "
                          "week, markov cc with per-site tables, per-site PV geometry, stats mode, day windows)")
     ap.add_argument("--gpus", type=int, default=1)
@@ -109,7 +109,8 @@ def parse():
     if a.compact is None:
         a.compact = int(c5)
     a.build_ahead = a.build_ahead or max(1, a.walks) + 1
-    a.pipeline = a.pipeline or (1 if a.workload == "c3" else a.build_ahead + 1)
+    # c3: two 1 M-chain batches in flight (2 x 83 GB of state + scratch): +3 % over one (r02)
+    a.pipeline = a.pipeline or (2 if a.workload == "c3" else a.build_ahead + 1)
     if a.minutes_ahead is None:
         a.minutes_ahead = int(a.walks > 1)
     if a.commit_stream is None:

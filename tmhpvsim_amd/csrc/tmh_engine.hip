@@ -1605,6 +1605,9 @@ __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t rs, uint32_t of
 #ifndef TMH_EXP_CHAIN_FAST
 #define TMH_EXP_CHAIN_FAST 0
 #endif
+#ifndef TMH_ROW_PREFETCH   // fp32 single-site expansion: next second's geometry row loaded early
+#define TMH_ROW_PREFETCH 0
+#endif
 #ifndef TMH_PVF_VGPR   // leading PVF fields pinned in VGPRs in the fp32 expansion
 #define TMH_PVF_VGPR 8
 #endif
@@ -1761,10 +1764,21 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
     const int32_t fault_eff = alive ? fault : 0;   // ok = j < fault_eff: one compare, no branch
     // One second.  Every lane computes it; a lane whose chain is faulted (or not
     // alive) emits NaN / no statistics.  un, um: the step's Philox words (noise, meter).
+    // fp32 single-site: the next second's geometry row is loaded (SMEM) as soon as this
+    // second's PV chain is done with the current one, so its latency overlaps the
+    // stores and bookkeeping instead of stalling the next second's first use (PMC:
+    // 40 % of the waves' cycles parked at s_waitcnt).  The load past the window's
+    // last row reads the plan's next table (unused).
+    constexpr bool PF = TMH_ROW_PREFETCH && sizeof(R) == 4 && !SITES;
+    R rowpf[row_w<R>()];
+    if constexpr (PF) {
+#pragma unroll
+        for (int i = 0; i < row_w<R>(); ++i) rowpf[i] = rowp[i];
+    }
     auto second = [&](uint32_t j, uint32_t un, uint32_t um) {
         R row[row_w<R>()];
 #pragma unroll
-        for (int i = 0; i < row_w<R>(); ++i) row[i] = rowp[i];
+        for (int i = 0; i < row_w<R>(); ++i) row[i] = PF ? rowpf[i] : rowp[i];
         rowp += RW;
         const uint32_t fl = sizeof(R) == 8 ? (uint32_t)(double)rowp[G_FLAGS - RW] : __float_as_uint(row[G_FLAGS + G32]);
         const bool ok = (int32_t)j < fault_eff;
@@ -1814,6 +1828,10 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
         R csi, pv, meter, res;
         bool held = false;   // fp32: PV in a guard band, recomputed in fp64 by fixup_kernel
         second_body<R>(kp, pkv, row, flp, fs, covered, noise_z<R>(un), meter_w<R>(um), csi, pv, meter, res, held);
+        if constexpr (PF) {
+#pragma unroll
+            for (int i = 0; i < row_w<R>(); ++i) rowpf[i] = rowp[i];
+        }
         held = held && ok;
         if constexpr (sizeof(R) == 4) {
 #if TMH_HELD_LDS
