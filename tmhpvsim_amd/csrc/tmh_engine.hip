@@ -1126,14 +1126,6 @@ constexpr int RCH = TMH_RCH;   // register chunks of 16 entries: sigma entries 0
 #define TMH_RCH_FIXED 4
 #endif
 constexpr int RCH_FIXED = TMH_RCH_FIXED;   // chunks always processed; chunk ch >= RCH_FIXED only when some row needs it
-#ifndef TMH_LCH
-#define TMH_LCH 0
-#endif
-// chunks RCH .. RCH + LCH - 1 in LDS (16 rows per workgroup x LCH chunks x 16 lanes,
-// 512 B per chunk and row), scanned only when some row of the wave needs them;
-// entries past 16 (RCH + LCH) in the chain's global sigma row
-constexpr int LCH = TMH_LCH;
-constexpr int GCH = RCH + LCH;   // first chunk in global memory
 
 // P1: segment walk.  Four chains per wavefront, one per row of 16 lanes; entry
 // k of a chain's sigma arrays lives in chunk k / 16, lane k % 16 of its row
@@ -1168,8 +1160,6 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
     const int64_t W1 = W0 + nsteps;
     const uint32_t nev = min(*n_events, ev_cap_dev(nsteps));
     const WinClock wck = win_clock(ck, W0);
-    __shared__ double lsc[16][LCH > 0 ? LCH : 1][16], lsl[16][LCH > 0 ? LCH : 1][16];   // the LDS chunks
-    const int rowi = threadIdx.x >> 4;
     // Rows take chains: row r starts with chain r, and a row whose chain is done
     // takes the next unstarted one from the window's queue (chains rows.. n - 1), so
     // with fewer rows than chains the walk's waves stay busy instead of idling
@@ -1271,12 +1261,6 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
             vc[ch] = k < L ? gsc[k] : 0.0;
             vl[ch] = k < L ? gsl[k] : 0.0;
         }
-#pragma unroll
-        for (int q = 0; q < LCH; ++q) {
-            const int k = (RCH + q) * 16 + p;
-            lsc[rowi][q][p] = k < L ? gsc[k] : 0.0;
-            lsl[rowi][q][p] = k < L ? gsl[k] : 0.0;
-        }
         s_start = W0 - sec0;   // step at which sec was 1
         e = s_start + ceil_thr(cl + clr) - 1;
         rec = sg.rec + (size_t)cs * sg.cap;
@@ -1315,14 +1299,6 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
                 if (k < L) {
                     gsc[k] = vc[ch];
                     gsl[k] = vl[ch];
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < LCH; ++q) {   // and the LDS chunks
-                const int k = (RCH + q) * 16 + p;
-                if (k < L) {
-                    gsc[k] = lsc[rowi][q][p];
-                    gsl[k] = lsl[rowi][q][p];
                 }
             }
             if (p == 0) {
@@ -1456,15 +1432,10 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
 #pragma unroll
             for (int ch = RCH_FIXED; ch < RCH; ++ch)
                 if (Lmax > 16 * ch) scan(ch * 16 + p, vc[ch], vl[ch]);   // wave-uniform
-#pragma unroll
-            for (int q = 0; q < LCH; ++q)
-                if (Lmax > 16 * (RCH + q)) scan((RCH + q) * 16 + p, lsc[rowi][q][p], lsl[rowi][q][p]);   // wave-uniform
-#ifndef TMH_DIAG_WALK_NOGLOBAL   // diagnostic only (wrong results): no global sigma chunks
-            for (int ch = GCH; ch * 16 < L; ++ch) {   // rare: entries 16 GCH..
+            for (int ch = RCH; ch * 16 < L; ++ch) {   // rare: entries 128..
                 const int k = ch * 16 + p;
                 if (k < L) scan(k, gsc[k], gsl[k]);
             }
-#endif
             const double dmin = row_min_f64(bd);
             if (dmin < INFINITY) {
                 last = row_min_i32(bd == dmin ? bk : INT_MAX);
@@ -1529,40 +1500,21 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
             sc_last = bperm_f64(src, a);
             sl_last = bperm_f64(src, b);
         }
-        if (lc >= GCH) {
+        if (lc >= RCH) {
             sc_last = gsc[last];
             sl_last = gsl[last];
-        } else if (lc >= RCH) {   // row-uniform address: an LDS broadcast read
-            sc_last = lsc[rowi][lc - RCH][last & 15];
-            sl_last = lsl[rowi][lc - RCH][last & 15];
         }
         const double nclr = f * (ncl + sc_last) - sl_last;
         // entry 16 RCH - 1 (register chunk RCH - 1, lane 15) for lane 0 of the first global chunk:
         // the DPP runs with the whole row active (under a p == 0 branch lane 15 would be
         // masked off and the read would return the DPP's old value)
-        const double carry_g = LCH > 0 ? lsc[rowi][LCH > 0 ? LCH - 1 : 0][15] : dpp_row_f64<0x121>(0.0, vc[RCH - 1]);
-#ifndef TMH_DIAG_WALK_NOGLOBAL
-        for (int ch = top; ch >= GCH; --ch) {   // rare, descending: reads before writes
+        const double carry_g = dpp_row_f64<0x121>(0.0, vc[RCH - 1]);
+        for (int ch = top; ch >= RCH; --ch) {   // rare, descending: reads before writes
             const int k = ch * 16 + p;
-            const double prev = (ch == GCH && p == 0) ? carry_g : gsc[k - 1];
+            const double prev = (ch == RCH && p == 0) ? carry_g : gsc[k - 1];
             const double nsc = ncl + prev;
             gsc[k] = nsc;
             gsl[k] = f * nsc;
-        }
-#endif
-        if (LCH > 0) {   // the LDS chunks, descending: every lane reads before any lane writes
-            const double carry_r = dpp_row_f64<0x121>(0.0, vc[RCH - 1]);   // whole row active
-#pragma unroll
-            for (int q = LCH - 1; q >= 0; --q) {
-                if (topmax >= RCH + q) {   // wave-uniform
-                    const double prev = p == 0 ? (q == 0 ? carry_r : lsc[rowi][q > 0 ? q - 1 : 0][15])
-                                               : lsc[rowi][q][p > 0 ? p - 1 : 0];
-                    const double nsc = ncl + prev;
-                    asm volatile("" ::: "memory");   // the row's reads of this chunk before its writes
-                    lsc[rowi][q][p] = nsc;
-                    lsl[rowi][q][p] = f * nsc;
-                }
-            }
         }
         // rows with a lower top rewrite entries >= their new L: harmless
 #pragma unroll
