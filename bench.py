@@ -582,8 +582,10 @@ def main():
                 "valu": valu(kms_launch)}
     else:
         v = valu(kms_launch) or {}
+        va = valu(alone_ms / nwin) or {}   # the same launch with no other batch in flight
         roof = {"bound": "valu", "achieved": v.get("achieved"), "peak": VALU_PEAK_TLANE, "unit": "T lane-ops/s",
                 "frac": v.get("frac"), "traffic": rec["traffic_bytes_per_launch"] if rec else None,
+                "alone": {"kernel_ms": alone_ms / nwin, "achieved": va.get("achieved"), "frac": va.get("frac")},
                 "kernel": "expand_kernel (P2, " + sim.path + ")", "kernel_ms": kms_launch,
                 "launches_per_batch": nwin, "chain_seconds_per_launch": n * launch_secs,
                 "valu_per_chain_second": v.get("valu_per_chain_second"),

@@ -13,6 +13,6 @@ for spec in "$@"; do
   TMHPVSIM_LIB=$so timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline $bargs > gpurun_out/vab_${TAG}_$name.json 2> gpurun_out/vab_${TAG}_$name.err || exit $?
   python3 -c "
 import json; d=json.loads(open('gpurun_out/vab_${TAG}_$name.json').read()); r=d['roofline']
-print('$name value %.4g ms/step %.3f expand %.3f alone %.3f' % (d['value'], d['ms_per_step'], r['kernel_ms'], r['alone']['kernel_ms']), {k: round(v, 3) for k, v in d['phases_ms'].items() if v})"
+print('$name value %.4g ms/step %.3f expand %.3f alone %.3f' % (d['value'], d['ms_per_step'], r['kernel_ms'], (r.get('alone') or {}).get('kernel_ms', float('nan'))), {k: round(v, 3) for k, v in d['phases_ms'].items() if v})"
 done
 done

@@ -1617,8 +1617,8 @@ __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t rs, uint32_t of
 #ifndef TMH_EXP_WAVES   // min waves per SIMD of the fp32 single-site expansion: 7 = at most 72 VGPRs (alone -4 % vs 6, no VGPR spills)
 #define TMH_EXP_WAVES 7
 #endif
-#ifndef TMH_EXP_WAVES_STATS   // the same for the statistics / other outputs (C3, C4): 5 = 96 VGPRs (their 16-KB LDS histogram + 12 KB staging allow 5 workgroups per CU anyway)
-#define TMH_EXP_WAVES_STATS 5
+#ifndef TMH_EXP_WAVES_STATS   // the same for the statistics / other outputs (C3, C4): 6 = 80 VGPRs (the 16-bit-pair LDS histogram, 8 KB, + 12 KB staging: 8 workgroups per CU; C3 / C4 +6 % over 5 waves)
+#define TMH_EXP_WAVES_STATS 6
 #endif
 template <typename R, int OUT, bool SITES>
 #ifndef TMH_SITES_WAVES   // min waves per SIMD of the per-chain-site expansion: 2 (a few spills) is 35 % faster than 1
@@ -1645,7 +1645,7 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
 #endif
     const bool live = c < n;
     if (sv.hist) {
-        for (uint32_t i = threadIdx.x; i < sv.n_bins; i += blockDim.x) lds_hist[i] = 0;
+        for (uint32_t i = threadIdx.x; i < (sv.n_bins + 1) / 2; i += blockDim.x) lds_hist[i] = 0;   // 16-bit bin pairs
         __syncthreads();
     }
     const uint32_t j0 = b * BLOCK_STEPS, j1 = min(j0 + (uint32_t)BLOCK_STEPS, nsteps);
@@ -1850,7 +1850,7 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
         const uint8_t cov = ok ? (covered ? 1 : 0) : 255;
 #ifdef TMH_DIAG_NO_STORE
         if (live && csi == R(-12345))
-            emit<R, OUT>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok, held);
+            emit<R, OUT, true>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok, held);
 #else
         if constexpr (OUT == OUT_TRACE3) {
             row_store(rs_pv, voff, pv);
@@ -1858,7 +1858,7 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
             row_store(rs_r, voff, res);
             voff += rowb;
         } else if (live) {
-            emit<R, OUT>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok, held);
+            emit<R, OUT, true>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok, held);
         }
 #endif
     };
@@ -1897,8 +1897,11 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
     }
     if (sv.hist) {
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < sv.n_bins; i += blockDim.x)
-            if (lds_hist[i]) atomicAdd((unsigned long long*)&sv.hist[i], (unsigned long long)lds_hist[i]);
+        for (uint32_t i = threadIdx.x; i < (sv.n_bins + 1) / 2; i += blockDim.x) {
+            const uint32_t w = lds_hist[i], lo = w & 0xFFFFu, hi = w >> 16;
+            if (lo) atomicAdd((unsigned long long*)&sv.hist[2 * i], (unsigned long long)lo);
+            if (hi) atomicAdd((unsigned long long*)&sv.hist[2 * i + 1], (unsigned long long)hi);   // hi = 0 past n_bins
+        }
     }
 }
 
@@ -2803,8 +2806,9 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     if (out == OUT_TRACE3 && tv.ld * (f64 ? 8u : 4u) * BLOCK_STEPS >= (1ull << 31))   // one block's rows: one buffer range
         return fail(TMH_E_INVAL, "trace ld %llu too large (a 128-step block of rows must stay under 2 GiB)",
                     (unsigned long long)tv.ld);
+    const size_t lds_exp = stats && stats->hist ? (size_t)((stats->n_bins + 1) / 2) * 4 : 0;   // 16-bit bin pairs
 #define LAUNCH(R, O, S)                                                                                            \
-    hipLaunchKernelGGL((expand_kernel<R, O, S>), grid2, dim3(256), lds + TMH_DIAG_EXP_LDS, s, eng->kp, eng->dp, v, chain0, n_chains,      \
+    hipLaunchKernelGGL((expand_kernel<R, O, S>), grid2, dim3(256), lds_exp + TMH_DIAG_EXP_LDS, s, eng->kp, eng->dp, v, chain0, n_chains,      \
                        step0, n_steps, utc0, pv.tab64, pv.tab32, pv.sun, pv.events, pv.n_events, pv.desc, sg, tv, sv)
     if (eng->kp.sites) {   // per-chain sites: one instantiation per precision, any output
         if (f64) LAUNCH(double, OUT_ANY, true);

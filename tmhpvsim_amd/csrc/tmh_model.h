@@ -1255,7 +1255,9 @@ enum : int {
 // held: a guard-band second whose pv / residual fixup_kernel replaces; it enters
 // the sums here (fixup_kernel adds the exact difference) but not the maximum or
 // the histogram (fixup_kernel adds its final value)
-template <typename R, int OUT = OUT_ANY>
+// PACK: the workgroup's LDS histogram holds two 16-bit bins per word (a 128-second
+// block of 256 chains adds at most 32,768 to a bin), half the LDS of one word each
+template <typename R, int OUT = OUT_ANY, bool PACK = false>
 __device__ __forceinline__ void emit(const TraceView& tr, const StatsView& sv, uint32_t* lds_hist, uint64_t o,
                                      uint8_t cov, R csi, R pv, R meter, R res, Acc& acc, bool ok, bool held = false)
 {
@@ -1282,7 +1284,8 @@ __device__ __forceinline__ void emit(const TraceView& tr, const StatsView& sv, u
         if (sv.hist && !held) {
             const double x = ((double)res - sv.lo) * sv.scale;
             const int bin = x < 0.0 ? 0 : (x >= (double)(sv.n_bins - 1) ? (int)sv.n_bins - 1 : (int)x);
-            atomicAdd(&lds_hist[bin], 1u);
+            if constexpr (PACK) atomicAdd(&lds_hist[bin >> 1], 1u << ((bin & 1) << 4));
+            else atomicAdd(&lds_hist[bin], 1u);
         }
     }
 }
