@@ -30,4 +30,5 @@ python3 scripts/pmc_summary.py "$OUT" > "$OUT/summary.txt" 2>&1
 python3 scripts/pmc_summary.py "$OUT" --record workload=$WL chains=$CH launch_seconds=$LS precision=$PREC mode=$MODE cc=$CC $EXTRA \
     > "$OUT/record.json" || exit 1
 cp profiles/pmc_kernels.json gpurun_out/pmc_kernels.json
+rm -rf "$OUT"/p[0-9]*/   # the per-dispatch CSVs (tens of MB for C4); summary.txt and record.json stay
 cat "$OUT/record.json"
