@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--walk-cpr", type=int, default=1,
                     help="chains per walk row (tmh_set_walk_chains_per_row): the walk launches n / cpr rows "
                          "that take the next chain when theirs is done")
+    ap.add_argument("--walk-lanes", type=int, default=0,
+                    help="lanes per chain in the segment walk (tmh_set_walk_lanes: 4, 8 or 16; 0 = the build's default)")
     ap.add_argument("--build-ahead", type=int, default=None,
                     help="gated schedule: when the walk of batch k ends, the construction of batch k + A is "
                          "released (default A = walks + 1; needs --pipeline >= A + 1)")
@@ -220,6 +222,8 @@ def main():
     real = sim.real
     if args.walk_cpr != 1:
         _lib.check(L.tmh_set_walk_chains_per_row(sim._eng, args.walk_cpr))
+    if args.walk_lanes:
+        _lib.check(L.tmh_set_walk_lanes(sim._eng, args.walk_lanes))
 
     nwin = (secs + win - 1) // win
     prio_lo, prio_hi = torch.cuda.Stream.priority_range()
@@ -606,7 +610,7 @@ def main():
                    "batches_in_flight": len(ctxs), "staggered": bool(args.stagger and nwin == 1),
                    "construction_on": args.build_on, "walk_priority": args.walk_priority,
                    "schedule": args.schedule if (args.stagger and nwin == 1 and len(ctxs) >= 3) else None,
-                   "walks_in_flight": W, "walk_chains_per_row": args.walk_cpr, "build_ahead": A,
+                   "walks_in_flight": W, "walk_chains_per_row": args.walk_cpr, "walk_lanes": args.walk_lanes or None, "build_ahead": A,
                    "minutes_ahead": bool(args.minutes_ahead), "commit_stream": bool(args.commit_stream),
                    "compacted_windows": bool(args.compact and args.mode == "stats" and nwin > 1)},
         "roofline": roof,

@@ -160,6 +160,11 @@ size_t tmh_workspace_bytes(uint32_t n_chains, uint32_t n_steps);
  * beside other kernels).  Results do not depend on k.  0 or 1 = one chain per row
  * (default); at most 64. */
 int tmh_set_walk_chains_per_row(struct tmh_engine* eng, uint32_t chains_per_row);
+/* Lanes per chain in the segment walk: 16 (four chains per wavefront), 8 or 4
+ * (sixteen chains per wavefront, four times the sigma entries per lane); 0 = the
+ * build's default.  Fewer lanes per chain: fewer issue slots and waves per
+ * chain-call, more work per lane.  Results do not depend on it. */
+int tmh_set_walk_lanes(struct tmh_engine* eng, uint32_t lanes);
 /* Compaction (batches whose chains fault, e.g. the reference's markov-mode
  * AssertionError, cloud_cover_binary.py:91): run later windows on the live chains
  * only.  A launch slot then holds chain ids[slot] of a full batch of n_full chains:

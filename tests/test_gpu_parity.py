@@ -467,6 +467,37 @@ def test_walk_chains_per_row_invariance(window):
             np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("window", [86400, 7200])
+def test_walk_lanes_invariance(window):
+    """tmh_set_walk_lanes: the segment walk with 4, 8 or 16 lanes per chain (sigma
+    entries spread over fewer lanes, more register chunks per lane; entries past
+    the registers in the chain's global row) gives bit-identical results -- covered
+    bit, PV, status, call counts and the window-end sigma arrays -- alone and with
+    groups that take queued chains, in one window or in chained windows.  2,000
+    chain-days reach sigma lengths past 64 (~0.5 % of the calls) on every path."""
+    from tmhpvsim_amd import _lib
+    L = _lib.load()
+    n, steps, start = 2000, 86400, "2019-09-05 00:00:00"
+    outs = []
+    for lanes, cpr in ((16, 1), (8, 1), (4, 1), (4, 3), (8, 2)):
+        s = _sim(n, start, tz="Europe/Berlin", prec="fp32", kernel_path="time_parallel", horizon=steps)
+        _lib.check(L.tmh_set_walk_lanes(s._eng, lanes))
+        _lib.check(L.tmh_set_walk_chains_per_row(s._eng, cpr))
+        out = s.run(steps, trace=("covered", "pv"), window=window)
+        torch.cuda.synchronize()
+        outs.append((s.status(), _np(out["covered"]), _np(out["pv"]), s.state_field("ncalls").cpu().numpy(),
+                     s.state_field("sigma_len").cpu().numpy(), s.state_field("sigma_cloud").cpu().numpy(),
+                     s.state_field("sigma_clear").cpu().numpy()))
+    Lend = outs[0][4]
+    assert Lend.max() > 40
+    for o in outs[1:]:
+        for i, (a, b) in enumerate(zip(outs[0], o)):
+            if i >= 5:   # sigma rows: entries < L only
+                m = np.arange(a.shape[1])[None, :] < Lend[:, None]
+                a, b = np.where(m, a, 0), np.where(m, b, 0)
+            np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize("markov", [False, True])
 def test_parts_minutes_ahead_equal_step(markov):
     """bench.py's gated order through the C-ABI -- draws, the minute table ahead

@@ -65,7 +65,7 @@ EXPORTS = ["tmh_abi_version", "tmh_last_error", "tmh_state_bytes", "tmh_state_of
            "tmh_init", "tmh_run", "tmh_plan", "tmh_step", "tmh_probe", "tmh_profile_enable", "tmh_profile_read",
            "tmh_set_shape_tables", "tmh_set_sites", "tmh_walk", "tmh_expand",
            "tmh_walk_part", "tmh_expand_part", "tmh_set_clock", "tmh_test_set_segment_capacity",
-           "tmh_set_walk_chains_per_row", "tmh_set_chain_ids", "tmh_live_chains", "tmh_state_move"]
+           "tmh_set_walk_chains_per_row", "tmh_set_walk_lanes", "tmh_set_chain_ids", "tmh_live_chains", "tmh_state_move"]
 K_EXPAND, K_SEGMENTS, K_CANDIDATES, K_STEP = 0, 1, 2, 3
 WALK_DRAWS, WALK_SEGMENTS = 1, 2
 EXPAND_KERNEL, EXPAND_COMMIT, EXPAND_MINUTES, EXPAND_NO_MINUTES = 1, 2, 4, 8
@@ -105,6 +105,8 @@ def load():
     L.tmh_test_set_segment_capacity.argtypes = [u32, u32]
     if hasattr(L, "tmh_set_walk_chains_per_row"):
         L.tmh_set_walk_chains_per_row.argtypes = [p, u32]
+    if hasattr(L, "tmh_set_walk_lanes"):
+        L.tmh_set_walk_lanes.argtypes = [p, u32]
     if hasattr(L, "tmh_set_chain_ids"):
         L.tmh_set_chain_ids.argtypes = [p, p, u32]
         L.tmh_live_chains.argtypes = [p, p, u32, p, p, p, p]

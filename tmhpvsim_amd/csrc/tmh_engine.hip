@@ -1044,7 +1044,7 @@ __global__ __launch_bounds__(256) void candidates_kernel(DrawParams dp, StateVie
 __device__ uint64_t g_p1diag[65536 * 8];
 #endif
 
-// ---- 16-lane row primitives (DPP inside each row of 16 lanes: one chain per row)
+// ---- lane-group primitives (DPP inside groups of G = 4, 8 or 16 lanes: one chain per group)
 template <int CTRL>
 __device__ __forceinline__ double dpp_row_f64(double old, double v)
 {
@@ -1053,27 +1053,36 @@ __device__ __forceinline__ double dpp_row_f64(double old, double v)
     return __hiloint2double(hi, lo);
 }
 
-__device__ __forceinline__ double row_min_f64(double v)
+// min over the G lanes of each group: quad_perm [1,0,3,2], [2,3,0,1], then
+// row_half_mirror (G >= 8: the other quad of the half row), row_mirror (G = 16)
+template <int G>
+__device__ __forceinline__ double grp_min_f64(double v)
 {
-    v = fmin(v, dpp_row_f64<0xB1>(v, v));    // quad_perm [1,0,3,2]
-    v = fmin(v, dpp_row_f64<0x4E>(v, v));    // quad_perm [2,3,0,1]
-    v = fmin(v, dpp_row_f64<0x141>(v, v));   // row_half_mirror
-    v = fmin(v, dpp_row_f64<0x140>(v, v));   // row_mirror
+    v = fmin(v, dpp_row_f64<0xB1>(v, v));
+    v = fmin(v, dpp_row_f64<0x4E>(v, v));
+    if constexpr (G >= 8) v = fmin(v, dpp_row_f64<0x141>(v, v));
+    if constexpr (G >= 16) v = fmin(v, dpp_row_f64<0x140>(v, v));
     return v;
 }
 
-__device__ __forceinline__ int row_min_i32(int v)
+template <int G>
+__device__ __forceinline__ int grp_min_i32(int v)
 {
     v = min(v, __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false));
     v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false));
-    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false));
-    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false));
+    if constexpr (G >= 8) v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false));
+    if constexpr (G >= 16) v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false));
     return v;
 }
 
-// max over the four rows of a row-uniform value (wave-uniform result, SGPR)
-__device__ __forceinline__ int rows_max(int v)
+// max over the wave of a group-uniform value (wave-uniform result, SGPR).  Every
+// lane must be active: the DPP steps fold the groups of a row together first
+// (row_half_mirror pairs the quads of a half row, row_mirror the halves).
+template <int G>
+__device__ __forceinline__ int wave_max_grp(int v)
 {
+    if constexpr (G <= 4) v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false));
+    if constexpr (G <= 8) v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false));
     const int a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
     const int c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
     return max(max(a, b), max(c, d));
@@ -1086,32 +1095,40 @@ __device__ __forceinline__ double bperm_f64(int src_lane, double v)
     return __hiloint2double(hi, lo);
 }
 
-#ifndef TMH_RCH
-#define TMH_RCH 4
+#ifndef TMH_WALK_LANES_DEFAULT   // lanes per chain of the walk unless tmh_set_walk_lanes says otherwise
+#define TMH_WALK_LANES_DEFAULT 16
+#endif
+#ifndef TMH_WALK_REG   // sigma entries held in VGPRs per chain (entries past them: the chain's global row)
+#define TMH_WALK_REG 64
+#endif
+#ifndef TMH_WALK_FIX   // sigma entries scanned unconditionally (>= 12: a reset_sigma array); the rest only when some chain of the wave needs them
+#define TMH_WALK_FIX 32
 #endif
 #ifndef TMH_DOOM_SKIP   // skip provably rejected tries (bit-exact, GPU-tested; measured: walk +1-3 %, off)
 #define TMH_DOOM_SKIP 0
 #endif
+static_assert(TMH_WALK_FIX >= 12, "reset_sigma writes up to 11 entries into the unconditional chunks");
+constexpr int WALK_CAND = 32;   // try-0 candidates per LDS refill of a chain (one exposed load per 32 calls)
 
-// True if, for the row's sigma arrays (lane-distributed: entry k = chunk k / 16,
-// lane k % 16), no cloud length a candidate can take (x / ws, x in the
+// True if, for the group's sigma arrays (lane-distributed: entry k = chunk k / G,
+// lane k % G), no cloud length a candidate can take (x / ws, x in the
 // power law's [xmin, xmax], cloud_cover_binary.py:35-40) makes any entry
 // possible (:83-87).  In real arithmetic entry k is possible for
 // ncl in (sl_k / f - sc_k, 5400 / (1 + f) - sc_k); the tests below keep a
 // relative margin of 1e-6, far above the few-ulp difference between these and
 // the fp64 predicate, so "doomed" never holds while some candidate could pass.
-// Entries past the register chunks (L > 16 RCH): not doomed (no shortcut).
-template <int NCH>
-__device__ __forceinline__ bool row_doomed(const double (&vc)[NCH], const double (&vl)[NCH], int L, int p, int row0,
+// Entries past the register chunks: not doomed (no shortcut).
+template <int G, int NCH>
+__device__ __forceinline__ bool grp_doomed(const double (&vc)[NCH], const double (&vl)[NCH], int L, int p, int row0,
                                            double f, double ws, const DrawParams& dp)
 {
     constexpr double m = 1e-6;
     const double rws = 1.0 / ws;
     const double cmin = dp.x_lo * rws * (1.0 - m), cmax = dp.x_hi * rws * (1.0 + m);
-    bool hope = L > 16 * NCH;
+    bool hope = L > G * NCH;
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
-        const int k = ch * 16 + p;
+        const int k = ch * G + p;
         const double sc = vc[ch], sl = vl[ch];
         const bool h1 = sl * (1.0 + f) < 5400.0 * f * (1.0 + m);   // sl / f < 5400 / (1 + f)
         const bool h2 = sl < f * (cmax + sc) * (1.0 + m);          // some ncl <= cmax passes nsl > sl
@@ -1119,54 +1136,59 @@ __device__ __forceinline__ bool row_doomed(const double (&vc)[NCH], const double
         hope |= (k < L) & h1 & h2 & h3;
     }
     const uint64_t bal = __builtin_amdgcn_ballot_w64(hope);
-    return ((bal >> row0) & 0xFFFFull) == 0;
+    return ((bal >> row0) & ((1ull << G) - 1)) == 0;
 }
-constexpr int RCH = TMH_RCH;   // register chunks of 16 entries: sigma entries 0..127 (all but ~1e-5 of calls)
-#ifndef TMH_RCH_FIXED
-#define TMH_RCH_FIXED 4
-#endif
-constexpr int RCH_FIXED = TMH_RCH_FIXED;   // chunks always processed; chunk ch >= RCH_FIXED only when some row needs it
 
-// P1: segment walk.  Four chains per wavefront, one per row of 16 lanes; entry
-// k of a chain's sigma arrays lives in chunk k / 16, lane k % 16 of its row
-// (entries 128.. stay in the chain's global sigma row).  Each loop iteration
-// is one CloudCoverBinary.next_cloud call (cloud_cover_binary.py:80-107) of
-// every row that still has a call inside the window; the per-call scalar work
-// (clock fractions, update_parameters, the two divisions) is shared by four
-// chains, the argmin is a DPP row reduction with np.argmin's first-index rule,
-// the r_[cl, nsc[:last+1]] shift is row_shr:1 / row_ror:1.  Output per chain:
-// segment records (first uncovered step, next call step) and the window-end
-// binary state.
+// P1: segment walk.  64 / G chains per wavefront, one per group of G lanes
+// (G = 16 / 8 / 4, tmh_set_walk_lanes); entry k of a chain's sigma arrays lives
+// in register chunk k / G, lane k % G of its group (entries TMH_WALK_REG.. stay
+// in the chain's global sigma row).  Each loop iteration is one
+// CloudCoverBinary.next_cloud call (cloud_cover_binary.py:80-107) of every group
+// that still has a call inside the window; the per-call scalar work (clock
+// fractions, update_parameters, the two divisions) is shared by the G lanes of a
+// chain, the argmin is a DPP group reduction with np.argmin's first-index rule,
+// the r_[cl, nsc[:last+1]] shift is row_shr:1 plus row_shl:G-1 for the carry
+// between chunks.  Smaller G: fewer lanes (and issue slots) per chain-call,
+// more chunks per lane.  Output per chain: segment records (first uncovered
+// step, next call step) and the window-end binary state.
 #ifndef TMH_SEG_WAVES
 #define TMH_SEG_WAVES 1
 #endif
-#ifndef TMH_RETRY_BATCH   // retry candidates 16 at a time across the row (measured: walk +3 %, off)
+#ifndef TMH_RETRY_BATCH   // retry candidates G at a time across the group (measured: walk +3 %, off)
 #define TMH_RETRY_BATCH 0
 #endif
 #ifndef TMH_SEG_PRIO   // wave issue priority of the walk (s_setprio) over the expansion beside it
 #define TMH_SEG_PRIO 0
 #endif
-template <bool QUEUE>
+template <bool QUEUE, int G>
 __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
                                                           int64_t W0, uint32_t nsteps, tmh_clock ck,
                                                           const int2* __restrict__ events,
                                                           const uint32_t* __restrict__ n_events, SegView sg,
                                                           PrevView prev)
 {
+    static_assert(G == 4 || G == 8 || G == 16, "lanes per chain");
+    constexpr int NCH = TMH_WALK_REG / G;                          // register chunks
+    constexpr int NFIX = (TMH_WALK_FIX + G - 1) / G < NCH ? (TMH_WALK_FIX + G - 1) / G : NCH;
+    static_assert(NCH * G == TMH_WALK_REG, "TMH_WALK_REG: a multiple of 16");
+    constexpr int GSH = G == 4 ? 2 : G == 8 ? 3 : 4;
+    constexpr int CARRY = 0x100 | (G - 1);                        // row_shl:G-1: group lane 0 <- group lane G-1
+    extern __shared__ double walk_lds[];                           // [groups of the workgroup][WALK_CAND]
 #if TMH_SEG_PRIO
     __builtin_amdgcn_s_setprio(TMH_SEG_PRIO);
 #endif
-    const int lane = threadIdx.x & 63, p = lane & 15, row0 = lane & ~15;
+    const int lane = threadIdx.x & 63, p = lane & (G - 1), row0 = lane & ~(G - 1);
+    double* const cbuf = walk_lds + (threadIdx.x >> GSH) * WALK_CAND;
     const int64_t W1 = W0 + nsteps;
     const uint32_t nev = min(*n_events, ev_cap_dev(nsteps));
     const WinClock wck = win_clock(ck, W0);
-    // Rows take chains: row r starts with chain r, and a row whose chain is done
-    // takes the next unstarted one from the window's queue (chains rows.. n - 1), so
-    // with fewer rows than chains the walk's waves stay busy instead of idling
+    // Groups take chains: group r starts with chain r, and a group whose chain is done
+    // takes the next unstarted one from the window's queue (chains groups.. n - 1), so
+    // with fewer groups than chains the walk's waves stay busy instead of idling
     // behind the windiest chain of their wave (its duration is the longest chain's
     // call count either way; its footprint on the CUs shrinks).  Everything below
-    // is the row's current chain, row-uniform.
-    uint32_t c = (blockIdx.x * blockDim.x + threadIdx.x) >> 4;
+    // is the group's current chain, group-uniform.
+    uint32_t c = (blockIdx.x * blockDim.x + threadIdx.x) >> GSH;
     bool live = c < n;
     uint32_t status = 0xFFFFFFFFu;
     double ccb = 0.0, cca = 0.0, wsb = 0.0, wsa = 0.0;   // window-start cloud-cover and wind pairs
@@ -1176,17 +1198,19 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
     int L = 0;
     double* gsc = nullptr;
     double* gsl = nullptr;
-    double vc[RCH], vl[RCH];
+    double vc[NCH], vl[NCH];
     int64_t s_start = 0, e = 0;
-    // No global load or store sits on the per-call path: records, boundary
-    // events and candidates move through 16-entry lane-distributed buffers
-    // (lane p of a row = entry p), flushed / refilled once per 16 uses, and
-    // are read back with ds_bpermute.  (A per-call load behind a per-call
-    // store makes every call wait for the store's round trip: vmcnt counts both.)
+    // No global load or store sits on the per-call path: records and boundary
+    // events move through G-entry lane-distributed buffers (lane p of a group =
+    // entry p), flushed / refilled once per G uses and read back with
+    // ds_bpermute; the try-0 candidates through the group's LDS slots, refilled
+    // once per WALK_CAND calls from registers loaded one refill ahead.  (A per-call
+    // load behind a per-call store makes every call wait for the store's round
+    // trip: vmcnt counts both.)
     int2* rec = nullptr;
     int rb_x = 0, rb_y = 0;       // record buffer: lane p = record rbase + p
     uint32_t rbase = 0;
-    int32_t chunk = 0;            // the overflow chunk of records >= cap (row-uniform)
+    int32_t chunk = 0;            // the overflow chunk of records >= cap (group-uniform)
     auto group_at = [&](uint32_t b) {   // where the record group starting at b goes
         return b < sg.cap ? rec + b : sg.pool + (size_t)chunk * OVF_CHUNK + (b - sg.cap) % OVF_CHUNK;
     };
@@ -1195,9 +1219,9 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
         const bool mine = (uint32_t)p == slot;
         rb_x = mine ? x : rb_x;
         rb_y = mine ? y : rb_y;
-        if (slot == 15) {
+        if (slot == G - 1) {
             group_at(rbase)[p] = make_int2(rb_x, rb_y);
-            rbase += 16;
+            rbase += G;
         }
     };
     uint32_t ev = 0, evb = 0;
@@ -1218,7 +1242,7 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
     int ev_fl = 0;
     double ev_cc = 0.0, ev_ws = 0.0;
     auto fetch_event = [&]() {   // event `ev` out of the buffer
-        if (ev - evb >= 16) {
+        if (ev - evb >= G) {
             evb = ev;
             load_events();
         }
@@ -1231,10 +1255,17 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
     };
     uint32_t ncall0 = 0, ncall = 0;
     auto cand_at = [&](uint32_t k) { return k < sg.kcap ? sg.cand[(size_t)k * n + c] : -1.0; };
-    uint32_t kb = 0;                                     // candidate buffer: lane p = calls kb + p, kb + 16 + p
-    double cb_a = 0.0, cb_b = 0.0;
+    uint32_t kb = 0;                                     // cbuf holds the try-0 lengths of calls kb .. kb + WALK_CAND - 1
+    double cn[WALK_CAND / G];                            // lane p: calls kb + WALK_CAND + j G + p (the next refill)
+    auto cand_fill = [&]() {   // cn -> cbuf, then load the refill after it
+#pragma unroll
+        for (int j = 0; j < WALK_CAND / G; ++j) cbuf[j * G + p] = cn[j];
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int j = 0; j < WALK_CAND / G; ++j) cn[j] = cand_at(kb + 2 * WALK_CAND + j * G + p);
+    };
     bool active = false;
-    auto start_chain = [&]() {   // the row's chain c (< n) at the window start
+    auto start_chain = [&]() {   // the group's chain c (< n) at the window start
         const uint32_t cs = c;
         status = prev.status ? prev.status[cs] : st.status[cs];
         if (prev.status) {
@@ -1256,8 +1287,8 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
         gsc = sig_c(st, cs);
         gsl = sig_l(st, cs);
 #pragma unroll
-        for (int ch = 0; ch < RCH; ++ch) {
-            const int k = ch * 16 + p;
+        for (int ch = 0; ch < NCH; ++ch) {
+            const int k = ch * G + p;
             vc[ch] = k < L ? gsc[k] : 0.0;
             vl[ch] = k < L ? gsl[k] : 0.0;
         }
@@ -1273,12 +1304,14 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
         load_events();
         fetch_event();
         ncall0 = ncall = st.ncalls[cs];
+#pragma unroll
+        for (int j = 0; j < WALK_CAND / G; ++j) cn[j] = cand_at(j * G + p);
+        kb = -(uint32_t)WALK_CAND;   // cand_fill: cbuf <- calls 0.., cn <- calls WALK_CAND..
+        cand_fill();
         kb = 0;
-        cb_a = cand_at(p);
-        cb_b = cand_at(16 + p);
         active = status == 0;
     };
-    auto finish_chain = [&]() {   // the row's chain at the window end: records, state, walk outputs
+    auto finish_chain = [&]() {   // the group's chain at the window end: records, state, walk outputs
         if ((uint32_t)p < nrec - rbase) group_at(rbase)[p] = make_int2(rb_x, rb_y);   // partial record group
         if (status == 0) {
             while (next_ev <= W1 - 1) {   // remaining boundaries of the window
@@ -1294,8 +1327,8 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
                 fetch_event();
             }
 #pragma unroll
-            for (int ch = 0; ch < RCH; ++ch) {   // register chunks back to the state row
-                const int k = ch * 16 + p;
+            for (int ch = 0; ch < NCH; ++ch) {   // register chunks back to the state row
+                const int k = ch * G + p;
                 if (k < L) {
                     gsc[k] = vc[ch];
                     gsl[k] = vl[ch];
@@ -1319,7 +1352,7 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
             sg.end_p1[3 * (size_t)n + c] = wsa;
         }
     };
-    const uint32_t rows = gridDim.x * blockDim.x / 16;
+    const uint32_t groups = gridDim.x * blockDim.x / G;
     if (live) start_chain();
 #ifdef TMH_DIAG_P1   // diagnostic build only: cycles per section of the walk (s_memtime)
     uint64_t dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1335,19 +1368,21 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
 #endif
     for (;;) {
         if constexpr (QUEUE) {
-            while (live && !(active && e < W1)) {   // row-uniform: the row's chain is done, take the next one
+            while (live && !(active && e < W1)) {   // group-uniform: the group's chain is done, take the next one
                 finish_chain();
                 int v = 0;
                 if (p == 0) v = (int)atomicAdd(sg.walk_q, 1u);
-                c = rows + (uint32_t)__builtin_amdgcn_ds_bpermute(row0 << 2, v);   // the whole row is active here
+                c = groups + (uint32_t)__builtin_amdgcn_ds_bpermute(row0 << 2, v);   // the whole group is active here
                 live = c < n;
                 if (live) start_chain();
             }
         }
         const bool run = active && e < W1;
         if (__builtin_amdgcn_ballot_w64(run) == 0) break;
-        // wave-uniform chunk bound: the loops over register chunks branch on SGPRs only
-        const int Lmax = rows_max(run ? L : 0);
+        // wave-uniform bound on the sigma lengths: the gated chunk loops branch on SGPRs only.
+        // Every chunk an array of the wave reaches (and, for the shift, the one past it:
+        // (last + 1) / G <= L / G) is processed; a reset (L <= 11) stays in the NFIX chunks.
+        const int Lmax = wave_max_grp<G>(run ? L : 0);
 #ifdef TMH_DIAG_P1
         dg[7] += 1;
 #endif
@@ -1373,31 +1408,29 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
         const double ws = interp(wsb, wsa, df);
         const double f = 1.0 / h - 1.0;
         const uint32_t rel = ncall - ncall0;
-        if (rel - kb >= 32) {   // refill once per 32 calls (its latency is exposed once)
-            kb += 32;
-            cb_a = cand_at(kb + p);
-            cb_b = cand_at(kb + 16 + p);
+        if (rel - kb >= WALK_CAND) {   // refill once per WALK_CAND calls (loaded one refill ahead)
+            cand_fill();
+            kb += WALK_CAND;
         }
-        const uint32_t slot = rel - kb;
-        const double x0 = bperm_f64(row0 | (int)(slot & 15), slot < 16 ? cb_a : cb_b);
+        const double x0 = cbuf[rel - kb];
         DSTAMP(1)
         // ---- next_cloud: tries (cloud_cover_binary.py:82-98)
         int tries = 0, last = -1;
-        double ncl = 0.0;
+        double ncl = 0.0, bdl = 0.0;
 #if TMH_RETRY_BATCH
-        // Retry candidates, 16 at a time: lane p of the row draws try tb + p's cloud
+        // Retry candidates, G at a time: lane p of the group draws try tb + p's cloud
         // length (keyed by the call and the try, so any lane can) and divides it by
-        // the row's wind speed; a retry then costs one bpermute instead of a
-        // Philox block, a pow and a division on all 16 lanes.  ~2 % of the calls
+        // the chain's wind speed; a retry then costs one bpermute instead of a
+        // Philox block, a pow and a division on all G lanes.  ~2 % of the calls
         // reject 20 candidates in a row (reset_sigma), ~8 % at least one.
         double nb = 0.0;
-        int tb = -16;
+        int tb = -G;
 #endif
         for (;;) {
 #if TMH_RETRY_BATCH
             if (tries == 0 && x0 >= 0.0) ncl = x0 / ws;
             else {
-                if (tries - tb >= 16) {   // row-uniform
+                if (tries - tb >= G) {   // group-uniform
                     tb = tries;
                     const int t = tries + p;
                     nb = pow_d(dp.alpha + dp.delta * keyed_u(dp.seed, chain0 + gid(dp.ids, c), ncall, TAG_CLOUD, (uint32_t)(t >> 1), t & 1),
@@ -1419,34 +1452,37 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
                 const double nsc = ncl + sc;
                 const double nsl = f * nsc;
                 const double tot = nsc + nsl;
-                const bool ok = (k < L) & (nsl - sl > 0.0) & (tot < 5400.0);
+                const double dl = nsl - sl;   // the new clear length if k is picked (:103)
+                const bool ok = (k < L) & (dl > 0.0) & (tot < 5400.0);
                 const double d = ok ? fabs(tot - 3600.0) : INFINITY;
                 const bool take = d < bd;   // ascending k: ties keep the lower k
                 bd = take ? d : bd;
                 bk = take ? k : bk;
+                bdl = take ? dl : bdl;
             };
-            // chunks 0..3 straight-line (independent chains overlap: latency, not
-            // issue, bounds this loop); 4..7 only when some row has L > 64
 #pragma unroll
-            for (int ch = 0; ch < RCH_FIXED; ++ch) scan(ch * 16 + p, vc[ch], vl[ch]);
+            for (int ch = 0; ch < NFIX; ++ch) scan(ch * G + p, vc[ch], vl[ch]);
 #pragma unroll
-            for (int ch = RCH_FIXED; ch < RCH; ++ch)
-                if (Lmax > 16 * ch) scan(ch * 16 + p, vc[ch], vl[ch]);   // wave-uniform
-            for (int ch = RCH; ch * 16 < L; ++ch) {   // rare: entries 128..
-                const int k = ch * 16 + p;
+            for (int ch = NFIX; ch < NCH; ++ch)
+                if (Lmax > G * ch) scan(ch * G + p, vc[ch], vl[ch]);   // wave-uniform
+            for (int k0 = NCH * G; k0 < L; k0 += G) {   // rare: entries TMH_WALK_REG..
+                const int k = k0 + p;
                 if (k < L) scan(k, gsc[k], gsl[k]);
             }
-            const double dmin = row_min_f64(bd);
+            const double dmin = grp_min_f64<G>(bd);
             if (dmin < INFINITY) {
-                last = row_min_i32(bd == dmin ? bk : INT_MAX);
+                last = grp_min_i32<G>(bd == dmin ? bk : INT_MAX);
                 break;
             }
             ++tries;
             for (;;) {
                 if (tries == 20) {   // reset_sigma (cloud_cover_binary.py:76-78); 300 (k+1) is exact
                     const int nl = (int)(h * 12);
-                    vc[0] = 300.0 * (p + 1);
-                    vl[0] = f * vc[0];
+#pragma unroll
+                    for (int ch = 0; ch * G < 12; ++ch) {
+                        vc[ch] = 300.0 * (ch * G + p + 1);
+                        vl[ch] = f * vc[ch];
+                    }
                     L = nl;
                 }
 #if TMH_DOOM_SKIP
@@ -1454,7 +1490,7 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
                 // the candidates can take makes any entry possible, every try up to the
                 // reset (or the assert) is rejected -- skip them.  Tries are keyed by
                 // (call, try), so skipping changes no later draw.
-                if ((tries == 1 || tries == 20) && row_doomed(vc, vl, L, p, row0, f, ws, dp)) {
+                if ((tries == 1 || tries == 20) && grp_doomed<G>(vc, vl, L, p, row0, f, ws, dp)) {
                     tries = tries == 1 ? 20 : 40;
                     continue;
                 }
@@ -1478,63 +1514,29 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
             continue;
         }
         DSTAMP(3)
-        // sigma_cloud = r_[cl, nsc[:last+1]], sigma_clear = r_[clr, nsl[:last+1]] (:101-105)
-        const int lc = last >> 4, src = row0 | (last & 15);
-        const int top = (last + 1) >> 4;   // highest chunk written
-        const int topmax = rows_max(top);
-        double sc_last = 0.0, sl_last = 0.0;
-        {   // select chunk lc in registers first (one bpermute pair instead of one per chunk)
-            double a = vc[0], b = vl[0];
-#pragma unroll
-            for (int ch = 1; ch < RCH_FIXED; ++ch) {
-                a = lc == ch ? vc[ch] : a;
-                b = lc == ch ? vl[ch] : b;
-            }
-#pragma unroll
-            for (int ch = RCH_FIXED; ch < RCH; ++ch) {
-                if (topmax >= ch) {   // wave-uniform
-                    a = lc == ch ? vc[ch] : a;
-                    b = lc == ch ? vl[ch] : b;
-                }
-            }
-            sc_last = bperm_f64(src, a);
-            sl_last = bperm_f64(src, b);
-        }
-        if (lc >= RCH) {
-            sc_last = gsc[last];
-            sl_last = gsl[last];
-        }
-        const double nclr = f * (ncl + sc_last) - sl_last;
-        // entry 16 RCH - 1 (register chunk RCH - 1, lane 15) for lane 0 of the first global chunk:
-        // the DPP runs with the whole row active (under a p == 0 branch lane 15 would be
-        // masked off and the read would return the DPP's old value)
-        const double carry_g = dpp_row_f64<0x121>(0.0, vc[RCH - 1]);
-        for (int ch = top; ch >= RCH; --ch) {   // rare, descending: reads before writes
-            const int k = ch * 16 + p;
-            const double prev = (ch == RCH && p == 0) ? carry_g : gsc[k - 1];
-            const double nsc = ncl + prev;
+        // sigma_cloud = r_[cl, nsc[:last+1]], sigma_clear = r_[clr, nsl[:last+1]] (:101-105);
+        // clr = nsl[last] - sigma_clear[last] is the scan's dl of entry `last`, held by
+        // the lane that owns it (its best is `last`)
+        const double nclr = bperm_f64(row0 | (last & (G - 1)), bdl);
+        const int top = (last + 1) / G;   // highest chunk written
+        // entry G NCH - 1 (register chunk NCH - 1, group lane G - 1) for lane 0 of the first
+        // global chunk: the DPP runs with the whole group active
+        const double carry_g = dpp_row_f64<CARRY>(0.0, vc[NCH - 1]);
+        for (int ch = top; ch >= NCH; --ch) {   // rare, descending: reads before writes
+            const int k = ch * G + p;
+            const double prv = (ch == NCH && p == 0) ? carry_g : gsc[k - 1];
+            const double nsc = ncl + prv;
             gsc[k] = nsc;
             gsl[k] = f * nsc;
         }
-        // rows with a lower top rewrite entries >= their new L: harmless
+        // chunks a longer array of the wave needs are rewritten for every group: entries >= the new L, harmless
 #pragma unroll
-        for (int ch = RCH - 1; ch >= RCH_FIXED; --ch) {
-            if (topmax >= ch) {   // wave-uniform
-                const double sh = dpp_row_f64<0x111>(0.0, vc[ch]);
-                const double carry = dpp_row_f64<0x121>(0.0, vc[ch - 1]);
-                const double prev = p == 0 ? carry : sh;
-                const double nsc = ncl + prev;
-                vc[ch] = nsc;
-                vl[ch] = f * nsc;
-            }
-        }
-#pragma unroll
-        for (int ch = RCH_FIXED - 1; ch >= 0; --ch) {
-            {
-                const double sh = dpp_row_f64<0x111>(0.0, vc[ch]);                       // row_shr:1
-                const double carry = ch > 0 ? dpp_row_f64<0x121>(0.0, vc[ch > 0 ? ch - 1 : 0]) : 0.0;   // row_ror:1
-                const double prev = p == 0 ? carry : sh;
-                const double nsc = ncl + prev;
+        for (int ch = NCH - 1; ch >= 0; --ch) {
+            if (ch < NFIX || Lmax >= G * ch) {   // wave-uniform
+                const double sh = dpp_row_f64<0x111>(0.0, vc[ch]);                               // row_shr:1
+                const double carry = ch > 0 ? dpp_row_f64<CARRY>(0.0, vc[ch > 0 ? ch - 1 : 0]) : 0.0;   // row_shl:G-1
+                const double prv = p == 0 ? carry : sh;
+                const double nsc = ncl + prv;
                 const bool first = ch == 0 && p == 0;
                 vc[ch] = first ? ncl : nsc;
                 vl[ch] = first ? nclr : f * nsc;
@@ -1552,7 +1554,7 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
             if (k < OVF_SLOTS) {
                 int v = 0;
                 if (p == 0) v = (int)atomicAdd(sg.pool_n, 1u);
-                got = __builtin_amdgcn_ds_bpermute(row0 << 2, v);   // the whole row is active here
+                got = __builtin_amdgcn_ds_bpermute(row0 << 2, v);   // the whole group is active here
                 if ((uint32_t)got >= sg.pool_cap) got = -1;
                 else if (p == 0) sg.ovf[(size_t)c * OVF_SLOTS + k] = got;
             }
@@ -1568,7 +1570,7 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
         ++nrec;
         DSTAMP(5)
     }
-    if constexpr (!QUEUE)   // one chain per row
+    if constexpr (!QUEUE)   // one chain per group
         if (live) finish_chain();
 #ifdef TMH_DIAG_P1
     if (lane == 0) {
@@ -1605,6 +1607,20 @@ __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t rs, uint32_t of
 #ifndef TMH_EXP_CHAIN_FAST
 #define TMH_EXP_CHAIN_FAST 0
 #endif
+#ifndef TMH_EXP_PRIO
+#define TMH_EXP_PRIO 0
+#endif
+#ifndef TMH_EXP_WG_TRACE   // threads per workgroup of the fp32 single-site trace expansion (C2)
+#define TMH_EXP_WG_TRACE 256
+#endif
+// Workgroup size of an expansion instantiation: one wave per workgroup lets the CUs'
+// SIMDs take expansion waves independently beside a walk wave that holds registers
+// on one of them (a 4-wave workgroup needs a slot on all four).
+template <typename R, int OUT, bool SITES>
+constexpr int exp_wg()
+{
+    return (OUT == OUT_TRACE3 && sizeof(R) == 4 && !SITES) ? TMH_EXP_WG_TRACE : 256;
+}
 #ifndef TMH_ROW_PREFETCH   // fp32 single-site expansion: next second's geometry row loaded early
 #define TMH_ROW_PREFETCH 0
 #endif
@@ -1635,8 +1651,11 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
                                                      StatsView sv)
 {
     extern __shared__ uint32_t lds_hist[];
+#if TMH_EXP_PRIO   // wave issue priority of the expansion over the walks beside it (s_setprio)
+    __builtin_amdgcn_s_setprio(TMH_EXP_PRIO);
+#endif
 #if TMH_EXP_CHAIN_FAST   // 1-D grid, chain block fastest: the workgroups writing one trace row run together
-    const uint32_t ncb = (n + 255) / 256;
+    const uint32_t ncb = (n + blockDim.x - 1) / blockDim.x;
     const uint32_t b = blockIdx.x / ncb;
     const uint32_t c = (blockIdx.x - b * ncb) * blockDim.x + threadIdx.x;
 #else
@@ -1693,8 +1712,9 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
     // waits behind the trace stores (gfx9's vmcnt counts loads and stores alike;
     // per-second record loads cost 42 % of the waves' cycles in such waits, PMC
     // SQ_WAIT_ANY).  Word-major: lane-consecutive dwords, no bank conflicts.
-    __shared__ uint32_t cov_lds[4][256];
-    __shared__ R min_lds[4][256];   // minute boundaries mA, mA + 1 of the block: cloudy, clear noise
+    constexpr int WGT = exp_wg<R, OUT, SITES>();   // threads per workgroup
+    __shared__ uint32_t cov_lds[4][WGT];
+    __shared__ R min_lds[4][WGT];   // minute boundaries mA, mA + 1 of the block: cloudy, clear noise
     const int32_t s0i = (int32_t)(W0 + j0), s1i = (int32_t)(W0 + j1);
     const int32_t mA = (int32_t)j0 <= (int32_t)fm ? 0 : ((int32_t)j0 - (int32_t)fm + 59) / 60;
     {
@@ -1739,7 +1759,7 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
     uint32_t cov_w = 0;
     const double* evd = sg.evd + c;
 #if TMH_HELD_LDS   // the guard-band seconds of the lane's block, a bit each, in LDS: no register carried through the loop
-    __shared__ uint4 held_lds[256];
+    __shared__ uint4 held_lds[WGT];
     held_lds[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
 #else
     bool held_any = false;   // fp32: some second of this block lies in a guard band (pv_power_f)
@@ -2320,6 +2340,7 @@ struct tmh_engine {
     uint32_t n_tab = 0;     // rows of the per-chain shape tables (0: none)
     uint32_t n_sites = 0;   // rows of the per-chain sites (0: the engine's one site)
     uint32_t walk_cpr = 1;  // chains per walk row (tmh_set_walk_chains_per_row)
+    uint32_t walk_lanes = TMH_WALK_LANES_DEFAULT;  // lanes per chain in the walk (tmh_set_walk_lanes)
     // kernel timing (tmh_profile_*): event pairs per kernel, read and recycled
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[TMH_K_COUNT];
@@ -2576,6 +2597,15 @@ int tmh_set_walk_chains_per_row(struct tmh_engine* eng, uint32_t chains_per_row)
     return TMH_OK;
 }
 
+int tmh_set_walk_lanes(struct tmh_engine* eng, uint32_t lanes)
+{
+    if (!eng) return fail(TMH_E_INVAL, "NULL engine");
+    if (lanes == 0) lanes = TMH_WALK_LANES_DEFAULT;
+    if (lanes != 4 && lanes != 8 && lanes != 16) return fail(TMH_E_INVAL, "walk lanes %u: 4, 8 or 16", lanes);
+    eng->walk_lanes = lanes;
+    return TMH_OK;
+}
+
 int tmh_set_chain_ids(struct tmh_engine* eng, const uint32_t* ids, uint32_t n_full)
 {
     if (!eng) return fail(TMH_E_INVAL, "NULL engine");
@@ -2764,13 +2794,19 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     }
     if (phases & PH_SEGMENTS) {
     hipEvent_t t_seg = eng->mark(s);
-    const uint32_t rows = (uint32_t)(((uint64_t)n_chains + eng->walk_cpr - 1) / eng->walk_cpr);   // 16 per workgroup
-    if (rows < n_chains)   // rows take queued chains
-        hipLaunchKernelGGL(segments_kernel<true>, dim3((rows + 15) / 16), dim3(256), 0, s, eng->dp, v, chain0, n_chains,
-                           step0, n_steps, eng->gp.clock, pv.events, pv.n_events, sg, prev);
-    else
-        hipLaunchKernelGGL(segments_kernel<false>, dim3((rows + 15) / 16), dim3(256), 0, s, eng->dp, v, chain0,
-                           n_chains, step0, n_steps, eng->gp.clock, pv.events, pv.n_events, sg, prev);
+    // groups of walk_lanes lanes, 16 per workgroup (16 G threads, 16 x WALK_CAND candidate slots in LDS)
+    const uint32_t rows = (uint32_t)(((uint64_t)n_chains + eng->walk_cpr - 1) / eng->walk_cpr);
+    const uint32_t G = eng->walk_lanes;
+    const dim3 wg((rows + 15) / 16), wt(16 * G);
+    const size_t wlds = 16 * WALK_CAND * sizeof(double);
+#define WALK(Q, GG)                                                                                           \
+    hipLaunchKernelGGL((segments_kernel<Q, GG>), wg, wt, wlds, s, eng->dp, v, chain0, n_chains, step0, n_steps, \
+                       eng->gp.clock, pv.events, pv.n_events, sg, prev)
+    const bool q = rows < n_chains;   // groups take queued chains
+    if (G == 4) { if (q) WALK(true, 4); else WALK(false, 4); }
+    else if (G == 8) { if (q) WALK(true, 8); else WALK(false, 8); }
+    else { if (q) WALK(true, 16); else WALK(false, 16); }
+#undef WALK
     eng->close(TMH_K_SEGMENTS, t_seg, s);
     if (int rc = hip_check(hipGetLastError(), "segments kernel launch")) return rc;
     }
@@ -2798,17 +2834,20 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     const int out = (no_stats && tv.pv && tv.meter && tv.residual && !tv.csi && !tv.covered) ? OUT_TRACE3
                     : (!tv.pv && !tv.meter && !tv.residual && !tv.csi && !tv.covered) ? OUT_STATS
                                                                                       : OUT_ANY;
+    auto exp_grid = [&](uint32_t wg) {
+        const uint32_t ecb = (n_chains + wg - 1) / wg;
 #if TMH_EXP_CHAIN_FAST
-    dim3 grid2(sg.nblk * cb);
+        return dim3(sg.nblk * ecb);
 #else
-    dim3 grid2(sg.nblk, cb);
+        return dim3(sg.nblk, ecb);
 #endif
+    };
     if (out == OUT_TRACE3 && tv.ld * (f64 ? 8u : 4u) * BLOCK_STEPS >= (1ull << 31))   // one block's rows: one buffer range
         return fail(TMH_E_INVAL, "trace ld %llu too large (a 128-step block of rows must stay under 2 GiB)",
                     (unsigned long long)tv.ld);
     const size_t lds_exp = stats && stats->hist ? (size_t)((stats->n_bins + 1) / 2) * 4 : 0;   // 16-bit bin pairs
 #define LAUNCH(R, O, S)                                                                                            \
-    hipLaunchKernelGGL((expand_kernel<R, O, S>), grid2, dim3(256), lds_exp + TMH_DIAG_EXP_LDS, s, eng->kp, eng->dp, v, chain0, n_chains,      \
+    hipLaunchKernelGGL((expand_kernel<R, O, S>), exp_grid(exp_wg<R, O, S>()), dim3(exp_wg<R, O, S>()), lds_exp + TMH_DIAG_EXP_LDS, s, eng->kp, eng->dp, v, chain0, n_chains,      \
                        step0, n_steps, utc0, pv.tab64, pv.tab32, pv.sun, pv.events, pv.n_events, pv.desc, sg, tv, sv)
     if (eng->kp.sites) {   // per-chain sites: one instantiation per precision, any output
         if (f64) LAUNCH(double, OUT_ANY, true);
