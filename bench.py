@@ -79,14 +79,14 @@ def parse():
     ap.add_argument("--schedule", default="gated", choices=["gated", "stagger"],
                     help="pipelined one-window batches: 'gated' releases the expansion of batch k, the walk of "
                          "k + 1 and the construction of k + 2 together when walk k ends; 'stagger' is round 1's")
-    ap.add_argument("--walks", type=int, default=1,
+    ap.add_argument("--walks", type=int, default=None,
                     help="gated schedule: segment walks in flight on their own streams (each batch's walk "
                          "overlaps the next one's; use with --walk-cpr > 1 so they share the CUs' walk slots)")
     ap.add_argument("--walk-cpr", type=int, default=1,
                     help="chains per walk row (tmh_set_walk_chains_per_row): the walk launches n / cpr rows "
                          "that take the next chain when theirs is done")
     ap.add_argument("--walk-lanes", type=int, default=0,
-                    help="lanes per chain in the segment walk (tmh_set_walk_lanes: 4, 8 or 16; 0 = the build's default)")
+                    help="lanes per chain in the segment walk (tmh_set_walk_lanes: 4, 8 or 16; 0 = by batch size: 16 up to 8,192 chains, else 4)")
     ap.add_argument("--build-ahead", type=int, default=None,
                     help="gated schedule: when the walk of batch k ends, the construction of batch k + A is "
                          "released (default A = walks + 1; needs --pipeline >= A + 1)")
@@ -110,6 +110,11 @@ def parse():
     a.seconds = a.seconds or {"c2": 86400, "c3": 86400, "c4": 365 * 86400, "c5": 604800}[a.workload]
     if a.compact is None:
         a.compact = int(c5)
+    # C2: two walks in flight (r02, same-box A/B: 1.71-1.72 ms per batch against 1.81 with one)
+    a.walks = a.walks if a.walks is not None else (2 if a.workload == "c2" else 1)
+    # C5's compacted windows walk and expand in turn (latency-bound walk): 16 lanes per
+    # chain (1.76e10 against 1.73e10 with the batch-size default, r02 same box)
+    a.walk_lanes = a.walk_lanes or (16 if c5 else 0)
     a.build_ahead = a.build_ahead or max(1, a.walks) + 1
     # c3: two 1 M-chain batches in flight (2 x 83 GB of state + scratch): +3 % over one (r02)
     a.pipeline = a.pipeline or (2 if a.workload == "c3" else a.build_ahead + 1)
@@ -610,7 +615,7 @@ def main():
                    "batches_in_flight": len(ctxs), "staggered": bool(args.stagger and nwin == 1),
                    "construction_on": args.build_on, "walk_priority": args.walk_priority,
                    "schedule": args.schedule if (args.stagger and nwin == 1 and len(ctxs) >= 3) else None,
-                   "walks_in_flight": W, "walk_chains_per_row": args.walk_cpr, "walk_lanes": args.walk_lanes or None, "build_ahead": A,
+                   "walks_in_flight": W, "walk_chains_per_row": args.walk_cpr, "walk_lanes": args.walk_lanes or "auto", "build_ahead": A,
                    "minutes_ahead": bool(args.minutes_ahead), "commit_stream": bool(args.commit_stream),
                    "compacted_windows": bool(args.compact and args.mode == "stats" and nwin > 1)},
         "roofline": roof,

@@ -161,9 +161,10 @@ size_t tmh_workspace_bytes(uint32_t n_chains, uint32_t n_steps);
  * (default); at most 64. */
 int tmh_set_walk_chains_per_row(struct tmh_engine* eng, uint32_t chains_per_row);
 /* Lanes per chain in the segment walk: 16 (four chains per wavefront), 8 or 4
- * (sixteen chains per wavefront, four times the sigma entries per lane); 0 = the
- * build's default.  Fewer lanes per chain: fewer issue slots and waves per
- * chain-call, more work per lane.  Results do not depend on it. */
+ * (sixteen chains per wavefront, four times the sigma entries per lane); 0 = by
+ * batch size (the default: 16 up to 8,192 chains, where the walk is latency-bound,
+ * else 4).  Fewer lanes per chain: fewer instructions and registers per chain-call,
+ * a longer chain of work per call.  Results do not depend on it. */
 int tmh_set_walk_lanes(struct tmh_engine* eng, uint32_t lanes);
 /* Compaction (batches whose chains fault, e.g. the reference's markov-mode
  * AssertionError, cloud_cover_binary.py:91): run later windows on the live chains

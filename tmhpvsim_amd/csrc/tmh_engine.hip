@@ -1095,9 +1095,15 @@ __device__ __forceinline__ double bperm_f64(int src_lane, double v)
     return __hiloint2double(hi, lo);
 }
 
-#ifndef TMH_WALK_LANES_DEFAULT   // lanes per chain of the walk unless tmh_set_walk_lanes says otherwise
-#define TMH_WALK_LANES_DEFAULT 16
+#ifndef TMH_WALK_LANES_DEFAULT   // lanes per chain of the walk unless tmh_set_walk_lanes says otherwise (0: by batch size)
+#define TMH_WALK_LANES_DEFAULT 0
 #endif
+// Batch size up to which the automatic choice walks with 16 lanes per chain: up to 2
+// waves per SIMD the walk is latency-bound (C2: 4,096 chains, 1,024 waves) and the
+// short per-call chain of 16 lanes wins; past it the walk is throughput-bound and 4
+// lanes per chain (37 % fewer instructions, 14 instead of 36 VGPRs per chain) win
+// (r02, same box: C3 2.48 -> 2.69e11, C4 2.24 -> 2.36e11 chain-s/s).
+constexpr uint32_t WALK_AUTO_SMALL = 8192;
 #ifndef TMH_WALK_REG   // sigma entries held in VGPRs per chain (entries past them: the chain's global row)
 #define TMH_WALK_REG 64
 #endif
@@ -2601,7 +2607,7 @@ int tmh_set_walk_lanes(struct tmh_engine* eng, uint32_t lanes)
 {
     if (!eng) return fail(TMH_E_INVAL, "NULL engine");
     if (lanes == 0) lanes = TMH_WALK_LANES_DEFAULT;
-    if (lanes != 4 && lanes != 8 && lanes != 16) return fail(TMH_E_INVAL, "walk lanes %u: 4, 8 or 16", lanes);
+    if (lanes != 0 && lanes != 4 && lanes != 8 && lanes != 16) return fail(TMH_E_INVAL, "walk lanes %u: 4, 8 or 16", lanes);
     eng->walk_lanes = lanes;
     return TMH_OK;
 }
@@ -2796,7 +2802,7 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     hipEvent_t t_seg = eng->mark(s);
     // groups of walk_lanes lanes, 16 per workgroup (16 G threads, 16 x WALK_CAND candidate slots in LDS)
     const uint32_t rows = (uint32_t)(((uint64_t)n_chains + eng->walk_cpr - 1) / eng->walk_cpr);
-    const uint32_t G = eng->walk_lanes;
+    const uint32_t G = eng->walk_lanes ? eng->walk_lanes : (n_chains > WALK_AUTO_SMALL ? 4u : 16u);
     const dim3 wg((rows + 15) / 16), wt(16 * G);
     const size_t wlds = 16 * WALK_CAND * sizeof(double);
 #define WALK(Q, GG)                                                                                           \
