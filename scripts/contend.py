@@ -21,6 +21,7 @@ from tmhpvsim_amd.params import ModelParams  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--walk-lanes", type=int, default=0)
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--occupy", action="store_true", help="also beside scripts/micro/libocc*.so (resident dummy waves)")
 args = ap.parse_args()
 L = _lib.load()
 dev = "cuda:0"
@@ -88,6 +89,13 @@ variants = {
     "walk+build": lambda sp: (walk(b, sp), build(Ctx.spare, p3)),
 }
 Ctx.spare = Ctx(2)
+if args.occupy:   # dummy waves, one per SIMD, ~1.5 ms: sleeping with 138 / 70 VGPRs, or fp64 FMA chains
+    occ_out = torch.zeros(256, dtype=torch.float64, device=dev)
+    for tag, so in (("138", "libocc.so"), ("70", "libocc72.so")):
+        lib = C.CDLL(os.path.join(ROOT, "scripts", "micro", so))
+        lib.launch_occupy.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        variants[f"sleep{tag}"] = (lambda l: lambda sp: l.launch_occupy(0, 250, 256, sp, P(occ_out)))(lib)
+        variants[f"fma{tag}"] = (lambda l: lambda sp: l.launch_occupy(1, 20000, 256, sp, P(occ_out)))(lib)
 res = {}
 for name, other in variants.items():
     ts, to = [], []
