@@ -1,10 +1,11 @@
 #!/bin/bash
+# Walk-alone and C2 bench A/B of library builds: walk_ab.sh TAG variant... ("cur" = libtmhpvsim.so)
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-PYTEST_K="${PYTEST_K:-}" bash scripts/gpu_tests.sh ${1:-wab} || exit $?
-timeout -k 10 200 python scripts/diag_p1.py > gpurun_out/diag_p1_batch.txt 2>&1 || exit $?
-cat gpurun_out/diag_p1_batch.txt
-shift || true
-bash scripts/varab.sh wab "$@"
+TAG=$1; shift
+for v in "$@"; do
+  lib=$PWD/tmhpvsim_amd/libtmh_$v.so; [ "$v" = cur ] && lib=$PWD/tmhpvsim_amd/libtmhpvsim.so
+  echo "== $v"; TMHPVSIM_LIB=$lib timeout -k 10 100 python scripts/walk_only.py --reps 5 ${WARGS:-} || exit $?
+done
+bash scripts/libab.sh $TAG "$@"

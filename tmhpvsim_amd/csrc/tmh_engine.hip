@@ -1053,25 +1053,35 @@ __device__ __forceinline__ double dpp_row_f64(double old, double v)
     return __hiloint2double(hi, lo);
 }
 
+// the same without an `old` operand: lanes whose source lies outside the row read
+// 0 (bound_ctrl), so no register is initialised for them first
+template <int CTRL>
+__device__ __forceinline__ double mov_dpp_f64(double v)
+{
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
+    return __hiloint2double(hi, lo);
+}
+
 // min over the G lanes of each group: quad_perm [1,0,3,2], [2,3,0,1], then
 // row_half_mirror (G >= 8: the other quad of the half row), row_mirror (G = 16)
 template <int G>
 __device__ __forceinline__ double grp_min_f64(double v)
 {
-    v = fmin(v, dpp_row_f64<0xB1>(v, v));
-    v = fmin(v, dpp_row_f64<0x4E>(v, v));
-    if constexpr (G >= 8) v = fmin(v, dpp_row_f64<0x141>(v, v));
-    if constexpr (G >= 16) v = fmin(v, dpp_row_f64<0x140>(v, v));
+    v = fmin(v, mov_dpp_f64<0xB1>(v));
+    v = fmin(v, mov_dpp_f64<0x4E>(v));
+    if constexpr (G >= 8) v = fmin(v, mov_dpp_f64<0x141>(v));
+    if constexpr (G >= 16) v = fmin(v, mov_dpp_f64<0x140>(v));
     return v;
 }
 
 template <int G>
 __device__ __forceinline__ int grp_min_i32(int v)
 {
-    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false));
-    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false));
-    if constexpr (G >= 8) v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false));
-    if constexpr (G >= 16) v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false));
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true));
+    v = min(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true));
+    if constexpr (G >= 8) v = min(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, true));
+    if constexpr (G >= 16) v = min(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, true));
     return v;
 }
 
@@ -1081,8 +1091,8 @@ __device__ __forceinline__ int grp_min_i32(int v)
 template <int G>
 __device__ __forceinline__ int wave_max_grp(int v)
 {
-    if constexpr (G <= 4) v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false));
-    if constexpr (G <= 8) v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false));
+    if constexpr (G <= 4) v = max(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, true));
+    if constexpr (G <= 8) v = max(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, true));
     const int a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
     const int c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
     return max(max(a, b), max(c, d));
@@ -1460,8 +1470,8 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
                 const double tot = nsc + nsl;
                 const double dl = nsl - sl;   // the new clear length if k is picked (:103)
                 const bool ok = (k < L) & (dl > 0.0) & (tot < 5400.0);
-                const double d = ok ? fabs(tot - 3600.0) : INFINITY;
-                const bool take = d < bd;   // ascending k: ties keep the lower k
+                const double d = fabs(tot - 3600.0);
+                const bool take = ok & (d < bd);   // ascending k: ties keep the lower k (bd starts at +inf)
                 bd = take ? d : bd;
                 bk = take ? k : bk;
                 bdl = take ? dl : bdl;
@@ -1527,7 +1537,7 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
         const int top = (last + 1) / G;   // highest chunk written
         // entry G NCH - 1 (register chunk NCH - 1, group lane G - 1) for lane 0 of the first
         // global chunk: the DPP runs with the whole group active
-        const double carry_g = dpp_row_f64<CARRY>(0.0, vc[NCH - 1]);
+        const double carry_g = mov_dpp_f64<CARRY>(vc[NCH - 1]);
         for (int ch = top; ch >= NCH; --ch) {   // rare, descending: reads before writes
             const int k = ch * G + p;
             const double prv = (ch == NCH && p == 0) ? carry_g : gsc[k - 1];
@@ -1539,8 +1549,8 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
 #pragma unroll
         for (int ch = NCH - 1; ch >= 0; --ch) {
             if (ch < NFIX || Lmax >= G * ch) {   // wave-uniform
-                const double sh = dpp_row_f64<0x111>(0.0, vc[ch]);                               // row_shr:1
-                const double carry = ch > 0 ? dpp_row_f64<CARRY>(0.0, vc[ch > 0 ? ch - 1 : 0]) : 0.0;   // row_shl:G-1
+                const double sh = mov_dpp_f64<0x111>(vc[ch]);                               // row_shr:1
+                const double carry = ch > 0 ? mov_dpp_f64<CARRY>(vc[ch > 0 ? ch - 1 : 0]) : 0.0;   // row_shl:G-1
                 const double prv = p == 0 ? carry : sh;
                 const double nsc = ncl + prv;
                 const bool first = ch == 0 && p == 0;
