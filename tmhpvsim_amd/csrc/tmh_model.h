@@ -817,9 +817,13 @@ __device__ void sun_at(int64_t utc, int doy, int leap, const double* linke, doub
     o[SUN_RDNIX] = 1.0 / o[SUN_DNIX];       // the fp32 row's reciprocal, once per step
 }
 
+// x^y for x > 0 as exp2(y log2 x): within a few ulps of pow (|y log2 x| < 16 here),
+// about half of ocml's pow (its extra-precise log and special cases)
+__device__ __forceinline__ double pow_pos(double x, double y) { return exp2(y * log2(x)); }
+
 // per-site constants of the geometry (site row: lat, lon, altitude, tilt, azimuth, albedo)
 struct SiteK {
-    double lon, slat, clat, pres, refr, alt, fh1, fh2, cg1, cg2, ctilt, stilt, saz, term2, gfac;
+    double lon, slat, clat, pres, refr, alt, fh1, fh2, cg1, cg2, ctilt, stilt, saz, term2, gfac, csaz, ssaz;
 };
 
 __device__ __forceinline__ SiteK site_k(const double* site)
@@ -842,13 +846,14 @@ __device__ __forceinline__ SiteK site_k(const double* site)
     k.stilt = sind(tilt);
     k.term2 = 0.5 * (1.0 + cosd(tilt));
     k.gfac = albedo * (1.0 - cos(rad(tilt))) * 0.5;
+    sincos(rad(k.saz), &k.ssaz, &k.csaz);
     return k;
 }
 
 // geometry row fields G_COSZ..G_F2 of one site and step (fp64); returns true
 // when the clear-sky GHI is 0 (pv = 0 whatever the csi).  FULL = false stops
 // there at night (the per-chain-second path); FULL fills every field.
-template <bool FULL>
+template <bool FULL, bool F32 = false>
 __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, double tl, const double* m, double* g)
 {
     // fmod(x, 1440) for x in (-1440, 2880): one exact subtraction (Sterbenz) or none
@@ -865,15 +870,36 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     double de = 0.0;
     if (e0 >= -1.0 * (0.26667 + 0.5667)) de = k.refr / (60.0 * tan(rad(e0 + 10.3 / (e0 + 5.11))));
     const double azen = 90.0 - (e0 + de);
+    // cos / sin of the apparent zenith zen - de from the true zenith's (czr, sqrt(1 - czr^2))
+    // and the refraction angle's: |de| < 0.6 deg (0 below the horizon band), so its sine and
+    // cosine are short Taylor series (truncation < 1e-18): two fp64 sincos calls fewer
+    // than sincos(rad(azen)), the same to a few ulps
     double szs, czs;
-    sincos(rad(azen), &szs, &czs);
+    {
+        const double sz = sqrt(fmax(1.0 - czr * czr, 0.0));
+        const double d = rad(de), d2 = d * d;
+        const double sd = d * (1.0 - d2 * (1.0 / 6.0) * (1.0 - d2 * (1.0 / 20.0) * (1.0 - d2 * (1.0 / 42.0))));
+        const double cd = 1.0 - d2 * 0.5 * (1.0 - d2 * (1.0 / 12.0) * (1.0 - d2 * (1.0 / 30.0) * (1.0 - d2 * (1.0 / 56.0))));
+        czs = czr * cd + sz * sd;
+        szs = sz * cd - czr * sd;
+    }
     if (!FULL && !(czs > 0.0)) return true;   // ghi_cs = cg1 * .. * max(cos(apparent zenith), 0) = 0
-    const double az = deg(atan2(sha, cha * k.slat - sun[SUN_TAND] * k.clat)) + 180.0;
+    // azimuth az = atan2(Y, X) + 180 deg (NOAA, the oracle's solpos): only cos(az - saz) is
+    // used (Hay-Davies / AOI projection), = -(X cos saz + Y sin saz) / hypot(X, Y)
+    const double azY = sha, azX = cha * k.slat - sun[SUN_TAND] * k.clat;
+    const double azr = sqrt(azX * azX + azY * azY);
+    const double caz = azr > 0.0 ? -(azX * k.csaz + azY * k.ssaz) / azr : -k.csaz;   // atan2(0, 0) = 0: az = 180
     const double ct = czr;   // cos(rad(deg(acos(czr)))): the same to ~3e-16 absolute
     g[G_COSZ] = ct;
-    g[G_CSIMAX] = 27.21 * exp(-114 * ct) + 1.665 * exp(-4.494 * ct) + 1.08;   // pvmodel.py:52-58
+    // pvmodel.py:52-58; F32 (a per-chain site's fp32 row): in fp32, 1e-7 relative -- the bound
+    // only clips csi, and a clipped second's fp32 PV carries that relative error, far inside 1e-5
+    if constexpr (F32) {
+        const float cf = (float)ct;
+        g[G_CSIMAX] = fmaf(27.21f, __expf(-114.0f * cf), fmaf(1.665f, __expf(-4.494f * cf), 1.08f));
+    } else
+        g[G_CSIMAX] = 27.21 * exp(-114 * ct) + 1.665 * exp(-4.494 * ct) + 1.08;
     const double dni_extra = sun[SUN_DNIX];
-    const double am_rel = azen <= 90.0 ? 1.0 / (czs + 0.50572 * pow(6.07995 + (90.0 - azen), -1.6364)) : NAN;
+    const double am_rel = azen <= 90.0 ? 1.0 / (czs + 0.50572 * pow_pos(6.07995 + (90.0 - azen), -1.6364)) : NAN;
     const double am_abs = am_rel * k.pres / 101325.0;
     const double cz = czs > 0.0 ? czs : 0.0;
     const double gexp = exp(-k.cg2 * am_abs * (k.fh1 + k.fh2 * (tl - 1.0)));
@@ -882,14 +908,14 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     const double I0 = sun[SUN_I0];
     g[G_I0] = I0;                                                              // disc (pvmodel.py:63)
     g[G_I0H] = I0 * (ct > 0.065 ? ct : 0.065);
-    double amd = zen <= 90.0 ? 1.0 / (ct + 0.15 * pow(93.885 - zen, -1.253)) : NAN;
+    double amd = zen <= 90.0 ? 1.0 / (ct + 0.15 * pow_pos(93.885 - zen, -1.253)) : NAN;
     amd = amd * 101325.0 / 101325.0;
     amd = amd < 12.0 ? amd : (isnan(amd) ? amd : 12.0);
     g[G_AM] = amd;
     const double amd2 = amd * amd;
     g[G_KNC] = 0.866 - 0.122 * amd + 0.0121 * amd2 - 0.000653 * (amd2 * amd) + 0.000014 * (amd2 * amd2);
     g[G_DISCOK] = zen > 87.0 ? 0.0 : 1.0;
-    double proj = k.ctilt * czs + k.stilt * szs * cosd(az - k.saz);          // haydavies / aoi (pvmodel.py:66-72)
+    double proj = k.ctilt * czs + k.stilt * szs * caz;                      // haydavies / aoi (pvmodel.py:66-72)
     proj = proj > 1.0 ? 1.0 : (proj < -1.0 ? -1.0 : proj);
     const double cos_tt = proj > 0.0 ? proj : 0.0;
     g[G_RB] = cos_tt / (czs > 0.01745 ? czs : 0.01745);
@@ -947,7 +973,7 @@ __device__ __forceinline__ bool lane_row(LaneSite& ls, const double* sun, const 
         tl = ls.tl;
     }
     double g[ROW];
-    if (site_geom<false>(ls.k, sun, tl, module, g)) return true;
+    if (site_geom<false, sizeof(R) == 4>(ls.k, sun, tl, module, g)) return true;
     site_row<R>(g, sun, row);
     return g[G_GHICS] == 0.0;
 }
