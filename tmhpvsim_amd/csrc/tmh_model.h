@@ -865,6 +865,9 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     sincos(ha, &sha, &cha);
     double czr = k.slat * sun[SUN_SIND] + k.clat * sun[SUN_COSD] * cha;
     czr = czr > 1.0 ? 1.0 : (czr < -1.0 ? -1.0 : czr);
+    // the sun below -0.83 deg elevation (cos z < cos(90.84 deg) = -0.0147): outside the
+    // refraction band (de = 0), apparent zenith = zenith > 90 deg, night -- skip the rest
+    if (!FULL && czr < -0.015) return true;
     const double zen = deg(acos(czr));
     const double e0 = 90.0 - zen;
     double de = 0.0;
