@@ -77,6 +77,8 @@ s1, s2, s3 = torch.cuda.Stream(dev), torch.cuda.Stream(dev), torch.cuda.Stream(d
 p1, p2, p3 = C.c_void_p(s1.cuda_stream), C.c_void_p(s2.cuda_stream), C.c_void_p(s3.cuda_stream)
 build(a, p1)
 walk(a, p1)
+for _ in range(5):   # warm-up (clocks, code objects): the first variant is not the slow one
+    expand(a, p1)
 torch.cuda.synchronize()
 
 variants = {
