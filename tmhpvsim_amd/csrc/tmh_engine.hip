@@ -1703,10 +1703,13 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
     FSamp<R> fs;
     const MinuteCtx mc{dp, chain, W0, fm, events, (int)min(*n_events, ev_cap_dev(nsteps)), tab64};
     LaneSite ls{};   // per-chain sites (C5): this chain's site constants
+    bool blk_night = false;
     if constexpr (SITES) {
+        static_assert(BLOCK_STEPS <= 128, "site_block_night's bound assumes blocks of <= 128 s");
         ls.k = site_k(kp.sites + (size_t)(live ? gid(kp.ids, c) : 0) * 8);
         ls.linke = kp.site_linke ? kp.site_linke + (size_t)(live ? gid(kp.ids, c) : 0) * 12 : nullptr;
         ls.tl_doy = -1;
+        blk_night = site_block_night(ls.k, sun + (size_t)(b * BLOCK_STEPS) * SUN_W);
     }
     if (live) {
         alive = st.status[c] == 0;
@@ -1811,6 +1814,9 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
 #pragma unroll
         for (int i = 0; i < row_w<R>(); ++i) rowpf[i] = rowp[i];
     }
+#ifdef TMH_DIAG_HALF
+    R dg_csi = R(0), dg_pv = R(0);
+#endif
     auto second = [&](uint32_t j, uint32_t un, uint32_t um) {
         R row[row_w<R>()];
 #pragma unroll
@@ -1857,13 +1863,26 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 
         if ((jb & 31) == 0) cov_w = cov_lds[jb >> 5][threadIdx.x];
         const bool covered = (cov_w >> (jb & 31)) & 1u;
         uint32_t flp = fl;
-        if constexpr (SITES) {   // this chain's own site: geometry per chain-second
-            const bool night = lane_row<R>(ls, sun + (size_t)j * SUN_W, kp.module, row);
+        if constexpr (SITES) {   // this chain's own site: geometry per chain-second (none in a night block)
+            const bool night = blk_night || lane_row<R>(ls, sun + (size_t)j * SUN_W, kp.module, row);
             flp = night ? (fl | FL_NIGHT) : (fl & ~(uint32_t)FL_NIGHT);
         }
         R csi, pv, meter, res;
         bool held = false;   // fp32: PV in a guard band, recomputed in fp64 by fixup_kernel
+#ifdef TMH_DIAG_HALF   // diagnostic timing build only: the odd second reuses the even one's quantile / PV
+        if ((j & 1) && sizeof(R) == 4) {
+            csi = dg_csi;
+            pv = dg_pv;
+            meter = meter_w<R>(um);
+            res = meter - pv;
+        } else {
+            second_body<R>(kp, pkv, row, flp, fs, covered, noise_z<R>(un), meter_w<R>(um), csi, pv, meter, res, held);
+            dg_csi = csi + R(1e-7);
+            dg_pv = pv;
+        }
+#else
         second_body<R>(kp, pkv, row, flp, fs, covered, noise_z<R>(un), meter_w<R>(um), csi, pv, meter, res, held);
+#endif
         if constexpr (PF) {
 #pragma unroll
             for (int i = 0; i < row_w<R>(); ++i) rowpf[i] = rowp[i];

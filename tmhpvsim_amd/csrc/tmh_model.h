@@ -954,6 +954,21 @@ __device__ __forceinline__ void site_row(const double* g, const double* sun, R* 
     }
 }
 
+// True when the sun at site k stays below the refraction band (cos z < -0.015, where
+// site_geom<false> returns night) for the whole block of BLOCK seconds starting at the
+// sun row `sun`: cos z at the block start below -0.015 - 0.012.  Over 128 s the hour
+// angle moves by 2 pi 128 / 86400 = 0.0093 rad and cos z by at most that (its
+// derivative in the hour angle is cos(lat) cos(decl) sin(h) <= 1); the declination's
+// and the equation of time's drift add < 1e-5.  Exact: such a block's seconds are all night.
+__device__ __forceinline__ bool site_block_night(const SiteK& k, const double* sun)
+{
+    double tst = sun[SUN_MIN] + sun[SUN_EOT] + 4.0 * k.lon;
+    if (tst >= 1440.0) tst -= 1440.0;
+    if (tst < 0) tst += 1440.0;
+    const double czr = k.slat * sun[SUN_SIND] + k.clat * sun[SUN_COSD] * cos(rad(tst / 4.0 - 180.0));
+    return czr < -0.027;
+}
+
 // per-chain site state of a kernel lane: constants + the day's Linke turbidity
 struct LaneSite {
     SiteK k;
