@@ -1656,7 +1656,10 @@ template <typename R, int OUT, bool SITES>
 #ifndef TMH_SITES_WAVES   // min waves per SIMD of the per-chain-site expansion: 2 (a few spills) is 35 % faster than 1
 #define TMH_SITES_WAVES 2
 #endif
-__global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 1 : (OUT == OUT_TRACE3 ? TMH_EXP_WAVES : TMH_EXP_WAVES_STATS))) void expand_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0,
+#ifndef TMH_EXP_WAVES_F64   // min waves per SIMD of the fp64 single-site expansion: 4 = 128 VGPRs, 4-8 spilled (fp64 C2 6.2 -> 6.5e10, same box)
+#define TMH_EXP_WAVES_F64 4
+#endif
+__global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? TMH_EXP_WAVES_F64 : (OUT == OUT_TRACE3 ? TMH_EXP_WAVES : TMH_EXP_WAVES_STATS))) void expand_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0,
                                                      uint32_t n, int64_t W0, uint32_t nsteps, int64_t utc0,
                                                      const double* __restrict__ tab64,
                                                      const float* __restrict__ tab32,
