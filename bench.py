@@ -247,7 +247,7 @@ def main():
             self.expanded = None   # recorded after this context's last expansion
             self.state = torch.zeros(L.tmh_state_bytes(n), dtype=torch.uint8, device=dev)
             self.plan = torch.empty(L.tmh_plan_bytes(win), dtype=torch.uint8, device=dev)
-            self.scratch = torch.empty(L.tmh_scratch_bytes(n, win), dtype=torch.uint8, device=dev)
+            self.scratch = torch.empty(L.tmh_engine_scratch_bytes(sim._eng, n, win), dtype=torch.uint8, device=dev)
             if args.compact and args.mode == "stats" and nwin > 1:   # compacted windows: a working state
                 self.work = torch.empty_like(self.state)
                 self.ids = torch.empty(n, dtype=torch.int32, device=dev)

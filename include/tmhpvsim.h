@@ -152,6 +152,9 @@ int tmh_state_offsets(uint32_t n_chains, uint64_t* offsets);
 size_t tmh_plan_bytes(uint32_t n_steps);
 size_t tmh_scratch_bytes(uint32_t n_chains, uint32_t n_steps);
 size_t tmh_workspace_bytes(uint32_t n_chains, uint32_t n_steps);
+/* The scratch this engine's time-parallel path needs (its precision sizes the minute
+ * table: fp32 engines need less than tmh_scratch_bytes, which fits any engine). */
+size_t tmh_engine_scratch_bytes(const struct tmh_engine* eng, uint32_t n_chains, uint32_t n_steps);
 /* The segment walk's rows (16 lanes each, four per wavefront) per chain: with
  * chains_per_row = k the walk launches ceil(n / k) rows, each row starting with one
  * chain and taking the next unstarted chain of the window's queue when its chain

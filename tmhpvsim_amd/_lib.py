@@ -61,7 +61,7 @@ class Stats(C.Structure):
 
 
 EXPORTS = ["tmh_abi_version", "tmh_last_error", "tmh_state_bytes", "tmh_state_offsets", "tmh_plan_bytes",
-           "tmh_scratch_bytes", "tmh_workspace_bytes", "tmh_engine_create", "tmh_engine_destroy", "tmh_engine_path",
+           "tmh_scratch_bytes", "tmh_engine_scratch_bytes", "tmh_workspace_bytes", "tmh_engine_create", "tmh_engine_destroy", "tmh_engine_path",
            "tmh_init", "tmh_run", "tmh_plan", "tmh_step", "tmh_probe", "tmh_profile_enable", "tmh_profile_read",
            "tmh_set_shape_tables", "tmh_set_sites", "tmh_walk", "tmh_expand",
            "tmh_walk_part", "tmh_expand_part", "tmh_set_clock", "tmh_test_set_segment_capacity",
@@ -101,6 +101,8 @@ def load():
     L.tmh_plan_bytes.argtypes = [u32]
     L.tmh_scratch_bytes.restype = sz
     L.tmh_scratch_bytes.argtypes = [u32, u32]
+    L.tmh_engine_scratch_bytes.restype = sz
+    L.tmh_engine_scratch_bytes.argtypes = [p, u32, u32]
     L.tmh_workspace_bytes.restype = sz
     L.tmh_test_set_segment_capacity.argtypes = [u32, u32]
     if hasattr(L, "tmh_set_walk_chains_per_row"):

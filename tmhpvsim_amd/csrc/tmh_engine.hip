@@ -2291,16 +2291,17 @@ size_t plan_layout(uint32_t n_steps, void* base, PlanView* v)
     return o;
 }
 
-// ~4.2x the mean next_cloud calls of a window (~387 a day, max 806 in 16,384
-// chain-days measured with the oracle), a multiple of 16; the pool takes the rest
+// ~2.4x the mean next_cloud calls of a window (~400 a day, max 806 in 16,384
+// chain-days measured with the oracle; 931 a day), a multiple of 16; the pool takes the rest
 uint32_t g_cap_override = 0, g_pool_override = 0;   // tmh_test_set_segment_capacity (tests only)
-uint32_t seg_cap(uint32_t n_steps) { return g_cap_override ? g_cap_override : (n_steps / 64 + 256 + 15) & ~15u; }
+uint32_t seg_cap(uint32_t n_steps) { return g_cap_override ? g_cap_override : (n_steps / 128 + 256 + 15) & ~15u; }
 uint32_t pool_chunks(uint32_t n) { return g_pool_override ? g_pool_override : n / 16 + 8; }
 // (chain, block)s with a guard-band second of the fp32 PV chain: ~1e-5 of the
 // chain-seconds are such seconds, ~1.3e-3 of the blocks; room for 1/16
 uint32_t fix_cap(uint32_t n, uint32_t n_steps) { return (uint32_t)((uint64_t)n * nblk_of(n_steps) / 16) + 1024; }
 
-size_t scratch_layout(uint32_t n, uint32_t n_steps, void* base, SegView* v)
+// rbytes: bytes per minute-table entry, the engine's real (4 in fp32 mode, 8 in fp64)
+size_t scratch_layout(uint32_t n, uint32_t n_steps, void* base, SegView* v, size_t rbytes)
 {
     size_t o = 0;
     char* b = (char*)base;
@@ -2352,7 +2353,7 @@ size_t scratch_layout(uint32_t n, uint32_t n_steps, void* base, SegView* v)
         v->nmin = nmin;
         v->mtab = (void*)(b + o);
     }
-    o += align_up((size_t)n * nmin * 2 * 8);
+    o += align_up((size_t)n * nmin * 2 * rbytes);
     const uint32_t fc = fix_cap(n, n_steps);
     if (v) {
         v->fixcap = fc;
@@ -2453,12 +2454,23 @@ size_t tmh_plan_bytes(uint32_t n_steps) { return plan_layout(n_steps, nullptr, n
 
 size_t tmh_scratch_bytes(uint32_t n_chains, uint32_t n_steps)
 {
-    return scratch_layout(n_chains, n_steps, nullptr, nullptr);
+    return scratch_layout(n_chains, n_steps, nullptr, nullptr, 8);   // any engine (fp64 minute table)
 }
 
 size_t tmh_workspace_bytes(uint32_t n_chains, uint32_t n_steps)
 {
     return tmh_plan_bytes(n_steps) + tmh_scratch_bytes(n_chains, n_steps);
+}
+
+static size_t tmh_engine_scratch_rbytes(const struct tmh_engine* eng)
+{
+    return eng->kp.precision == TMH_FP64 ? 8 : 4;   // the minute table's real
+}
+
+size_t tmh_engine_scratch_bytes(const struct tmh_engine* eng, uint32_t n_chains, uint32_t n_steps)
+{
+    if (!eng) return tmh_scratch_bytes(n_chains, n_steps);
+    return scratch_layout(n_chains, n_steps, nullptr, nullptr, tmh_engine_scratch_rbytes(eng));
 }
 
 int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, struct tmh_engine** out)
@@ -2779,8 +2791,8 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
         return fail(TMH_E_INVAL, "bad histogram spec (n_bins %u in [1,16384], hi > lo)", stats->n_bins);
     if (int rc = check_tables(eng, n_chains)) return rc;
     const bool tp = eng->path == TMH_PATH_TIME_PARALLEL;
-    if (tp && (!scratch || scratch_bytes < tmh_scratch_bytes(n_chains, n_steps)))
-        return fail(TMH_E_INVAL, "scratch too small: %zu < %zu", scratch_bytes, tmh_scratch_bytes(n_chains, n_steps));
+    if (tp && (!scratch || scratch_bytes < tmh_engine_scratch_bytes(eng, n_chains, n_steps)))
+        return fail(TMH_E_INVAL, "scratch too small: %zu < %zu", scratch_bytes, tmh_engine_scratch_bytes(eng, n_chains, n_steps));
     if (int rc = hip_check(hipSetDevice(eng->device), "hipSetDevice")) return rc;
     PlanView pv;
     plan_layout(n_steps, (void*)plan, &pv);
@@ -2814,7 +2826,7 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
         return hip_check(hipGetLastError(), "chain_kernel launch");
     }
     SegView sg;
-    scratch_layout(n_chains, n_steps, scratch, &sg);
+    scratch_layout(n_chains, n_steps, scratch, &sg, f64 ? 8 : 4);
     const uint32_t cb = (n_chains + 255) / 256;
     const int64_t utc0 = eng->gp.clock.utc0;
     hipEvent_t t_step = phases == PH_ALL ? eng->mark(s) : nullptr;
@@ -2949,7 +2961,7 @@ int tmh_walk_part(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t
     PrevView prev{nullptr, nullptr};
     if (prev_scratch) {
         SegView ps;
-        scratch_layout(n_chains, prev_n_steps, const_cast<void*>(prev_scratch), &ps);
+        scratch_layout(n_chains, prev_n_steps, const_cast<void*>(prev_scratch), &ps, tmh_engine_scratch_rbytes(eng));
         prev = PrevView{ps.status, ps.end_p1};
     }
     const int ph = ((parts & TMH_WALK_DRAWS) ? PH_DRAWS : 0) | ((parts & TMH_WALK_SEGMENTS) ? PH_SEGMENTS : 0);
@@ -2986,7 +2998,7 @@ int tmh_run(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_cha
     if (!eng || !state) return fail(TMH_E_INVAL, "NULL engine/state");
     if (n_chains == 0 || n_steps == 0) return TMH_OK;
     const size_t pb = tmh_plan_bytes(n_steps);
-    const size_t need = eng->path == TMH_PATH_TIME_PARALLEL ? pb + tmh_scratch_bytes(n_chains, n_steps) : pb;
+    const size_t need = eng->path == TMH_PATH_TIME_PARALLEL ? pb + tmh_engine_scratch_bytes(eng, n_chains, n_steps) : pb;
     if (!workspace || workspace_bytes < need)
         return fail(TMH_E_INVAL, "workspace too small: %zu < %zu", workspace_bytes, need);
     if (int rc = tmh_plan(eng, step0, n_steps, workspace, stream)) return rc;

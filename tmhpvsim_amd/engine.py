@@ -169,7 +169,9 @@ class BatchedSim:
 
     # ------------------------------------------------------------------ run
     def workspace(self, n_steps):
-        return _torch().empty(self.L.tmh_workspace_bytes(self.n, n_steps), dtype=torch_uint8(), device=self.device)
+        """plan + scratch of one window (tmh_engine_scratch_bytes: this engine's precision)"""
+        nb = self.L.tmh_plan_bytes(n_steps) + self.L.tmh_engine_scratch_bytes(self._eng, self.n, n_steps)
+        return _torch().empty(nb, dtype=torch_uint8(), device=self.device)
 
     def run(self, n_steps, trace=TRACE_FIELDS, window=86400, out=None, compact=False):
         """Advance n_steps seconds.  Returns {field: tensor[n_steps, n_chains]} for `trace`.
