@@ -871,7 +871,12 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     const double zen = deg(acos(czr));
     const double e0 = 90.0 - zen;
     double de = 0.0;
-    if (e0 >= -1.0 * (0.26667 + 0.5667)) de = k.refr / (60.0 * tan(rad(e0 + 10.3 / (e0 + 5.11))));
+    // F32 rows: the refraction correction (< 0.6 deg) from an fp32 tangent, relative error
+    // ~1e-7 of de, i.e. ~1e-9 deg on the apparent zenith
+    if (e0 >= -1.0 * (0.26667 + 0.5667)) {
+        if constexpr (F32) de = k.refr / (60.0 * (double)tanf((float)rad(e0 + 10.3 / (e0 + 5.11))));
+        else de = k.refr / (60.0 * tan(rad(e0 + 10.3 / (e0 + 5.11))));
+    }
     const double azen = 90.0 - (e0 + de);
     // cos / sin of the apparent zenith zen - de from the true zenith's (czr, sqrt(1 - czr^2))
     // and the refraction angle's: |de| < 0.6 deg (0 below the horizon band), so its sine and
@@ -902,10 +907,16 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     } else
         g[G_CSIMAX] = 27.21 * exp(-114 * ct) + 1.665 * exp(-4.494 * ct) + 1.08;
     const double dni_extra = sun[SUN_DNIX];
-    const double am_rel = azen <= 90.0 ? 1.0 / (czs + 0.50572 * pow_pos(6.07995 + (90.0 - azen), -1.6364)) : NAN;
+    // F32 rows: the relative airmass only feeds Ineichen's exponent and the SAPM spectral
+    // polynomial (factors of GHI_cs and of the effective irradiance): fp32 power, ~2e-7
+    // relative; DISC's airmass (amd, below, ill-conditioned at low sun) stays fp64
+    const double am_rel = azen <= 90.0 ? 1.0 / (czs + 0.50572 * (F32 ? (double)__powf((float)(6.07995 + (90.0 - azen)), -1.6364f)
+                                                                      : pow_pos(6.07995 + (90.0 - azen), -1.6364)))
+                                       : NAN;
     const double am_abs = am_rel * k.pres / 101325.0;
     const double cz = czs > 0.0 ? czs : 0.0;
-    const double gexp = exp(-k.cg2 * am_abs * (k.fh1 + k.fh2 * (tl - 1.0)));
+    const double gx = -k.cg2 * am_abs * (k.fh1 + k.fh2 * (tl - 1.0));
+    const double gexp = F32 ? (double)__expf((float)gx) : exp(gx);   // F32: ~1e-7 relative on GHI_cs (kt guard band 4e-6)
     const double gmax = isnan(gexp) ? 0.0 : (gexp > 0.0 ? gexp : 0.0);
     g[G_GHICS] = k.cg1 * dni_extra * cz * tl / tl * gmax;                     // ineichen (pvmodel.py:60)
     const double I0 = sun[SUN_I0];
@@ -925,7 +936,9 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     g[G_DNIEXTRA] = dni_extra;
     g[G_TERM2] = k.term2;
     g[G_GFAC] = k.gfac;
-    const double aoi = deg(acos(proj));
+    // F32 rows: the angle of incidence only enters the SAPM AOI-loss polynomial (a factor
+    // of the direct POA): fp32 acos, ~1e-7 relative
+    const double aoi = F32 ? (double)(acosf((float)proj) * (float)(180.0 / 3.14159265358979323846)) : deg(acos(proj));
     g[G_COSAOI] = proj;   // cos(rad(aoi)): the same to ~3e-16 absolute
     double f1 = (((m[4] * am_abs + m[3]) * am_abs + m[2]) * am_abs + m[1]) * am_abs + m[0];   // sapm spectral
     f1 = isnan(f1) ? 0.0 : f1;
