@@ -2847,8 +2847,12 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     // groups of walk_lanes lanes, 16 per workgroup (16 G threads, 16 x WALK_CAND candidate slots in LDS)
     const uint32_t rows = (uint32_t)(((uint64_t)n_chains + eng->walk_cpr - 1) / eng->walk_cpr);
     const uint32_t G = eng->walk_lanes ? eng->walk_lanes : (n_chains > WALK_AUTO_SMALL ? 4u : 16u);
-    const dim3 wg((rows + 15) / 16), wt(16 * G);
-    const size_t wlds = 16 * WALK_CAND * sizeof(double);
+#ifndef TMH_WALK_WG_FULL   // 256-thread walk workgroups for every G (256 / G chains each) instead of 16 chains
+#define TMH_WALK_WG_FULL 0
+#endif
+    const uint32_t gpw = TMH_WALK_WG_FULL ? 256 / G : 16;   // groups (chains) per workgroup
+    const dim3 wg((rows + gpw - 1) / gpw), wt(gpw * G);
+    const size_t wlds = gpw * WALK_CAND * sizeof(double);
 #define WALK(Q, GG)                                                                                           \
     hipLaunchKernelGGL((segments_kernel<Q, GG>), wg, wt, wlds, s, eng->dp, v, chain0, n_chains, step0, n_steps, \
                        eng->gp.clock, pv.events, pv.n_events, sg, prev)
