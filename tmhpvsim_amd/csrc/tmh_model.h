@@ -817,6 +817,35 @@ __device__ void sun_at(int64_t utc, int doy, int leap, const double* linke, doub
     o[SUN_RDNIX] = 1.0 / o[SUN_DNIX];       // the fp32 row's reciprocal, once per step
 }
 
+// sine and cosine of x in [-pi, pi] (the hour angle): quadrant by rint(x 2/pi), the
+// Cody-Waite reduction and kernel polynomials of fdlibm's k_sin.c / k_cos.c / e_rem_pio2.c
+// (within 2.2e-16 relative on [-pi/4, pi/4], checked against numpy); straight-line,
+// about half of ocml's general-argument sincos
+__device__ __forceinline__ void sincos_pi(double x, double* sp, double* cp)
+{
+    const double k = rint(x * 0.63661977236758134308);
+    const double r = fma(-k, 6.07710050650619224932e-11, fma(-k, 1.57079632673412561417e+00, x));
+    const double z = r * r;
+    double ps = 1.58969099521155010221e-10;
+    ps = fma(ps, z, -2.50507602534068634195e-08);
+    ps = fma(ps, z, 2.75573137070700676789e-06);
+    ps = fma(ps, z, -1.98412698298579493134e-04);
+    ps = fma(ps, z, 8.33333333332248946124e-03);
+    ps = fma(ps, z, -1.66666666666666324348e-01);
+    const double sr = fma(r * z, ps, r);
+    double pc = -1.13596475577881948265e-11;
+    pc = fma(pc, z, 2.08757232129817482790e-09);
+    pc = fma(pc, z, -2.75573143513906633035e-07);
+    pc = fma(pc, z, 2.48015872894767294178e-05);
+    pc = fma(pc, z, -1.38888888888741095749e-03);
+    pc = fma(pc, z, 4.16666666666666019037e-02);
+    const double cr = fma(z * z, pc, fma(-0.5, z, 1.0));
+    const int q = (int)k & 3;
+    const double s0 = (q & 1) ? cr : sr, c0 = (q & 1) ? sr : cr;
+    *sp = (q & 2) ? -s0 : s0;
+    *cp = ((q + 1) & 2) ? -c0 : c0;
+}
+
 // x^y for x > 0 as exp2(y log2 x): within a few ulps of pow (|y log2 x| < 16 here),
 // about half of ocml's pow (its extra-precise log and special cases)
 __device__ __forceinline__ double pow_pos(double x, double y) { return exp2(y * log2(x)); }
@@ -862,7 +891,16 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     if (tst < 0) tst += 1440.0;
     const double ha = rad(tst / 4.0 - 180.0);
     double sha, cha;
-    sincos(ha, &sha, &cha);
+#ifdef TMH_DIAG_SINCOS32   // timing diagnostic only: the hour angle's sine / cosine in fp32
+    {
+        float sf, cf;
+        __sincosf((float)ha, &sf, &cf);
+        sha = sf;
+        cha = cf;
+    }
+#else
+    sincos_pi(ha, &sha, &cha);
+#endif
     double czr = k.slat * sun[SUN_SIND] + k.clat * sun[SUN_COSD] * cha;
     czr = czr > 1.0 ? 1.0 : (czr < -1.0 ? -1.0 : czr);
     // the sun below -0.83 deg elevation (cos z < cos(90.84 deg) = -0.0147): outside the
