@@ -1046,16 +1046,8 @@ __device__ uint64_t g_p1diag[65536 * 8];
 #endif
 
 // ---- lane-group primitives (DPP inside groups of G = 4, 8 or 16 lanes: one chain per group)
-template <int CTRL>
-__device__ __forceinline__ double dpp_row_f64(double old, double v)
-{
-    const int lo = __builtin_amdgcn_update_dpp(__double2loint(old), __double2loint(v), CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(v), CTRL, 0xF, 0xF, false);
-    return __hiloint2double(hi, lo);
-}
-
-// the same without an `old` operand: lanes whose source lies outside the row read
-// 0 (bound_ctrl), so no register is initialised for them first
+// a double moved across lanes by DPP without an `old` operand: lanes whose source lies
+// outside the row read 0 (bound_ctrl), so no register is initialised for them first
 template <int CTRL>
 __device__ __forceinline__ double mov_dpp_f64(double v)
 {
