@@ -41,6 +41,10 @@ def test_abi_version_and_layout():
         assert total >= int(off[21]) + 8 * n * _lib.TMH_SIGMA_CAP
     assert L.tmh_plan_bytes(86400) >= 86400 * 20 * 12
     assert L.tmh_workspace_bytes(4096, 86400) == L.tmh_plan_bytes(86400) + L.tmh_scratch_bytes(4096, 86400)
+    # no engine: the bound that fits any engine (an fp32 engine's minute table is half of it)
+    assert L.tmh_engine_scratch_bytes(None, 4096, 86400) == L.tmh_scratch_bytes(4096, 86400)
+    # a day window's scratch per chain (DESIGN.md "Data layout"): under 70 KB at the fp64 bound
+    assert L.tmh_scratch_bytes(1 << 20, 86400) < 70_000 * (1 << 20)
 
 
 def test_engine_create_validates_before_touching_device():
@@ -75,6 +79,8 @@ def test_null_arguments_rejected():
     assert L.tmh_walk_part(None, None, 0, 1, 0, 1, None, None, 0, None, 0, 3, None) == -1
     assert L.tmh_walk_part(None, None, 0, 1, 0, 1, None, None, 0, None, 0, 8, None) == -1
     assert b"parts" in L.tmh_last_error()
+    assert L.tmh_set_walk_lanes(None, 4) == -1
+    assert L.tmh_set_walk_chains_per_row(None, 2) == -1
 
 
 def test_params_struct_matches_header():
