@@ -470,19 +470,23 @@ def test_walk_chains_per_row_invariance(window):
             np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("window,markov", [(86400, False), (7200, False), (86400, True)])
-def test_walk_lanes_invariance(window, markov):
+@pytest.mark.parametrize("window,markov,start", [(86400, False, "2019-09-05 00:00:00"),
+                                                 (7200, False, "2019-09-05 00:00:00"),
+                                                 (7200, False, "2019-10-26 12:00:00"),   # DST fall-back
+                                                 (86400, True, "2019-09-05 00:00:00")])
+def test_walk_lanes_invariance(window, markov, start):
     """tmh_set_walk_lanes: the segment walk with 4, 8 or 16 lanes per chain (sigma
     entries spread over fewer lanes, more register chunks per lane; entries past
     the registers in the chain's global row) gives bit-identical results -- covered
     bit, PV, status, call counts and the window-end sigma arrays -- alone and with
     groups that take queued chains, in one window or in chained windows.  2,000
     chain-days reach sigma lengths past 64 (~0.5 % of the calls) on every path.  Markov
-    cloud cover with per-site tables (C5's walk inputs) too."""
+    cloud cover with per-site tables (C5's walk inputs) too, and chained windows across the
+    DST fall-back (the walk's clock shift)."""
     from tmhpvsim_amd import _lib
     from tmhpvsim_amd.params import site_shape_tables
     L = _lib.load()
-    n, steps, start = 2000, 86400, "2019-09-05 00:00:00"
+    n, steps = 2000, 86400
     mp = ModelParams(cc_mode=CC_MARKOV, seed=0x7AB1E) if markov else None
     tab = site_shape_tables(n) if markov else None
     outs = []
