@@ -8,9 +8,15 @@ chain-second's meter, pv and residual streamed to HBM (12 B / chain-second).
 One bench "step" = one batch: build the day's clock/geometry table, construct
 4,096 fresh chains (new global chain ids every step) and advance them 86,400 s.
 
-Multi-GPU (torchrun, one rank per GPU): weak scaling, every rank runs its own
-4,096 chains with distinct global ids; no data-path collective (chains are
-independent).  value = chain-seconds of all ranks / max rank time.
+Multi-GPU, one rank per GPU: `--gpus N` run directly (no WORLD_SIZE in the
+environment) starts N child ranks itself (`launch_ranks`, before this process
+touches torch or the GPU); under torchrun WORLD_SIZE must equal N.  C2 scales
+weakly: every rank runs its own 4,096 chains with distinct global ids, no
+data-path collective (chains are independent).  C3 / C4 / C5
+scale strongly: the node total (1,048,576 chains / 16,384 / 65,536 sites,
+BASELINE.json configs[2..4]) is split into contiguous global-id shards
+(`dist.shard`), and the RCCL all-reduce of the statistics is in the timed
+region.  value = chain-seconds of all ranks / max rank time.
 
 Roofline: the dominant kernel (expand_kernel, P2 of the time-parallel path) is
 timed with HIP events the library records on the stream it runs on
@@ -43,6 +49,73 @@ TRACE_BYTES = 12               # meter + pv + residual, fp32 (24 in fp64)
 # instruction issues over 2 cycles, MI355X_MICROARCH.md), in lane-ops/s
 VALU_PEAK_TLANE = 256 * 4 * 32 * 2.4e9 / 1e12
 
+# BASELINE.json configs[1..4]: C2 4,096 sites on one GPU (weak scaling: per GPU);
+# C3 1 M chains, C4 16,384 sites, C5 65,536 sites for the node (strong scaling)
+DEFAULT_CHAINS = {"c2": 4096, "c3": 1048576, "c4": 16384, "c5": 65536}
+STRONG = ("c3", "c4", "c5")
+
+
+def rank_chains(workload, chains, rank, world):
+    """This rank's chains: (chain0 of its shard within one batch, n_local, n_node, scaling).
+
+    Weak (c2): every rank has `chains` of its own, rank r's ids start at r * chains.
+    Strong (c3 / c4 / c5): `chains` is the node total, split into contiguous shards
+    (dist.shard: sizes differ by at most one)."""
+    from tmhpvsim_amd.dist import shard
+    if workload in STRONG:
+        c0, n = shard(chains, rank, world)
+        return c0, n, chains, "strong"
+    return rank * chains, chains, chains * world, "weak"
+
+
+def launch_ranks(n, argv, script=None):
+    """`bench.py --gpus N` started without a launcher: N child ranks of this script
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*, one GPU each), started before this
+    process imports torch.cuda or touches the GPU; this process only waits and
+    returns the worst exit status (it never execs).  Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    if os.environ.get("TMH_BENCH_SHARE_GPU") != "1":
+        visible = _visible_gpus()
+        if visible < n:
+            print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {visible} "
+                  f"(TMH_BENCH_SHARE_GPU=1 runs every rank on device 0, rehearsal only)", file=sys.stderr)
+            return 2
+    with socket.socket() as s:   # a free rendezvous port on the loopback interface
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                r = p.poll()
+                if r is None:
+                    continue
+                pending.remove(p)
+                if r != 0 and rc == 0:   # one rank failed: the others would wait in a collective
+                    rc = r
+                    for q in pending:
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc if rc >= 0 else 128 - rc
+
+
+def _visible_gpus():
+    """GPUs this process may use, without initialising HIP (torch.cuda.device_count
+    reads the device list only on this image)."""
+    import torch
+    return torch.cuda.device_count()
+
 
 def parse():
     ap = argparse.ArgumentParser()
@@ -54,7 +127,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--chains", type=int, default=None, help="chains per GPU (c2: 4096, c5: 65536)")
+    ap.add_argument("--chains", type=int, default=None,
+                    help="c2: chains per GPU (4096, weak scaling); c3 / c4 / c5: chains of the whole node, "
+                         "sharded over the GPUs (1048576 / 16384 / 65536, strong scaling)")
     ap.add_argument("--seconds", type=int, default=None, help="c2: 86400, c5: 604800")
     ap.add_argument("--window", type=int, default=None, help="steps per tmh_step window (c2: all, c5: 86400)")
     ap.add_argument("--cc", default=None, choices=["faithful", "markov"],
@@ -105,8 +180,10 @@ def parse():
                     help="batches in flight on separate HIP streams (1 = no overlap): the segment walks of the "
                          "next batches (latency-bound, one wave per SIMD) run beside this batch's expansion")
     a = ap.parse_args()
+    if a.gpus < 1:
+        ap.error("--gpus must be >= 1")
     c5, c4 = a.workload == "c5", a.workload == "c4"
-    a.chains = a.chains or {"c2": 4096, "c3": 1048576, "c4": 16384, "c5": 65536}[a.workload]
+    a.chains = a.chains or DEFAULT_CHAINS[a.workload]
     a.seconds = a.seconds or {"c2": 86400, "c3": 86400, "c4": 365 * 86400, "c5": 604800}[a.workload]
     if a.compact is None:
         a.compact = int(c5)
@@ -171,12 +248,17 @@ def pmc_record(args, n, launch_secs):
     """The committed PMC record of the dominant kernel on this workload
     (profiles/pmc_kernels.json, written by scripts/pmc_summary.py from the
     rocprofv3 --pmc passes of scripts/pmc_workload.sh): per-launch VALU / SALU
-    wave-instructions and HBM bytes.  None when that workload was not measured."""
+    wave-instructions and HBM bytes.  None when that workload was not measured
+    with this build of the library (the record's build_stamp: a hash of the
+    sources and compile flags), so a kernel change cannot reuse stale counters."""
+    from tmhpvsim_amd.build import build_stamp
     path = os.path.join(ROOT, "profiles", "pmc_kernels.json")
     try:
         recs = json.load(open(path))["records"]
     except (OSError, ValueError, KeyError):
         return None
+    stamp = build_stamp()
+    recs = [r for r in recs if r.get("build_stamp") == stamp]
     want = dict(workload=args.workload, chains=n, launch_seconds=launch_secs, precision=args.precision,
                 mode=args.mode, cc=args.cc)
     compact = int(bool(args.compact and args.mode == "stats" and args.seconds > launch_secs))
@@ -188,12 +270,17 @@ def pmc_record(args, n, launch_secs):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus, sys.argv[1:])
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # TMH_BENCH_SHARE_GPU=1 (rehearsal only): every rank on device 0 over gloo, so
@@ -207,6 +294,9 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    if world > 1:   # the process group's own count, not the flag
+        world = dist.get_world_size()
+        rank = dist.get_rank()
 
     from tmhpvsim_amd import _lib
     from tmhpvsim_amd.engine import BatchedSim
@@ -215,15 +305,19 @@ def main():
     from tmhpvsim_amd.dist import all_reduce_stats
 
     L = _lib.load()
-    n, secs, win = args.chains, args.seconds, args.window
+    shard0, n, n_node, scaling = rank_chains(args.workload, args.chains, rank, world)
+    secs, win = args.seconds, args.window
+
+    def batch_chain0(k):   # global id of this rank's first chain in batch k: fresh chains every batch
+        return k * n_node + shard0
+
     c5 = args.workload == "c5"
     kw = {}
-    if c5:   # the grid's sites (rank r takes rows [r n, (r+1) n) of a 256 x 256 x world sweep)
-        grid = site_grid(256 * world, 256) if n == 65536 else site_grid(max(1, n // 256) * world, 256)
-        sl = slice(rank * n, (rank + 1) * n)
-        kw = dict(shape_tables=site_shape_tables(n, site0=rank * n), sites=grid[sl][:n])
+    if c5:   # the node's 256 x 256 lat/lon grid (or chains / 256 rows); this rank's shard of it
+        grid = site_grid(max(1, (args.chains + 255) // 256), 256)
+        kw = dict(shape_tables=site_shape_tables(n, site0=shard0), sites=grid[shard0:shard0 + n])
     sim = BatchedSim(n, args.start, tz="Europe/Berlin", params=ModelParams(cc_mode=CC_MARKOV if args.cc == "markov" else 0),
-                     precision=args.precision, chain0=rank * n, device=dev, horizon=secs, kernel_path=args.path, **kw)
+                     precision=args.precision, chain0=shard0, device=dev, horizon=secs, kernel_path=args.path, **kw)
     real = sim.real
     if args.walk_cpr != 1:
         _lib.check(L.tmh_set_walk_chains_per_row(sim._eng, args.walk_cpr))
@@ -279,7 +373,7 @@ def main():
 
     def one_step(k):   # a whole batch on its context's streams
         cx = ctxs[k % len(ctxs)]
-        chain0 = (rank + k * world) * n                    # fresh global chains every batch
+        chain0 = batch_chain0(k)                          # fresh global chains every batch
         _lib.check(L.tmh_init(sim._eng, C.c_void_p(cx.state.data_ptr()), chain0, n, None, cx.sptr))
         if nwin == 1 or sim.path != "time_parallel":
             for s0 in range(0, secs, win):   # windows: a trace window is overwritten by the next
@@ -358,7 +452,7 @@ def main():
 
     def build(k):      # construction of batch k's chains, its plan and draws
         cx = ctxs[k % len(ctxs)]
-        cx.chain0 = (rank + k * world) * n
+        cx.chain0 = batch_chain0(k)
         if args.build_on == "walk":   # on the batch's walk stream, after the expansion
             bs, bp = cx.wstream, cx.wptr   # that last used this context: beside the running expansion
             if cx.expanded is not None:
@@ -415,7 +509,7 @@ def main():
 
     def g_build(j, gate):
         cx = ctxs[j % len(ctxs)]
-        cx.chain0 = (rank + j * world) * n
+        cx.chain0 = batch_chain0(j)
         if gate is not None:
             bst.wait_event(gate)
         if cx.expanded is not None:                        # the context's previous batch is committed
@@ -560,7 +654,10 @@ def main():
         t = torch.tensor([elapsed, kmean], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kmean = float(t[0]), float(t[1])
-    chain_seconds = world * n * secs * args.steps
+        b = torch.tensor([bad], device=dev, dtype=torch.int64)
+        dist.all_reduce(b, op=dist.ReduceOp.SUM)
+        bad = int(b[0])
+    chain_seconds = n_node * secs * args.steps                 # every rank's chains (C2: n per rank)
     # stats mode: the chain-seconds actually simulated = the histogram's count (a chain
     # that faults, e.g. the reference's AssertionError in markov mode, freezes and
     # records nothing more; edge bins absorb out-of-range residuals)
@@ -600,18 +697,24 @@ def main():
                 "valu_per_chain_second": v.get("valu_per_chain_second"),
                 "salu_per_chain_second": v.get("salu_per_chain_second"),
                 "source": "VALU lane-ops = SQ_INSTS_VALU x 64 per launch (profiles/pmc_kernels.json) / HIP-event "
-                          "launch time" if rec else "no PMC record for this workload in profiles/pmc_kernels.json"}
+                          "launch time" if rec else "no PMC record of this build for this workload in "
+                                                    "profiles/pmc_kernels.json"}
     line = {
         "metric": "simulated chain-seconds/sec (node) at 1/2/4/8 GPUs + % HBM roofline",
         "value": value, "unit": "chain-seconds/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic (keyed Philox)",
-        "config": {"workload": (f"{args.workload.upper()}: {n} chains/GPU x {secs} s at 1 s, Munich, Europe/Berlin, "
+        "scaling": scaling, "vs_baseline": None, "dtype": args.precision, "data": "synthetic (keyed Philox)",
+        "config": {"workload": (f"{args.workload.upper()}: {n_node} chains"
+                                + (f" ({n} per GPU)" if scaling == "weak" else f" on {world} GPU(s)")
+                                + f" x {secs} s at 1 s, Munich, Europe/Berlin, "
                                 + (f"{win} s windows, " if nwin > 1 else "") if not c5 else
-                                f"C5: {n} sites/GPU on a lat/lon grid (35-60 N, 10 W-30 E) x {secs} s, {args.cc} cc "
-                                f"with per-site tables, per-site PV geometry, {win} s windows, Europe/Berlin, ")
-                               + f"{args.start[:10]}, {args.mode} mode ({'meter+pv+residual fp32 trace' if args.mode == 'trace' else 'on-GPU stats'})",
-                   "chains_per_gpu": n, "seconds": secs, "parallelism": f"chains sharded over {world} GPU(s)",
+                                f"C5: {n_node} sites on a lat/lon grid (35-60 N, 10 W-30 E, {world} GPU(s)) x {secs} s, "
+                                f"{args.cc} cc with per-site tables, per-site PV geometry, {win} s windows, Europe/Berlin, ")
+                               + f"{args.start[:10]}, {args.mode} mode ("
+                               + (f"meter+pv+residual {args.precision} trace" if args.mode == "trace" else f"on-GPU {args.precision} stats")
+                               + ")",
+                   "chains_node": n_node, "chains_per_gpu": n, "seconds": secs,
+                   "parallelism": f"chains sharded over {world} GPU(s), {scaling} scaling",
                    "batches_in_flight": len(ctxs), "staggered": bool(args.stagger and nwin == 1),
                    "construction_on": args.build_on, "walk_priority": args.walk_priority,
                    "schedule": args.schedule if (args.stagger and nwin == 1 and len(ctxs) >= 3) else None,
@@ -634,4 +737,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -50,9 +50,11 @@ extern "C" {
 #define TMH_CHAIN_ASSERT_BINARY 2   /* cloud_cover_binary.py:90-98 (assert not recurse) */
 #define TMH_CHAIN_SIGMA_OVERFLOW 3  /* sigma arrays exceed TMH_SIGMA_CAP (no reference analogue) */
 #define TMH_CHAIN_U_EXHAUSTED 4     /* injected uniform stream ran out */
-#define TMH_CHAIN_SEGMENT_OVERFLOW 5 /* > n_steps/64 + 256 + 2,048 cloud segments in one window, or the
-                                         window's shared overflow pool (n/16 + 8 chunks of 256) is full
-                                         (time-parallel path) */
+#define TMH_CHAIN_SEGMENT_OVERFLOW 5 /* > n_steps/128 + 256 + 2,048 cloud segments in one window; or more
+                                         than n_steps/128 + 256 while the batch's demand exceeds the
+                                         window's shared overflow pool (n/16 + 8 chunks of 256): then every
+                                         such chain faults at its first record past the row (deterministic;
+                                         time-parallel path) */
 #define TMH_CHAIN_GUARD_OVERFLOW 6   /* fp32 guard-band records of the batch exceeded their room (never observed; time-parallel path) */
 
 /* ---- modes ---- */
@@ -189,7 +191,7 @@ int tmh_live_chains(struct tmh_engine* eng, const void* state, uint32_t n_chains
 int tmh_state_move(struct tmh_engine* eng, const void* src, uint32_t n_src, void* dst, uint32_t n_dst,
                    const uint32_t* map, const uint32_t* count, uint32_t cap, int scatter, void* stream);
 /* Tests only: segment records kept per chain (a multiple of 16; 0 = the default
- * n_steps/64 + 256) and the overflow pool's chunks (0 = n_chains/16 + 8), for
+ * n_steps/128 + 256, rounded up to 16) and the overflow pool's chunks (0 = n_chains/16 + 8), for
  * every later tmh_scratch_bytes / launch in this process.  Exercises the
  * overflow path, which the default sizes reach only on the windiest days. */
 int tmh_test_set_segment_capacity(uint32_t cap, uint32_t pool_chunks);

@@ -59,7 +59,10 @@ def record(d, **key):
     k = max(exp, key=lambda k: s[k].get("SQ_WAVES", 0) * s[k]["_dispatches"])
     c = s[k]
     rec = dict(key)
-    rec.update(kernel=k, dispatches=c["_dispatches"], source=os.path.basename(os.path.normpath(d)))
+    sys.path.insert(0, ROOT)
+    from tmhpvsim_amd.build import build_stamp
+    rec.update(kernel=k, dispatches=c["_dispatches"], source=os.path.basename(os.path.normpath(d)),
+               build_stamp=build_stamp())   # bench.py ignores a record of another build
     for name, cn in (("valu_insts_per_launch", "SQ_INSTS_VALU"), ("salu_insts_per_launch", "SQ_INSTS_SALU"),
                      ("trans_f32_insts_per_launch", "SQ_INSTS_VALU_TRANS_F32"), ("waves_per_launch", "SQ_WAVES"),
                      ("wave_cycles", "SQ_WAVE_CYCLES"), ("wait_any", "SQ_WAIT_ANY"),

@@ -1,0 +1,115 @@
+"""bench.py's multi-GPU plumbing on the CPU: per-rank chain arithmetic of the
+weak (C2) and strong (C3 / C4 / C5) workloads, the child-rank launcher, and the
+refusal of `--gpus N` without N devices."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def test_c3_divides_one_million_chains_over_the_node():
+    # BASELINE.json configs[2]: 1M chains x 1 day sharded over 8 x MI355X
+    for world in (1, 2, 4, 8):
+        parts = [bench.rank_chains("c3", bench.DEFAULT_CHAINS["c3"], r, world) for r in range(world)]
+        assert all(p[1] == 1_048_576 // world for p in parts)
+        assert all(p[2] == 1_048_576 and p[3] == "strong" for p in parts)
+        assert [p[0] for p in parts] == [r * (1_048_576 // world) for r in range(world)]
+    assert bench.rank_chains("c3", 1_048_576, 7, 8)[:2] == (7 * 131_072, 131_072)
+
+
+@pytest.mark.parametrize("wl,total", [("c4", 16_384), ("c5", 65_536), ("c3", 1_000_003)])
+def test_strong_workloads_cover_node_total_once(wl, total):
+    for world in (1, 3, 8):
+        parts = [bench.rank_chains(wl, total, r, world) for r in range(world)]
+        assert sum(p[1] for p in parts) == total
+        for (a0, an, _, _), (b0, _, _, _) in zip(parts, parts[1:]):
+            assert a0 + an == b0
+
+
+def test_c2_is_weak_scaled_per_gpu():
+    for world in (1, 2, 8):
+        parts = [bench.rank_chains("c2", 4096, r, world) for r in range(world)]
+        assert all(p[1] == 4096 and p[2] == 4096 * world and p[3] == "weak" for p in parts)
+        # distinct global ids: rank r's batch-0 chains start at r * 4096
+        assert [p[0] for p in parts] == [4096 * r for r in range(world)]
+
+
+def test_launch_ranks_starts_n_children_with_rank_env(tmp_path):
+    script = tmp_path / "child.py"
+    out = tmp_path / "out"
+    out.mkdir()
+    script.write_text(
+        "import json, os, sys\n"
+        "keys = ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT')\n"
+        f"open(os.path.join({str(out)!r}, os.environ['RANK']), 'w').write(json.dumps({{k: os.environ[k] for k in keys}}))\n"
+        "sys.exit(0)\n")
+    os.environ["TMH_BENCH_SHARE_GPU"] = "1"   # no device count check (no GPU here)
+    try:
+        rc = bench.launch_ranks(3, ["--gpus", "3"], script=str(script))
+    finally:
+        del os.environ["TMH_BENCH_SHARE_GPU"]
+    assert rc == 0
+    envs = [json.loads((out / str(r)).read_text()) for r in range(3)]
+    assert [e["RANK"] for e in envs] == ["0", "1", "2"] == [e["LOCAL_RANK"] for e in envs]
+    assert {e["WORLD_SIZE"] for e in envs} == {"3"}
+    assert {e["MASTER_ADDR"] for e in envs} == {"127.0.0.1"}
+    assert len({e["MASTER_PORT"] for e in envs}) == 1
+
+
+def test_launch_ranks_reports_a_failed_rank(tmp_path):
+    script = tmp_path / "child.py"
+    script.write_text("import os, sys, time\n"
+                      "if os.environ['RANK'] == '1': sys.exit(7)\n"
+                      "time.sleep(30)\n")   # the others are terminated, not waited for
+    os.environ["TMH_BENCH_SHARE_GPU"] = "1"
+    try:
+        rc = bench.launch_ranks(2, [], script=str(script))
+    finally:
+        del os.environ["TMH_BENCH_SHARE_GPU"]
+    assert rc == 7
+
+
+def test_gpus_2_without_two_devices_exits_nonzero():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "TMH_BENCH_SHARE_GPU")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    assert "needs 2 visible GPUs" in r.stderr
+
+
+def test_world_size_must_match_gpus():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "1"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2
+    assert "WORLD_SIZE=2" in r.stderr
+
+
+def test_stale_pmc_record_never_reaches_a_bench_line(tmp_path, monkeypatch):
+    """profiles/pmc_kernels.json records carry the build stamp of the library they
+    were measured with; bench.py uses only records of the current build."""
+    import argparse
+    from tmhpvsim_amd.build import build_stamp
+    key = dict(workload="c2", chains=4096, launch_seconds=86400, precision="fp32", mode="trace", cc="faithful")
+    (tmp_path / "profiles").mkdir()
+    args = argparse.Namespace(workload="c2", precision="fp32", mode="trace", cc="faithful", compact=0, seconds=86400)
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+
+    def write(stamp):
+        rec = dict(key, valu_insts_per_launch=1.0, salu_insts_per_launch=1.0, traffic_bytes_per_launch=1.0)
+        if stamp is not None:
+            rec["build_stamp"] = stamp
+        (tmp_path / "profiles" / "pmc_kernels.json").write_text(json.dumps({"records": [rec]}))
+
+    write(None)                     # an unstamped (pre-stamp) record
+    assert bench.pmc_record(args, 4096, 86400) is None
+    write("0123456789abcdef")       # another build's record
+    assert bench.pmc_record(args, 4096, 86400) is None
+    write(build_stamp())
+    assert bench.pmc_record(args, 4096, 86400)["traffic_bytes_per_launch"] == 1.0

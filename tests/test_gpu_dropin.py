@@ -104,3 +104,34 @@ def test_batched_sim_rolls_its_clock_past_the_horizon():
             x, y = torch.nan_to_num(x, nan=-1.0), torch.nan_to_num(y, nan=-1.0)
         assert torch.equal(x, y), f
     assert a.clock.step0 == 2 * 86400
+
+
+def test_read_pv_values_loop_shape():
+    """The reference's product loop (pvsim.py:21-41 with utils.py:13-45's fixedclock at
+    realtime=False): `pvmodel = PVModel()`, then `pvmodel.next(datetime(*t.timetuple()[:6]))`
+    for t = fromtimestamp(start + i), consecutive seconds across two 5,000-s look-ahead
+    block boundaries (pvmodel.py:45), through `from tmhpvsim_amd import PVModel` as
+    INTEGRATION.md tells a maintainer; equal to the oracle's keyed chain (fp64, 1e-12)."""
+    import time as _time
+    from tmhpvsim_amd import PVModel
+    from tmhpvsim_amd.clearskyindexmodel import _draw_seed
+    np.random.seed(20191027)
+    seed = _draw_seed()                 # the seed PVModel() draws from numpy's global state
+    np.random.seed(20191027)
+    pvmodel = PVModel()
+    start_time = _time.time()
+    n = 12000
+    pv, ks = [], []
+    for iteration in range(n):          # fixedclock(rate=1, realtime=False)
+        t = datetime.datetime.fromtimestamp(start_time + iteration)
+        time_sec = datetime.datetime(*t.timetuple()[:6])
+        pv.append(pvmodel.next(time_sec))
+        ks.append(int((pd.Timestamp(time_sec, tz="Europe/Berlin") - pvmodel._t0).total_seconds()))
+    pv, ks = np.array(pv), np.array(ks)
+    assert ks[0] >= 0 and (np.diff(ks) == 1).all()
+    t0 = pvmodel._t0.tz_localize(None).strftime("%Y-%m-%d %H:%M:%S")
+    ref = O.run(ModelParams(seed=seed), 0, 1, int(ks[-1]) + 1, t0, tz="Europe/Berlin", outputs=("pv",))
+    want = ref["pv"][ks, 0]
+    assert np.isfinite(pv).all() and (pv >= 0).all()
+    err = np.abs(pv - want) / np.maximum(np.abs(want), 1.0)
+    assert err.max() <= 1e-12

@@ -415,11 +415,14 @@ def test_c2_full_size_properties():
 @pytest.mark.parametrize("lanes", [16, 4])
 def test_segment_overflow_pool(lanes):
     """Segment records past a chain's row go to the shared overflow pool (the windy
-    tail of cloud_cover_binary.py:80-107's call count): with the row cut to 16
-    records every chain spills ~24 chunks' worth, and the outputs stay bit-identical;
-    with a pool too small for them, the chains that got no chunk end with
-    TMH_CHAIN_SEGMENT_OVERFLOW (5) and every other chain is unchanged.  Both walk
-    widths (16 and 4 lanes per chain: records flushed in groups of 16 / 4)."""
+    tail of cloud_cover_binary.py:80-107's call count).  With the row cut to 16
+    records every chain spills ~24 chunks' worth and the outputs stay bit-identical.
+    With the row cut to 400 records (only the windier chains spill) and a pool of
+    2 chunks, the fault is deterministic: exactly the chains with more than 400
+    records end with TMH_CHAIN_SEGMENT_OVERFLOW (5), at their first record past the
+    row (their outputs equal the unconstrained run's before that step and are NaN
+    from it), and every other chain is unchanged -- whichever claims of the
+    atomic pool counter the waves won.  Both walk widths (16 and 4 lanes per chain)."""
     from tmhpvsim_amd import _lib
     L = _lib.load()
     n, steps, start = 256, 86400, "2019-09-05 00:00:00"
@@ -427,27 +430,38 @@ def test_segment_overflow_pool(lanes):
     def run():
         s = _sim(n, start, tz="Europe/Berlin", prec="fp32", kernel_path="time_parallel", horizon=steps)
         _lib.check(L.tmh_set_walk_lanes(s._eng, lanes))
+        calls0 = s.state_field("ncalls").cpu().numpy().astype(np.int64)
         out = s.run(steps, trace=("covered", "pv"))
         torch.cuda.synchronize()
-        return s.status(), _np(out["covered"]), _np(out["pv"])
+        calls = s.state_field("ncalls").cpu().numpy().astype(np.int64) - calls0
+        return s.status(), _np(out["covered"]), _np(out["pv"]), calls
 
-    st0, cov0, pv0 = run()
+    st0, cov0, pv0, calls = run()
     try:
         _lib.check(L.tmh_test_set_segment_capacity(16, 4 * n))
-        st1, cov1, pv1 = run()
-        _lib.check(L.tmh_test_set_segment_capacity(16, 40))
-        st2, cov2, pv2 = run()
+        st1, cov1, pv1, _ = run()
+        _lib.check(L.tmh_test_set_segment_capacity(400, 2))
+        st2, cov2, pv2, _ = run()
     finally:
         L.tmh_test_set_segment_capacity(0, 0)
     np.testing.assert_array_equal(st1, st0)
     np.testing.assert_array_equal(cov1, cov0)
     np.testing.assert_array_equal(pv1, pv0)
-    hit = (st2 == 5)
-    assert 0 < hit.sum() < n
+    records = calls + 1                       # the window-start segment + one record per next_cloud call
+    ok0 = st0 == 0
+    want = ok0 & (records > 400)
+    assert 2 < want.sum() < ok0.sum()         # a pool of 2 chunks is short for them
+    hit = st2 == 5
+    np.testing.assert_array_equal(hit, want)  # exactly the chains that reached the pool
     keep = ~hit
     np.testing.assert_array_equal(st2[keep], st0[keep])
     np.testing.assert_array_equal(cov2[:, keep], cov0[:, keep])
     np.testing.assert_array_equal(pv2[:, keep], pv0[:, keep])
+    for c in np.nonzero(hit)[0]:               # equal up to the fault, NaN (covered 255) from it on
+        f = int(np.argmax(cov2[:, c] == 255))
+        assert 0 < f and (cov2[f:, c] == 255).all() and np.isnan(pv2[f:, c]).all()
+        np.testing.assert_array_equal(cov2[:f, c], cov0[:f, c])
+        np.testing.assert_array_equal(pv2[:f, c], pv0[:f, c])
 
 
 @pytest.mark.parametrize("window", [86400, 7200])

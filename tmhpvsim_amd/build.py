@@ -21,13 +21,26 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
+# -ffp-contract=off: no silent FMA contraction, so fp64 state arithmetic rounds
+# exactly like the reference's numpy/Python scalar operations.
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off"]
+
+
+def build_stamp():
+    """Hash of the library's sources and compile flags: measurement records taken
+    with another build (profiles/pmc_kernels.json) are recognised as stale."""
+    import hashlib
+    h = hashlib.sha256(" ".join([ARCH] + FLAGS).encode())
+    for d in DEPS:
+        h.update(os.path.basename(d).encode())
+        h.update(open(d, "rb").read())
+    return h.hexdigest()[:16]
+
+
 def build_lib(force=False, verbose=False):
     if not force and os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(d) for d in DEPS):
         return LIB
-    # -ffp-contract=off: no silent FMA contraction, so fp64 state arithmetic rounds
-    # exactly like the reference's numpy/Python scalar operations.
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
-           "-I", os.path.join(ROOT, "include"), "-o", LIB + ".tmp"] + SRC
+    cmd = [hipcc(), f"--offload-arch={ARCH}"] + FLAGS + ["-I", os.path.join(ROOT, "include"), "-o", LIB + ".tmp"] + SRC
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

@@ -46,10 +46,7 @@ using namespace tmh;
 
 namespace {
 
-#ifndef TMH_BLOCK_STEPS
-#define TMH_BLOCK_STEPS 128
-#endif
-constexpr int BLOCK_STEPS = TMH_BLOCK_STEPS;   // seconds per P2 work-item
+constexpr int BLOCK_STEPS = 128;   // seconds per P2 work-item
 static_assert(BLOCK_STEPS <= 128, "FixRec holds a 128-bit mask of a block's seconds");
 
 struct BlockDesc {                 // as of the step before the block start; -1 = none in the window
@@ -63,9 +60,13 @@ struct BlockDesc {                 // as of the step before the block start; -1 
 // Segment records: a chain's first `cap` records sit in its row of `rec`; records
 // past that go to 256-record chunks of a shared overflow pool, allocated by the
 // walk (atomic counter) and listed per chain in `ovf` (OVF_SLOTS chunks).  cap is
-// sized to ~4x the mean calls per window (~387 a day), so the pool
-// serves the windy tail; only a chain past cap + 256 OVF_SLOTS records, or a
-// full pool, ends with TMH_CHAIN_SEGMENT_OVERFLOW.
+// sized to ~2.3x the mean calls per window (~387 a day), so the pool
+// serves the windy tail.  TMH_CHAIN_SEGMENT_OVERFLOW is deterministic: a chain
+// past cap + 256 OVF_SLOTS records faults at that record (a property of the chain
+// alone); and when the batch's demand exceeds the pool (some claim failed: the
+// total demand, not the claim order, decides that), overflow_settle_kernel faults
+// EVERY chain that reached the pool, at its first record past the row
+// (`ovf_first`), whichever claims the atomic counter happened to grant.
 constexpr int OVF_SLOTS = 8, OVF_CHUNK = 256;
 struct SegView {                   // P1 -> P2 scratch
     int2* rec;                     // [n][cap] (first uncovered step, next call step), global steps
@@ -75,6 +76,8 @@ struct SegView {                   // P1 -> P2 scratch
     uint32_t pool_cap;
     uint32_t* pool_n;              // chunks handed out (zeroed by the draws phase)
     uint32_t* walk_q;              // the walk's chain queue: chains taken past the first `rows` (zeroed likewise)
+    uint32_t* pool_short;          // some chain found the pool exhausted (zeroed likewise)
+    int32_t* ovf_first;            // [n] window-relative step of the chain's record `cap` (INT_MAX: none)
     uint32_t* count;               // [n]
     int32_t* fault;                // [n] window-relative fault step (INT_MAX = none)
     uint32_t* status;              // [n] status after the window
@@ -1035,15 +1038,12 @@ __global__ __launch_bounds__(256) void candidates_kernel(DrawParams dp, StateVie
     if (c == 0 && k == 0) {   // the walk that follows hands out overflow chunks and queued chains
         *sg.pool_n = 0;
         *sg.walk_q = 0;
+        *sg.pool_short = 0;
     }
     if (c >= n || (prev.status ? prev.status[c] : st.status[c]) != 0) return;
     const U4 b = keyed_block(dp.seed, chain0 + gid(dp.ids, c), (uint64_t)(st.ncalls[c] + k), TAG_CLOUD, 0);
     sg.cand[(size_t)k * n + c] = pow_d(dp.alpha + dp.delta * u52(b.x, b.y), dp.expo);
 }
-
-#ifdef TMH_DIAG_P1
-__device__ uint64_t g_p1diag[65536 * 8];
-#endif
 
 // ---- lane-group primitives (DPP inside groups of G = 4, 8 or 16 lanes: one chain per group)
 // a double moved across lanes by DPP without an `old` operand: lanes whose source lies
@@ -1098,59 +1098,20 @@ __device__ __forceinline__ double bperm_f64(int src_lane, double v)
     return __hiloint2double(hi, lo);
 }
 
-#ifndef TMH_WALK_LANES_DEFAULT   // lanes per chain of the walk unless tmh_set_walk_lanes says otherwise (0: by batch size)
-#define TMH_WALK_LANES_DEFAULT 0
-#endif
 // Batch size up to which the automatic choice walks with 16 lanes per chain: up to 2
 // waves per SIMD the walk is latency-bound (C2: 4,096 chains, 1,024 waves) and the
 // short per-call chain of 16 lanes wins; past it the walk is throughput-bound and 4
 // lanes per chain (37 % fewer instructions, 14 instead of 36 VGPRs per chain) win
 // (r02, same box: C3 2.48 -> 2.69e11, C4 2.24 -> 2.36e11 chain-s/s).
 constexpr uint32_t WALK_AUTO_SMALL = 8192;
-#ifndef TMH_WALK_REG   // sigma entries held in VGPRs per chain (entries past them: the chain's global row)
-#define TMH_WALK_REG 64
-#endif
-#ifndef TMH_WALK_FIX   // sigma entries scanned unconditionally (>= 12: a reset_sigma array); the rest only when some chain of the wave needs them
-#define TMH_WALK_FIX 32
-#endif
-#ifndef TMH_DOOM_SKIP   // skip provably rejected tries (bit-exact, GPU-tested; measured: walk +1-3 %, off)
-#define TMH_DOOM_SKIP 0
-#endif
-static_assert(TMH_WALK_FIX >= 12, "reset_sigma writes up to 11 entries into the unconditional chunks");
+constexpr int WALK_REG = 64;   // sigma entries held in VGPRs per chain (entries past them: the chain's global row)
+constexpr int WALK_FIX = 32;   // entries scanned unconditionally; the rest only when some chain of the wave needs them
+static_assert(WALK_FIX >= 12, "reset_sigma writes up to 11 entries into the unconditional chunks");
 constexpr int WALK_CAND = 32;   // try-0 candidates per LDS refill of a chain (one exposed load per 32 calls)
-
-// True if, for the group's sigma arrays (lane-distributed: entry k = chunk k / G,
-// lane k % G), no cloud length a candidate can take (x / ws, x in the
-// power law's [xmin, xmax], cloud_cover_binary.py:35-40) makes any entry
-// possible (:83-87).  In real arithmetic entry k is possible for
-// ncl in (sl_k / f - sc_k, 5400 / (1 + f) - sc_k); the tests below keep a
-// relative margin of 1e-6, far above the few-ulp difference between these and
-// the fp64 predicate, so "doomed" never holds while some candidate could pass.
-// Entries past the register chunks: not doomed (no shortcut).
-template <int G, int NCH>
-__device__ __forceinline__ bool grp_doomed(const double (&vc)[NCH], const double (&vl)[NCH], int L, int p, int row0,
-                                           double f, double ws, const DrawParams& dp)
-{
-    constexpr double m = 1e-6;
-    const double rws = 1.0 / ws;
-    const double cmin = dp.x_lo * rws * (1.0 - m), cmax = dp.x_hi * rws * (1.0 + m);
-    bool hope = L > G * NCH;
-#pragma unroll
-    for (int ch = 0; ch < NCH; ++ch) {
-        const int k = ch * G + p;
-        const double sc = vc[ch], sl = vl[ch];
-        const bool h1 = sl * (1.0 + f) < 5400.0 * f * (1.0 + m);   // sl / f < 5400 / (1 + f)
-        const bool h2 = sl < f * (cmax + sc) * (1.0 + m);          // some ncl <= cmax passes nsl > sl
-        const bool h3 = (cmin + sc) * (1.0 + f) < 5400.0 * (1.0 + m);   // some ncl >= cmin passes tot < 5400
-        hope |= (k < L) & h1 & h2 & h3;
-    }
-    const uint64_t bal = __builtin_amdgcn_ballot_w64(hope);
-    return ((bal >> row0) & ((1ull << G) - 1)) == 0;
-}
 
 // P1: segment walk.  64 / G chains per wavefront, one per group of G lanes
 // (G = 16 / 8 / 4, tmh_set_walk_lanes); entry k of a chain's sigma arrays lives
-// in register chunk k / G, lane k % G of its group (entries TMH_WALK_REG.. stay
+// in register chunk k / G, lane k % G of its group (entries WALK_REG.. stay
 // in the chain's global sigma row).  Each loop iteration is one
 // CloudCoverBinary.next_cloud call (cloud_cover_binary.py:80-107) of every group
 // that still has a call inside the window; the per-call scalar work (clock
@@ -1160,32 +1121,20 @@ __device__ __forceinline__ bool grp_doomed(const double (&vc)[NCH], const double
 // between chunks.  Smaller G: fewer lanes (and issue slots) per chain-call,
 // more chunks per lane.  Output per chain: segment records (first uncovered
 // step, next call step) and the window-end binary state.
-#ifndef TMH_SEG_WAVES
-#define TMH_SEG_WAVES 1
-#endif
-#ifndef TMH_RETRY_BATCH   // retry candidates G at a time across the group (measured: walk +3 %, off)
-#define TMH_RETRY_BATCH 0
-#endif
-#ifndef TMH_SEG_PRIO   // wave issue priority of the walk (s_setprio) over the expansion beside it
-#define TMH_SEG_PRIO 0
-#endif
 template <bool QUEUE, int G>
-__global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
+__global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
                                                           int64_t W0, uint32_t nsteps, tmh_clock ck,
                                                           const int2* __restrict__ events,
                                                           const uint32_t* __restrict__ n_events, SegView sg,
                                                           PrevView prev)
 {
     static_assert(G == 4 || G == 8 || G == 16, "lanes per chain");
-    constexpr int NCH = TMH_WALK_REG / G;                          // register chunks
-    constexpr int NFIX = (TMH_WALK_FIX + G - 1) / G < NCH ? (TMH_WALK_FIX + G - 1) / G : NCH;
-    static_assert(NCH * G == TMH_WALK_REG, "TMH_WALK_REG: a multiple of 16");
+    constexpr int NCH = WALK_REG / G;                              // register chunks
+    constexpr int NFIX = (WALK_FIX + G - 1) / G < NCH ? (WALK_FIX + G - 1) / G : NCH;
+    static_assert(NCH * G == WALK_REG, "WALK_REG: a multiple of 16");
     constexpr int GSH = G == 4 ? 2 : G == 8 ? 3 : 4;
     constexpr int CARRY = 0x100 | (G - 1);                        // row_shl:G-1: group lane 0 <- group lane G-1
     extern __shared__ double walk_lds[];                           // [groups of the workgroup][WALK_CAND]
-#if TMH_SEG_PRIO
-    __builtin_amdgcn_s_setprio(TMH_SEG_PRIO);
-#endif
     const int lane = threadIdx.x & 63, p = lane & (G - 1), row0 = lane & ~(G - 1);
     double* const cbuf = walk_lds + (threadIdx.x >> GSH) * WALK_CAND;
     const int64_t W1 = W0 + nsteps;
@@ -1353,6 +1302,7 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
         }
         if (p == 0) {
             sg.count[c] = nrec;
+            if (nrec <= sg.cap) sg.ovf_first[c] = INT_MAX;   // never reached the pool
             sg.fault[c] = fault;
             sg.status[c] = status;
             sg.end_p1[c] = ccb;
@@ -1363,18 +1313,6 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
     };
     const uint32_t groups = gridDim.x * blockDim.x / G;
     if (live) start_chain();
-#ifdef TMH_DIAG_P1   // diagnostic build only: cycles per section of the walk (s_memtime)
-    uint64_t dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t dt = __builtin_amdgcn_s_memtime();
-#define DSTAMP(i)                                        \
-    {                                                    \
-        const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
-        dg[i] += t_ - dt;                                \
-        dt = t_;                                         \
-    }
-#else
-#define DSTAMP(i)
-#endif
     for (;;) {
         if constexpr (QUEUE) {
             while (live && !(active && e < W1)) {   // group-uniform: the group's chain is done, take the next one
@@ -1392,11 +1330,7 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
         // Every chunk an array of the wave reaches (and, for the shift, the one past it:
         // (last + 1) / G <= L / G) is processed; a reset (L <= 11) stays in the NFIX chunks.
         const int Lmax = wave_max_grp<G>(run ? L : 0);
-#ifdef TMH_DIAG_P1
-        dg[7] += 1;
-#endif
         if (!run) continue;
-        DSTAMP(6)
         while (next_ev <= e) {   // _next_day / _next_hour at steps <= e
             if (ev_fl & FL_DAY) {
                 wsb = wsa;
@@ -1411,7 +1345,6 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
         }
         double hf, df;
         fractions_at(wck, (int32_t)(e - W0), hf, df);
-        DSTAMP(0)
         const double hh = interp(ccb, cca, hf);
         const double h = 0.95 < hh ? 0.95 : hh;   // update_parameters
         const double ws = interp(wsb, wsa, df);
@@ -1422,39 +1355,16 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
             kb += WALK_CAND;
         }
         const double x0 = cbuf[rel - kb];
-        DSTAMP(1)
         // ---- next_cloud: tries (cloud_cover_binary.py:82-98)
         int tries = 0, last = -1;
         double ncl = 0.0, bdl = 0.0;
-#if TMH_RETRY_BATCH
-        // Retry candidates, G at a time: lane p of the group draws try tb + p's cloud
-        // length (keyed by the call and the try, so any lane can) and divides it by
-        // the chain's wind speed; a retry then costs one bpermute instead of a
-        // Philox block, a pow and a division on all G lanes.  ~2 % of the calls
-        // reject 20 candidates in a row (reset_sigma), ~8 % at least one.
-        double nb = 0.0;
-        int tb = -G;
-#endif
         for (;;) {
-#if TMH_RETRY_BATCH
-            if (tries == 0 && x0 >= 0.0) ncl = x0 / ws;
-            else {
-                if (tries - tb >= G) {   // group-uniform
-                    tb = tries;
-                    const int t = tries + p;
-                    nb = pow_d(dp.alpha + dp.delta * keyed_u(dp.seed, chain0 + gid(dp.ids, c), ncall, TAG_CLOUD, (uint32_t)(t >> 1), t & 1),
-                               dp.expo) / ws;
-                }
-                ncl = bperm_f64(row0 | (tries - tb), nb);
-            }
-#else
             double x;
             if (tries == 0 && x0 >= 0.0) x = x0;
             else x = pow_d(dp.alpha + dp.delta * keyed_u(dp.seed, chain0 + gid(dp.ids, c), ncall, TAG_CLOUD, (uint32_t)(tries >> 1),
                                                         tries & 1),
                            dp.expo);
             ncl = x / ws;
-#endif
             double bd = INFINITY;
             int bk = INT_MAX;
             auto scan = [&](int k, double sc, double sl) {   // :83-88, branch-free
@@ -1474,7 +1384,7 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
 #pragma unroll
             for (int ch = NFIX; ch < NCH; ++ch)
                 if (Lmax > G * ch) scan(ch * G + p, vc[ch], vl[ch]);   // wave-uniform
-            for (int k0 = NCH * G; k0 < L; k0 += G) {   // rare: entries TMH_WALK_REG..
+            for (int k0 = NCH * G; k0 < L; k0 += G) {   // rare: entries WALK_REG..
                 const int k = k0 + p;
                 if (k < L) scan(k, gsc[k], gsl[k]);
             }
@@ -1484,32 +1394,18 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
                 break;
             }
             ++tries;
-            for (;;) {
-                if (tries == 20) {   // reset_sigma (cloud_cover_binary.py:76-78); 300 (k+1) is exact
-                    const int nl = (int)(h * 12);
+            if (tries == 20) {   // reset_sigma (cloud_cover_binary.py:76-78); 300 (k+1) is exact
+                const int nl = (int)(h * 12);
 #pragma unroll
-                    for (int ch = 0; ch * G < 12; ++ch) {
-                        vc[ch] = 300.0 * (ch * G + p + 1);
-                        vl[ch] = f * vc[ch];
-                    }
-                    L = nl;
+                for (int ch = 0; ch * G < 12; ++ch) {
+                    vc[ch] = 300.0 * (ch * G + p + 1);
+                    vl[ch] = f * vc[ch];
                 }
-#if TMH_DOOM_SKIP
-                // try 0 failed (or the sigma arrays were just reset): if no cloud length
-                // the candidates can take makes any entry possible, every try up to the
-                // reset (or the assert) is rejected -- skip them.  Tries are keyed by
-                // (call, try), so skipping changes no later draw.
-                if ((tries == 1 || tries == 20) && grp_doomed<G>(vc, vl, L, p, row0, f, ws, dp)) {
-                    tries = tries == 1 ? 20 : 40;
-                    continue;
-                }
-#endif
-                break;
+                L = nl;
             }
             if (tries == 40) break;
         }
         ++ncall;
-        DSTAMP(2)
         if (last < 0) {   // assert not recurse (:91)
             status = TMH_CHAIN_ASSERT_BINARY;
             fault = (int32_t)(e - W0);
@@ -1522,7 +1418,6 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
             active = false;
             continue;
         }
-        DSTAMP(3)
         // sigma_cloud = r_[cl, nsc[:last+1]], sigma_clear = r_[clr, nsl[:last+1]] (:101-105);
         // clr = nsl[last] - sigma_clear[last] is the scan's dl of entry `last`, held by
         // the lane that owns it (its best is `last`)
@@ -1551,7 +1446,6 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
                 vl[ch] = first ? nclr : f * nsc;
             }
         }
-        DSTAMP(4)
         L = last + 2;
         cl = ncl;
         clr = nclr;
@@ -1559,13 +1453,16 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
         e = s_start + ceil_thr(cl + clr) - 1;
         if (nrec >= sg.cap && (nrec - sg.cap) % OVF_CHUNK == 0) {   // a new overflow chunk (windy tail)
             const uint32_t k = (nrec - sg.cap) / OVF_CHUNK;
+            if (k == 0 && p == 0) sg.ovf_first[c] = (int32_t)(s_start - W0);   // record `cap`: this call's
             int got = -1;
             if (k < OVF_SLOTS) {
                 int v = 0;
                 if (p == 0) v = (int)atomicAdd(sg.pool_n, 1u);
                 got = __builtin_amdgcn_ds_bpermute(row0 << 2, v);   // the whole group is active here
-                if ((uint32_t)got >= sg.pool_cap) got = -1;
-                else if (p == 0) sg.ovf[(size_t)c * OVF_SLOTS + k] = got;
+                if ((uint32_t)got >= sg.pool_cap) {
+                    got = -1;
+                    if (p == 0) atomicOr(sg.pool_short, 1u);   // the batch's demand exceeds the pool
+                } else if (p == 0) sg.ovf[(size_t)c * OVF_SLOTS + k] = got;
             }
             if (got < 0) {
                 status = TMH_CHAIN_SEGMENT_OVERFLOW;
@@ -1577,16 +1474,24 @@ __global__ __launch_bounds__(256, TMH_SEG_WAVES) void segments_kernel(DrawParams
         }
         put_rec(nrec, (int)(s_start + ceil_thr(cl) - 1), (int)e);
         ++nrec;
-        DSTAMP(5)
     }
     if constexpr (!QUEUE)   // one chain per group
         if (live) finish_chain();
-#ifdef TMH_DIAG_P1
-    if (lane == 0) {
-        const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-        for (int i = 0; i < 8; ++i) g_p1diag[w * 8 + i] = dg[i];
-    }
-#endif
+}
+
+// The pool ran short (overflow_settle, SegView): every chain that reached it faults
+// at its first record past the row, so which chains fault does not depend on the
+// order in which the walk's waves claimed chunks.  The chain's records below the
+// row cover every step before that fault; count is cut to them.
+__global__ __launch_bounds__(256) void overflow_settle_kernel(uint32_t n, SegView sg)
+{
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n || *sg.pool_short == 0) return;
+    const int32_t f = sg.ovf_first[c];
+    if (f == INT_MAX) return;
+    sg.status[c] = TMH_CHAIN_SEGMENT_OVERFLOW;
+    sg.fault[c] = f;
+    sg.count[c] = min(sg.count[c], sg.cap);
 }
 
 // ------------------------------------------------------------ P2: expand
@@ -1610,49 +1515,27 @@ __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t rs, uint32_t of
 // One work-item per (chain, block of 128 seconds).  The boundary draws come
 // from the draw tables, so the per-second loop holds only the R copies of the
 // sampler pairs and does no fp64 work in fp32 mode.
-#ifndef TMH_HELD_LDS
-#define TMH_HELD_LDS 1
-#endif
-#ifndef TMH_EXP_CHAIN_FAST
-#define TMH_EXP_CHAIN_FAST 0
-#endif
-#ifndef TMH_EXP_PRIO
-#define TMH_EXP_PRIO 0
-#endif
-#ifndef TMH_EXP_WG_TRACE   // threads per workgroup of the fp32 single-site trace expansion (C2)
-#define TMH_EXP_WG_TRACE 256
-#endif
-// Workgroup size of an expansion instantiation: one wave per workgroup lets the CUs'
-// SIMDs take expansion waves independently beside a walk wave that holds registers
-// on one of them (a 4-wave workgroup needs a slot on all four).
+// 256-thread workgroups: one-wave workgroups (so the SIMDs take expansion waves
+// independently of a walk wave's footprint) measured +5 % alone, no gain beside the walks
 template <typename R, int OUT, bool SITES>
 constexpr int exp_wg()
 {
-    return (OUT == OUT_TRACE3 && sizeof(R) == 4 && !SITES) ? TMH_EXP_WG_TRACE : 256;
+    return 256;
 }
-#ifndef TMH_ROW_PREFETCH   // fp32 single-site expansion: next second's geometry row loaded early
-#define TMH_ROW_PREFETCH 0
-#endif
-#ifndef TMH_PVF_VGPR   // leading PVF fields pinned in VGPRs in the fp32 expansion
-#define TMH_PVF_VGPR 8
-#endif
-#ifndef TMH_DIAG_EXP_LDS   // diagnostic: extra LDS per expand workgroup (caps its occupancy)
-#define TMH_DIAG_EXP_LDS 0
-#endif
-#ifndef TMH_EXP_WAVES   // min waves per SIMD of the fp32 single-site expansion: 7 = at most 72 VGPRs (alone -4 % vs 6, no VGPR spills)
-#define TMH_EXP_WAVES 7
-#endif
-#ifndef TMH_EXP_WAVES_STATS   // the same for the statistics / other outputs (C3, C4): 6 = 80 VGPRs (the 16-bit-pair LDS histogram, 8 KB, + 12 KB staging: 8 workgroups per CU; C3 / C4 +6 % over 5 waves)
-#define TMH_EXP_WAVES_STATS 6
-#endif
+constexpr int PVF_VGPR = 8;   // leading PVF fields pinned in VGPRs in the fp32 single-site expansion
+// min waves per SIMD (__launch_bounds__) of each expansion instantiation:
+//  fp32 single-site trace (C2): 7 = at most 72 VGPRs (alone -4 % vs 6, no VGPR spills);
+//  fp32 statistics / other outputs (C3, C4): 6 = 80 VGPRs (the 16-bit-pair LDS histogram,
+//    8 KB, + 12 KB staging: 8 workgroups per CU; +6 % over 5 waves);
+//  fp64 single-site: 4 = 128 VGPRs, 4-8 spilled (fp64 C2 6.2 -> 6.5e10, same box);
+//  per-chain sites (C5): 2 (a few spills) is 35 % faster than 1
 template <typename R, int OUT, bool SITES>
-#ifndef TMH_SITES_WAVES   // min waves per SIMD of the per-chain-site expansion: 2 (a few spills) is 35 % faster than 1
-#define TMH_SITES_WAVES 2
-#endif
-#ifndef TMH_EXP_WAVES_F64   // min waves per SIMD of the fp64 single-site expansion: 4 = 128 VGPRs, 4-8 spilled (fp64 C2 6.2 -> 6.5e10, same box)
-#define TMH_EXP_WAVES_F64 4
-#endif
-__global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? TMH_EXP_WAVES_F64 : (OUT == OUT_TRACE3 ? TMH_EXP_WAVES : TMH_EXP_WAVES_STATS))) void expand_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0,
+constexpr int exp_waves()
+{
+    return SITES ? 2 : (sizeof(R) == 8 ? 4 : (OUT == OUT_TRACE3 ? 7 : 6));
+}
+template <typename R, int OUT, bool SITES>
+__global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0,
                                                      uint32_t n, int64_t W0, uint32_t nsteps, int64_t utc0,
                                                      const double* __restrict__ tab64,
                                                      const float* __restrict__ tab32,
@@ -1663,17 +1546,8 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? TM
                                                      StatsView sv)
 {
     extern __shared__ uint32_t lds_hist[];
-#if TMH_EXP_PRIO   // wave issue priority of the expansion over the walks beside it (s_setprio)
-    __builtin_amdgcn_s_setprio(TMH_EXP_PRIO);
-#endif
-#if TMH_EXP_CHAIN_FAST   // 1-D grid, chain block fastest: the workgroups writing one trace row run together
-    const uint32_t ncb = (n + blockDim.x - 1) / blockDim.x;
-    const uint32_t b = blockIdx.x / ncb;
-    const uint32_t c = (blockIdx.x - b * ncb) * blockDim.x + threadIdx.x;
-#else
     const uint32_t c = blockIdx.y * blockDim.x + threadIdx.x;   // grid: x = time block, y = chain block
     const uint32_t b = blockIdx.x;
-#endif
     const bool live = c < n;
     if (sv.hist) {
         for (uint32_t i = threadIdx.x; i < (sv.n_bins + 1) / 2; i += blockDim.x) lds_hist[i] = 0;   // 16-bit bin pairs
@@ -1685,13 +1559,11 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? TM
     // the fp32 PV constants as per-lane registers (VGPRs): held in SGPRs across
     // the loop they are spilled to VGPR lanes and read back by v_readlane each step
     PVF pkv = kp.pvf;
-#if TMH_PVF_VGPR
     if constexpr (sizeof(R) == 4 && !SITES) {
         float* f = reinterpret_cast<float*>(&pkv);
 #pragma unroll
-        for (int i = 0; i < TMH_PVF_VGPR; ++i) asm volatile("v_mov_b32 %0, %1" : "=v"(f[i]) : "s"(f[i]));
+        for (int i = 0; i < PVF_VGPR; ++i) asm volatile("v_mov_b32 %0, %1" : "=v"(f[i]) : "s"(f[i]));
     }
-#endif
     Acc acc{0.0, 0.0, 0.0, -INFINITY};
     bool alive = false;
     int32_t fault = INT_MAX;
@@ -1773,12 +1645,9 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? TM
     }
     uint32_t cov_w = 0;
     const double* evd = sg.evd + c;
-#if TMH_HELD_LDS   // the guard-band seconds of the lane's block, a bit each, in LDS: no register carried through the loop
+    // the guard-band seconds of the lane's block, a bit each, in LDS: no register carried through the loop
     __shared__ uint4 held_lds[WGT];
     held_lds[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
-#else
-    bool held_any = false;   // fp32: some second of this block lies in a guard band (pv_power_f)
-#endif
     // Trace stores: one buffer resource per output for the block's rows (built here,
     // not per store) and one running per-lane byte offset; lanes past the last chain
     // start at 2^31, out of the resource's range, so the stores need no exec mask.
@@ -1799,24 +1668,10 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? TM
     const int32_t fault_eff = alive ? fault : 0;   // ok = j < fault_eff: one compare, no branch
     // One second.  Every lane computes it; a lane whose chain is faulted (or not
     // alive) emits NaN / no statistics.  un, um: the step's Philox words (noise, meter).
-    // fp32 single-site: the next second's geometry row is loaded (SMEM) as soon as this
-    // second's PV chain is done with the current one, so its latency overlaps the
-    // stores and bookkeeping instead of stalling the next second's first use (PMC:
-    // 40 % of the waves' cycles parked at s_waitcnt).  The load past the window's
-    // last row reads the plan's next table (unused).
-    constexpr bool PF = TMH_ROW_PREFETCH && sizeof(R) == 4 && !SITES;
-    R rowpf[row_w<R>()];
-    if constexpr (PF) {
-#pragma unroll
-        for (int i = 0; i < row_w<R>(); ++i) rowpf[i] = rowp[i];
-    }
-#ifdef TMH_DIAG_HALF
-    R dg_csi = R(0), dg_pv = R(0);
-#endif
     auto second = [&](uint32_t j, uint32_t un, uint32_t um) {
         R row[row_w<R>()];
 #pragma unroll
-        for (int i = 0; i < row_w<R>(); ++i) row[i] = PF ? rowpf[i] : rowp[i];
+        for (int i = 0; i < row_w<R>(); ++i) row[i] = rowp[i];
         rowp += RW;
         const uint32_t fl = sizeof(R) == 8 ? (uint32_t)(double)rowp[G_FLAGS - RW] : __float_as_uint(row[G_FLAGS + G32]);
         const bool ok = (int32_t)j < fault_eff;
@@ -1865,44 +1720,19 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? TM
         }
         R csi, pv, meter, res;
         bool held = false;   // fp32: PV in a guard band, recomputed in fp64 by fixup_kernel
-#ifdef TMH_DIAG_HALF   // diagnostic timing build only: the odd second reuses the even one's quantile / PV
-        if ((j & 1) && sizeof(R) == 4) {
-            csi = dg_csi;
-            pv = dg_pv;
-            meter = meter_w<R>(um);
-            res = meter - pv;
-        } else {
-            second_body<R>(kp, pkv, row, flp, fs, covered, noise_z<R>(un), meter_w<R>(um), csi, pv, meter, res, held);
-            dg_csi = csi + R(1e-7);
-            dg_pv = pv;
-        }
-#else
         second_body<R>(kp, pkv, row, flp, fs, covered, noise_z<R>(un), meter_w<R>(um), csi, pv, meter, res, held);
-#endif
-        if constexpr (PF) {
-#pragma unroll
-            for (int i = 0; i < row_w<R>(); ++i) rowpf[i] = rowp[i];
-        }
         held = held && ok;
         if constexpr (sizeof(R) == 4) {
-#if TMH_HELD_LDS
             if (held) {   // jb is wave-uniform: the word and the bit are scalars
                 uint32_t* hw = reinterpret_cast<uint32_t*>(&held_lds[threadIdx.x]) + (jb >> 5);
                 *hw |= 1u << (jb & 31);
             }
-#else
-            held_any |= held;   // guard band of a PV discontinuity: fixup_kernel redoes this block's such seconds in fp64
-#endif
         }
         csi = ok ? csi : R(NAN);
         pv = ok ? pv : R(NAN);
         meter = ok ? meter : R(NAN);
         res = ok ? res : R(NAN);
         const uint8_t cov = ok ? (covered ? 1 : 0) : 255;
-#ifdef TMH_DIAG_NO_STORE
-        if (live && csi == R(-12345))
-            emit<R, OUT, true>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok, held);
-#else
         if constexpr (OUT == OUT_TRACE3) {
             row_store(rs_pv, voff, pv);
             row_store(rs_m, voff, meter);
@@ -1911,7 +1741,6 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? TM
         } else if (live) {
             emit<R, OUT, true>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok, held);
         }
-#endif
     };
     // one Philox block per step pair: (x, y) for the even step, (z, w) for the odd one
     if (((W0 + j0) & 1) == 0 && ((j1 - j0) & 1) == 0) {
@@ -1928,12 +1757,8 @@ __global__ __launch_bounds__(256, SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? TM
         }
     }
     if constexpr (sizeof(R) == 4) {
-#if TMH_HELD_LDS
         const uint4 hm = held_lds[threadIdx.x];
         const bool held_any = (hm.x | hm.y | hm.z | hm.w) != 0;
-#else
-        const uint4 hm = make_uint4(~0u, ~0u, ~0u, ~0u);   // every second of the block
-#endif
         if (held_any) {   // (chain, block, seconds) for fixup_kernel (outside the loop: no registers held across it)
             const uint32_t k = atomicAdd(sg.nfix, 1u);
             if (k < sg.fixcap) sg.fix[k] = FixRec{c, b, jr, 0u, hm};
@@ -2344,8 +2169,11 @@ size_t scratch_layout(uint32_t n, uint32_t n_steps, void* base, SegView* v, size
     if (v) {
         v->pool_n = (uint32_t*)(b + o);
         v->walk_q = v->pool_n + 1;
+        v->pool_short = v->pool_n + 2;
     }
     o += ALIGN;
+    if (v) v->ovf_first = (int32_t*)(b + o);
+    o += align_up((size_t)n * 4);
     if (v) v->count = (uint32_t*)(b + o);
     o += align_up((size_t)n * 4);
     if (v) v->fault = (int32_t*)(b + o);
@@ -2401,7 +2229,7 @@ struct tmh_engine {
     uint32_t n_tab = 0;     // rows of the per-chain shape tables (0: none)
     uint32_t n_sites = 0;   // rows of the per-chain sites (0: the engine's one site)
     uint32_t walk_cpr = 1;  // chains per walk row (tmh_set_walk_chains_per_row)
-    uint32_t walk_lanes = TMH_WALK_LANES_DEFAULT;  // lanes per chain in the walk (tmh_set_walk_lanes)
+    uint32_t walk_lanes = 0;  // lanes per chain in the walk (tmh_set_walk_lanes; 0: by batch size)
     // kernel timing (tmh_profile_*): event pairs per kernel, read and recycled
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[TMH_K_COUNT];
@@ -2654,13 +2482,6 @@ static int check_tables(const tmh_engine* eng, uint32_t n_chains)
     return TMH_OK;
 }
 
-#ifdef TMH_DIAG_P1
-int tmh_diag_p1(uint64_t* out, uint32_t n)   // diagnostic build only
-{
-    return hip_check(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_p1diag), (size_t)n * 8), "diag copy");
-}
-#endif
-
 int tmh_set_walk_chains_per_row(struct tmh_engine* eng, uint32_t chains_per_row)
 {
     if (!eng) return fail(TMH_E_INVAL, "NULL engine");
@@ -2672,7 +2493,6 @@ int tmh_set_walk_chains_per_row(struct tmh_engine* eng, uint32_t chains_per_row)
 int tmh_set_walk_lanes(struct tmh_engine* eng, uint32_t lanes)
 {
     if (!eng) return fail(TMH_E_INVAL, "NULL engine");
-    if (lanes == 0) lanes = TMH_WALK_LANES_DEFAULT;
     if (lanes != 0 && lanes != 4 && lanes != 8 && lanes != 16) return fail(TMH_E_INVAL, "walk lanes %u: 4, 8 or 16", lanes);
     eng->walk_lanes = lanes;
     return TMH_OK;
@@ -2869,10 +2689,7 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     // groups of walk_lanes lanes, 16 per workgroup (16 G threads, 16 x WALK_CAND candidate slots in LDS)
     const uint32_t rows = (uint32_t)(((uint64_t)n_chains + eng->walk_cpr - 1) / eng->walk_cpr);
     const uint32_t G = eng->walk_lanes ? eng->walk_lanes : (n_chains > WALK_AUTO_SMALL ? 4u : 16u);
-#ifndef TMH_WALK_WG_FULL   // 256-thread walk workgroups for every G (256 / G chains each) instead of 16 chains
-#define TMH_WALK_WG_FULL 0
-#endif
-    const uint32_t gpw = TMH_WALK_WG_FULL ? 256 / G : 16;   // groups (chains) per workgroup
+    const uint32_t gpw = 16;   // groups (chains) per workgroup
     const dim3 wg((rows + gpw - 1) / gpw), wt(gpw * G);
     const size_t wlds = gpw * WALK_CAND * sizeof(double);
 #define WALK(Q, GG)                                                                                           \
@@ -2883,6 +2700,7 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     else if (G == 8) { if (q) WALK(true, 8); else WALK(false, 8); }
     else { if (q) WALK(true, 16); else WALK(false, 16); }
 #undef WALK
+    hipLaunchKernelGGL(overflow_settle_kernel, dim3(cb), dim3(256), 0, s, n_chains, sg);
     eng->close(TMH_K_SEGMENTS, t_seg, s);
     if (int rc = hip_check(hipGetLastError(), "segments kernel launch")) return rc;
     }
@@ -2912,18 +2730,14 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
                                                                                       : OUT_ANY;
     auto exp_grid = [&](uint32_t wg) {
         const uint32_t ecb = (n_chains + wg - 1) / wg;
-#if TMH_EXP_CHAIN_FAST
-        return dim3(sg.nblk * ecb);
-#else
         return dim3(sg.nblk, ecb);
-#endif
     };
     if (out == OUT_TRACE3 && tv.ld * (f64 ? 8u : 4u) * BLOCK_STEPS >= (1ull << 31))   // one block's rows: one buffer range
         return fail(TMH_E_INVAL, "trace ld %llu too large (a 128-step block of rows must stay under 2 GiB)",
                     (unsigned long long)tv.ld);
     const size_t lds_exp = stats && stats->hist ? (size_t)((stats->n_bins + 1) / 2) * 4 : 0;   // 16-bit bin pairs
 #define LAUNCH(R, O, S)                                                                                            \
-    hipLaunchKernelGGL((expand_kernel<R, O, S>), exp_grid(exp_wg<R, O, S>()), dim3(exp_wg<R, O, S>()), lds_exp + TMH_DIAG_EXP_LDS, s, eng->kp, eng->dp, v, chain0, n_chains,      \
+    hipLaunchKernelGGL((expand_kernel<R, O, S>), exp_grid(exp_wg<R, O, S>()), dim3(exp_wg<R, O, S>()), lds_exp, s, eng->kp, eng->dp, v, chain0, n_chains,      \
                        step0, n_steps, utc0, pv.tab64, pv.tab32, pv.sun, pv.events, pv.n_events, pv.desc, sg, tv, sv)
     if (eng->kp.sites) {   // per-chain sites: one instantiation per precision, any output
         if (f64) LAUNCH(double, OUT_ANY, true);

@@ -19,38 +19,23 @@ struct U4 {
     uint32_t x, y, z, w;
 };
 
-// Key schedule bump on the scalar unit (keys are the seed: wave-uniform).  The
-// asm is volatile so the compiler cannot hoist the twenty round keys of a
-// loop-invariant seed out of a kernel's main loop: held across the loop they
-// spill into VGPR lanes and every round pays a v_readlane (seen in expand_kernel).
-__device__ __forceinline__ void key_bump(uint32_t& k0, uint32_t& k1)
-{
-    asm volatile("s_add_u32 %0, %0, 0x9e3779b9\n\ts_add_u32 %1, %1, 0xbb67ae85" : "+s"(k0), "+s"(k1) : : "scc");
-}
-
-#ifndef TMH_PHILOX_OPAQUE
-#define TMH_PHILOX_OPAQUE 1
-#endif
+// Philox4x32-10 (Random123).  The key (the seed) is wave-uniform: round key r =
+// key + r (W0, W1) is one s_add with a literal each, from a base the compiler must
+// treat as fresh per call (the empty asm), so it neither hoists twenty
+// loop-invariant round keys of a kernel's main loop into SGPRs (held across the
+// loop they spill into VGPR lanes and every round pays a v_readlane) nor copies a
+// bumped register it still needs.
 __device__ __forceinline__ U4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                             uint32_t k0, uint32_t k1)
 {
     k0 = __builtin_amdgcn_readfirstlane(k0);
     k1 = __builtin_amdgcn_readfirstlane(k1);
-#if TMH_PHILOX_OPAQUE
-    // round key r = key + r (W0, W1): one s_add with a literal each, from a base the
-    // compiler must treat as fresh per call (so it neither hoists twenty loop-invariant
-    // round keys into SGPRs nor copies a bumped register it still needs)
     asm volatile("" : "+s"(k0), "+s"(k1));
     const uint32_t kb0 = k0, kb1 = k1;
-#endif
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-#if TMH_PHILOX_OPAQUE
         k0 = kb0 + (uint32_t)r * 0x9E3779B9u;
         k1 = kb1 + (uint32_t)r * 0xBB67AE85u;
-#else
-        if (r) key_bump(k0, k1);
-#endif
         // one v_mad_u64_u32 per product (both halves) instead of mul_lo + mul_hi:
         // about 25 % less issue time per block on gfx950 (scripts/micro/philox_bench.hip)
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0;

@@ -891,16 +891,7 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     if (tst < 0) tst += 1440.0;
     const double ha = rad(tst / 4.0 - 180.0);
     double sha, cha;
-#ifdef TMH_DIAG_SINCOS32   // timing diagnostic only: the hour angle's sine / cosine in fp32
-    {
-        float sf, cf;
-        __sincosf((float)ha, &sf, &cf);
-        sha = sf;
-        cha = cf;
-    }
-#else
     sincos_pi(ha, &sha, &cha);
-#endif
     double czr = k.slat * sun[SUN_SIND] + k.clat * sun[SUN_COSD] * cha;
     czr = czr > 1.0 ? 1.0 : (czr < -1.0 ? -1.0 : czr);
     // the sun below -0.83 deg elevation (cos z < cos(90.84 deg) = -0.0147): outside the
@@ -1182,19 +1173,9 @@ __device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float 
     // selecting twelve coefficient pairs per lane.
     const bool lo = kt <= 0.6f;
     const float t = kt - 0.6f;
-#ifdef TMH_DIAG_LITERAL_DISC   // diagnostic builds only: the literal (unshifted) coefficients
-    const float a_lo = fmaf(fmaf(fmaf(-2.222f, kt, 2.286f), kt, -1.56f), kt, 0.512f);
-    const float a_hi = fmaf(fmaf(fmaf(11.56f, kt, -27.49f), kt, 21.77f), kt, -5.743f);
-    const float b_lo = fmaf(0.962f, kt, 0.37f);
-    const float b_hi = fmaf(fmaf(fmaf(31.9f, kt, 66.05f), kt, -118.5f), kt, 41.4f);
-    const float c_lo = fmaf(fmaf(-2.048f, kt, 0.932f), kt, -0.28f);
-    const float c_hi = fmaf(fmaf(fmaf(73.81f, kt, -222.0f), kt, 184.2f), kt, -47.01f);
-    const float a = lo ? a_lo : a_hi, b = lo ? b_lo : b_hi, cc = lo ? c_lo : c_hi;
-#else
     const float a = lo ? disc_poly<3>(DISC_A_LO, t) : disc_poly<3>(DISC_A_HI, t);
     const float b = lo ? disc_poly<1>(DISC_B_LO, t) : disc_poly<3>(DISC_B_HI, t);
     const float cc = lo ? disc_poly<2>(DISC_C_LO, t) : disc_poly<3>(DISC_C_HI, t);
-#endif
     // exp(cc am) = exp2(cc * (am log2 e)): the fp32 row holds am log2 e (one rounding)
     const float dkn = fmaf(b, __builtin_amdgcn_exp2f(cc * g[G_AM]), a);
     float dni = (g[G_KNC] - dkn) * g[G_I0];
@@ -1223,11 +1204,7 @@ __device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float 
     const float C = k.ic0 * fmaf(k.ic3, dv, 1.0f);
     const float AmB = A - B, pmB = pdc - B;
     const float ac = fmaf(C, pmB * pmB, fmaf(-C, AmB, k.paco * __builtin_amdgcn_rcpf(AmB)) * pmB);
-#ifdef TMH_DIAG_NO_GUARD   // diagnostic builds only: cost of the guard band
-    risky = false;
-#else
     risky = fabsf(t) < KT_GUARD || fabsf(pdc - k.pso) < PDC_GUARD * k.pso;
-#endif
     // min(ac, Paco) unless NaN, -|Pnt| below the cut-in, .fillna(0), .clip(lower=0):
     // -|Pnt| <= 0 clips to 0 and a NaN fills to 0; the rest is one med3 into [0, Paco]
     return (pdc < k.pso || isnan(ac)) ? 0.0f : __builtin_amdgcn_fmed3f(ac, 0.0f, k.pacoc);
@@ -1282,16 +1259,9 @@ __device__ __forceinline__ R rinterp_row(const FSamp<R>& f, int k, const R* row,
 template <typename R>
 __device__ __forceinline__ R noise_z(uint32_t w)
 {
-#ifdef TMH_DIAG_NO_NDTRI
-    return R((double)w * 0x1p-32 - 0.5);
-#else
-#ifdef TMH_NOISE_POLISH   // the polished quantile for the per-second noise too
-    if constexpr (sizeof(R) == 8) return ndtri(u32d(w));
-#else   // ocml's ncdfinv alone: within 7e-16 of the exact quantile, far inside the fp64 bar
+    // fp64: ocml's ncdfinv alone, within 7e-16 of the exact quantile, far inside the fp64 bar
     if constexpr (sizeof(R) == 8) return ndtri_fast(u32d(w));
-#endif
     else return ndtri_w(w);
-#endif
 }
 
 template <typename R>
@@ -1318,12 +1288,8 @@ __device__ __forceinline__ void second_body(const KParams& kp, const PVF& pk, co
     const R a_clear = rinterp_row(fs, S_CLEAR_DAY, row, G_DAYF), a_cloudy = rinterp_row(fs, S_CLOUDY_HOUR, row, G_HOURF);
     const R n_clear = rinterp_row(fs, S_CLEAR_NOISE, row, G_MINF), n_cloudy = rinterp_row(fs, S_CLOUDY_NOISE, row, G_MINF);
     csi = (covered ? a_clear : a_cloudy) * ((covered ? n_clear : n_cloudy) + eps);
-#ifdef TMH_DIAG_NO_PV
-    pv = csi * row[G_GHICS + row_off<R>()];
-#else
     if constexpr (sizeof(R) == 8) pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power<R>(kp, row, csi) : R(0);
     else pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power_f(pk, row + G32, csi, risky) : 0.0f;
-#endif
     meter = meter_in;
     res = meter - pv;
 }
