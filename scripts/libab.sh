@@ -8,7 +8,7 @@ TAG="$1"; shift
 for rep in 1 2; do
 for v in "$@"; do
   lib=$PWD/tmhpvsim_amd/libtmh_$v.so; [ "$v" = cur ] && lib=$PWD/tmhpvsim_amd/libtmhpvsim.so
-  b=bench.py; [ "$v" = r01base ] && b=scripts/bench_r01.py   # the round-1 library (libtmh_r01base.so) with the round-1 bench
+  b=bench.py
   TMHPVSIM_LIB=$lib timeout -k 10 300 python $b --steps 10 --warmup 3 --no-cpu-baseline ${BARGS:-} > gpurun_out/lab_${TAG}_$v.json 2> gpurun_out/lab_${TAG}_$v.err || exit $?
   python3 -c "
 import json; d=json.loads(open('gpurun_out/lab_${TAG}_$v.json').read()); r=d['roofline']

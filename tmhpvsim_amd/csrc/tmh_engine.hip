@@ -1668,13 +1668,17 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
     const int32_t fault_eff = alive ? fault : 0;   // ok = j < fault_eff: one compare, no branch
     // One second.  Every lane computes it; a lane whose chain is faulted (or not
     // alive) emits NaN / no statistics.  un, um: the step's Philox words (noise, meter).
-    auto second = [&](uint32_t j, uint32_t un, uint32_t um) {
+    // wave_ok: no lane of the wave has a fault before the block's end (the common case),
+    // so a scalar branch skips the per-second NaN selects.
+    // lanes past the last chain store out of range (voff) and emit nothing: they never fault the wave
+    const bool wave_ok = __builtin_amdgcn_ballot_w64(live && fault_eff < (int32_t)j1) == 0;
+    auto second = [&](uint32_t j, uint32_t un, uint32_t um) __attribute__((always_inline)) {
         R row[row_w<R>()];
 #pragma unroll
         for (int i = 0; i < row_w<R>(); ++i) row[i] = rowp[i];
         rowp += RW;
         const uint32_t fl = sizeof(R) == 8 ? (uint32_t)(double)rowp[G_FLAGS - RW] : __float_as_uint(row[G_FLAGS + G32]);
-        const bool ok = (int32_t)j < fault_eff;
+        const bool ok = wave_ok || (int32_t)j < fault_eff;
         if (fl & (FL_DAY | FL_HOUR)) {            // _next_day, _next_hour (rare: loads waited here)
             const size_t eo = (size_t)evi * 4 * n;
             if (live) {
@@ -1720,7 +1724,17 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
         }
         R csi, pv, meter, res;
         bool held = false;   // fp32: PV in a guard band, recomputed in fp64 by fixup_kernel
-        second_body<R>(kp, pkv, row, flp, fs, covered, noise_z<R>(un), meter_w<R>(um), csi, pv, meter, res, held);
+        if (OUT != OUT_ANY && (!kp.with_pv || (flp & FL_NIGHT))) {
+            // the CSI is not an output (trace of pv / meter / residual, or statistics) and
+            // pv = 0 whatever it is (second_body: night, or no PV): no noise quantile, no
+            // samplers, no PV chain; the same values.  Wave-uniform for a single site.
+            csi = R(0);
+            pv = R(0);
+            meter = meter_w<R>(um);
+            res = meter - pv;
+        } else {
+            second_body<R>(kp, pkv, row, flp, fs, covered, noise_z<R>(un), meter_w<R>(um), csi, pv, meter, res, held);
+        }
         held = held && ok;
         if constexpr (sizeof(R) == 4) {
             if (held) {   // jb is wave-uniform: the word and the bit are scalars
@@ -1728,10 +1742,12 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
                 *hw |= 1u << (jb & 31);
             }
         }
-        csi = ok ? csi : R(NAN);
-        pv = ok ? pv : R(NAN);
-        meter = ok ? meter : R(NAN);
-        res = ok ? res : R(NAN);
+        if (!wave_ok) {
+            csi = ok ? csi : R(NAN);
+            pv = ok ? pv : R(NAN);
+            meter = ok ? meter : R(NAN);
+            res = ok ? res : R(NAN);
+        }
         const uint8_t cov = ok ? (covered ? 1 : 0) : 255;
         if constexpr (OUT == OUT_TRACE3) {
             row_store(rs_pv, voff, pv);
