@@ -1,0 +1,15 @@
+#!/bin/bash
+# GPU session: the -m gpu suite, then same-box A/B of the library against libtmh_$BASE.so
+# on C2 / C3 / C4 (scripts/libab.sh).  Usage: gpu_sess_c.sh TAG BASE
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TAG=${1:-c} BASE=${2:-nskip}
+[ -x scripts/micro/isa_rate ] && timeout -k 10 120 scripts/micro/isa_rate > gpurun_out/isa_rate.txt 2>&1; cat gpurun_out/isa_rate.txt
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider -rf --timeout 400 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_$TAG.log
+[ $rc -eq 0 ] || exit $rc
+bash scripts/libab.sh ${TAG}c2 $BASE cur || exit $?
+BARGS="--workload c3 --steps 4 --warmup 1" bash scripts/libab.sh ${TAG}c3 $BASE cur || exit $?
+BARGS="--workload c4 --steps 3 --warmup 1" bash scripts/libab.sh ${TAG}c4 $BASE cur || exit $?

@@ -82,8 +82,6 @@ struct SegView {                   // P1 -> P2 scratch
     int32_t* fault;                // [n] window-relative fault step (INT_MAX = none)
     uint32_t* status;              // [n] status after the window
     double* end_p1;                // [4][n] cc before/after, ws before/after at window end
-    double* end_p2;                // [6][n] clear_day, cloudy_noise, clear_noise pairs at window end
-    double* part;                  // [4][nblk][n] stats partials
     uint32_t nblk;
     double* evd;                   // [ev_cap][4][n] per boundary event: cc, ws, clear_day (day), clear_day (hour)
     uint32_t evcap;
@@ -95,7 +93,25 @@ struct SegView {                   // P1 -> P2 scratch
     uint32_t fixcap;
     uint32_t* nfix;                // records appended (> fixcap: some were lost, see commit_kernel)
     double* corr;                  // [2][n] exact pv / residual sum corrections of the fixed seconds
+    // The window's per-chain statistics, summed over its 128-s blocks by integer atomics:
+    // sums of pv, meter, residual in fixed point (units of 1 / fx_scale W s; integer
+    // addition is associative, so the totals do not depend on the order the blocks
+    // finish in) and the peak residual as an order-preserving int64 key (max_key).
+    long long* acc_fx;             // [3][n], zeroed with nfix / corr before each expansion
+    long long* acc_mx;             // [n]
+    double fx_scale, fx_inv;       // 2^k with 9,001 W x n_steps x 2^k < 2^62
 };
+
+// double <-> int64 key with the same order (max of keys = key of the max)
+__device__ __forceinline__ long long max_key(double v)
+{
+    const long long b = __double_as_longlong(v);
+    return b >= 0 ? b : b ^ 0x7FFFFFFFFFFFFFFFll;
+}
+__device__ __forceinline__ double max_unkey(long long k)
+{
+    return __longlong_as_double(k >= 0 ? k : k ^ 0x7FFFFFFFFFFFFFFFll);
+}
 
 // A (chain, 128-s block) of the fp32 expansion with a second in a guard band of
 // the PV chain's discontinuities (pv_power_f): fixup_kernel recomputes it.
@@ -383,7 +399,9 @@ __global__ __launch_bounds__(1024) void events_kernel(const float* __restrict__ 
     if (t == 1023) *n_events = cnt[1023];
 }
 
-__device__ __forceinline__ uint32_t ev_cap_dev(uint32_t n_steps) { return n_steps / 1800 + 64; }
+// Room for a window's day / hour boundary events: a local hour boundary every 3,600 s
+// (a day boundary is one of them) plus one per clock shift (<= 8), so n / 3600 + 10 at most
+__device__ __forceinline__ uint32_t ev_cap_dev(uint32_t n_steps) { return n_steps / 3600 + 16; }
 
 __host__ __device__ __forceinline__ int64_t first_minute(int64_t utc0, int64_t W0)
 {   // window-relative step of the first candidate minute boundary (UTC second 0)
@@ -645,6 +663,8 @@ __global__ __launch_bounds__(256) void minute_table_kernel(DrawParams dp, StateV
         if (c == 0) *sg.nfix = 0;
         sg.corr[c] = 0.0;
         sg.corr[(size_t)n + c] = 0.0;
+        for (int k = 0; k < 3; ++k) sg.acc_fx[(size_t)k * n + c] = 0;
+        sg.acc_mx[c] = max_key(-INFINITY);
     }
     if (c >= n || jm >= (int64_t)nsteps) return;
     const int ne = (int)min(*n_events, ev_cap_dev(nsteps));
@@ -997,6 +1017,7 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
 // local second-of-day at W0: 32-bit arithmetic, shift table in registers
 struct WinClock {
     int32_t sod0;                 // local second of day at W0
+    int32_t shifts;               // clock shifts inside or after the window (0: skip the table)
     int32_t step[8], delta[8];    // window-relative shift steps (INT_MAX = unused) and sizes
 };
 
@@ -1005,11 +1026,13 @@ __device__ __forceinline__ WinClock win_clock(const tmh_clock& ck, int64_t W0)
     WinClock w;
     const int64_t l0 = local_at(ck, W0);
     w.sod0 = (int32_t)(l0 - floordiv(l0, 86400) * 86400);
+    w.shifts = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const bool use = i < ck.n_shifts && ck.shift_step[i] > W0;
         w.step[i] = use ? (int32_t)(ck.shift_step[i] - W0) : INT_MAX;
         w.delta[i] = use ? ck.shift_delta[i] : 0;
+        w.shifts += use ? 1 : 0;
     }
     return w;
 }
@@ -1017,9 +1040,11 @@ __device__ __forceinline__ WinClock win_clock(const tmh_clock& ck, int64_t W0)
 __device__ __forceinline__ void fractions_at(const WinClock& w, int32_t j, double& hour_f, double& day_f)
 {
     int32_t sod = w.sod0 + j;
+    if (w.shifts) {   // wave-uniform: most windows (no DST change ahead) skip the shift table
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-        if (j >= w.step[i]) sod += w.delta[i];
+        for (int i = 0; i < 8; ++i)
+            if (j >= w.step[i]) sod += w.delta[i];
+    }
     sod %= 86400;
     if (sod < 0) sod += 86400;
     const int hour = sod / 3600, minute = (sod / 60) % 60, second = sod % 60;
@@ -1105,7 +1130,7 @@ __device__ __forceinline__ double bperm_f64(int src_lane, double v)
 // (r02, same box: C3 2.48 -> 2.69e11, C4 2.24 -> 2.36e11 chain-s/s).
 constexpr uint32_t WALK_AUTO_SMALL = 8192;
 constexpr int WALK_REG = 64;   // sigma entries held in VGPRs per chain (entries past them: the chain's global row)
-constexpr int WALK_FIX = 32;   // entries scanned unconditionally; the rest only when some chain of the wave needs them
+constexpr int WALK_FIX = 16;   // entries scanned unconditionally (one chunk at G = 16); the rest only when some chain of the wave needs them
 static_assert(WALK_FIX >= 12, "reset_sigma writes up to 11 entries into the unconditional chunks");
 constexpr int WALK_CAND = 32;   // try-0 candidates per LDS refill of a chain (one exposed load per 32 calls)
 
@@ -1212,7 +1237,13 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
         ev_ws = bperm_f64(src, eb_ws);
     };
     uint32_t ncall0 = 0, ncall = 0;
-    auto cand_at = [&](uint32_t k) { return k < sg.kcap ? sg.cand[(size_t)k * n + c] : -1.0; };
+    // call ncall0 + k's try-0 length: the table, or past it (the windiest chains) drawn here,
+    // one per lane of the group per refill, as candidates_kernel would have
+    auto cand_at = [&](uint32_t k) {
+        if (k < sg.kcap) return sg.cand[(size_t)k * n + c];
+        const U4 b = keyed_block(dp.seed, chain0 + gid(dp.ids, c), (uint64_t)(ncall0 + k), TAG_CLOUD, 0);
+        return pow_d(dp.alpha + dp.delta * u52(b.x, b.y), dp.expo);
+    };
     uint32_t kb = 0;                                     // cbuf holds the try-0 lengths of calls kb .. kb + WALK_CAND - 1
     double cn[WALK_CAND / G];                            // lane p: calls kb + WALK_CAND + j G + p (the next refill)
     auto cand_fill = [&]() {   // cn -> cbuf, then load the refill after it
@@ -1780,12 +1811,12 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
             if (k < sg.fixcap) sg.fix[k] = FixRec{c, b, jr, 0u, hm};
         }
     }
-    if (live && sv.acc) {
-        const size_t o = (size_t)b * n + c, stride = (size_t)sg.nblk * n;
-        sg.part[o] = acc.pv;
-        sg.part[stride + o] = acc.m;
-        sg.part[2 * stride + o] = acc.r;
-        sg.part[3 * stride + o] = acc.mx;
+    if (live && sv.acc) {   // the block's sums into the chain's fixed-point window totals (order-free)
+        unsigned long long* fx = reinterpret_cast<unsigned long long*>(sg.acc_fx);
+        atomicAdd(fx + c, (unsigned long long)llrint(acc.pv * sg.fx_scale));
+        atomicAdd(fx + (size_t)n + c, (unsigned long long)llrint(acc.m * sg.fx_scale));
+        atomicAdd(fx + 2 * (size_t)n + c, (unsigned long long)llrint(acc.r * sg.fx_scale));
+        __hip_atomic_fetch_max(sg.acc_mx + c, max_key(acc.mx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (sv.hist) {
         __syncthreads();
@@ -1867,18 +1898,6 @@ __global__ __launch_bounds__(256) void state_move_kernel(StateView src, StateVie
     }
 }
 
-// fmax into a double in global memory (compare-and-swap; rare: fixup_kernel only)
-__device__ void atomic_fmax(double* p, double v)
-{
-    unsigned long long* a = reinterpret_cast<unsigned long long*>(p);
-    unsigned long long old = *a;
-    while (v > __longlong_as_double((long long)old)) {
-        const unsigned long long seen = atomicCAS(a, old, (unsigned long long)__double_as_longlong(v));
-        if (seen == old) break;
-        old = seen;
-    }
-}
-
 // The fp32 expansion's guard-band seconds (the blocks FixRec lists), recomputed
 // in fp64 (redo_second) after the expansion and before the commit: the trace's pv and
 // residual are overwritten; the statistics get the exact differences of the
@@ -1918,7 +1937,7 @@ __global__ __launch_bounds__(256) void fixup_kernel(KParams kp, DrawParams dp, S
         if (sv.acc) {
             atomicAdd(&sg.corr[c], (double)pv - (double)pv32);
             atomicAdd(&sg.corr[(size_t)n + c], (double)res - (double)res32);
-            atomic_fmax(&sg.part[3 * (size_t)sg.nblk * n + (size_t)(j / BLOCK_STEPS) * n + c], (double)res);
+            __hip_atomic_fetch_max(sg.acc_mx + c, max_key((double)res), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (sv.hist) {
             const double x = ((double)res - sv.lo) * sv.scale;
@@ -1929,46 +1948,18 @@ __global__ __launch_bounds__(256) void fixup_kernel(KParams kp, DrawParams dp, S
     }
 }
 
-// Stats partials -> per-chain accumulators (fixed order: deterministic), then
-// the window-end state of P1/P2 -> chain state.
-// The window's per-chain statistics from the expansion's per-(block, chain) partials:
-// 32 chains x 8 segments of blocks per workgroup, each segment summed in block order,
-// the 8 segment sums combined in segment order (deterministic; 8x the memory-level
-// parallelism of one thread per chain, which left a 16,384-chain window on 64
-// workgroups: C4's commit 0.36 ms per day window).
-constexpr int RED_SEG = 8, RED_CH = 32;
-__global__ __launch_bounds__(256) void partials_reduce_kernel(uint32_t n, SegView sg, StatsView sv,
-                                                              const uint32_t* __restrict__ ids, uint32_t acc_n)
+// The window's per-chain statistics (fixed-point block sums + fixup_kernel's exact
+// corrections) into the caller's accumulators; every input is order-free, so the
+// result is deterministic.
+__global__ __launch_bounds__(256) void stats_commit_kernel(uint32_t n, SegView sg, StatsView sv,
+                                                           const uint32_t* __restrict__ ids, uint32_t acc_n)
 {
-    __shared__ double red[RED_SEG][4][RED_CH];
-    const uint32_t cl = threadIdx.x % RED_CH, seg = threadIdx.x / RED_CH;
-    const uint32_t c = blockIdx.x * RED_CH + cl;
-    const size_t stride = (size_t)sg.nblk * n;
-    double p = 0.0, m = 0.0, r = 0.0, mx = -INFINITY;
-    if (c < n) {
-        const uint32_t b0 = seg * sg.nblk / RED_SEG, b1 = (seg + 1) * sg.nblk / RED_SEG;
-        for (uint32_t b = b0; b < b1; ++b) {
-            const size_t o = (size_t)b * n + c;
-            p += sg.part[o];
-            m += sg.part[stride + o];
-            r += sg.part[2 * stride + o];
-            mx = fmax(mx, sg.part[3 * stride + o]);
-        }
-    }
-    red[seg][0][cl] = p;
-    red[seg][1][cl] = m;
-    red[seg][2][cl] = r;
-    red[seg][3][cl] = mx;
-    __syncthreads();
-    if (seg != 0 || c >= n) return;
-    for (int k = 1; k < RED_SEG; ++k) {
-        p += red[k][0][cl];
-        m += red[k][1][cl];
-        r += red[k][2][cl];
-        mx = fmax(mx, red[k][3][cl]);
-    }
-    p += sg.corr[c];                 // fixup_kernel's exact corrections
-    r += sg.corr[(size_t)n + c];
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const double p = (double)sg.acc_fx[c] * sg.fx_inv + sg.corr[c];
+    const double m = (double)sg.acc_fx[(size_t)n + c] * sg.fx_inv;
+    const double r = (double)sg.acc_fx[2 * (size_t)n + c] * sg.fx_inv + sg.corr[(size_t)n + c];
+    const double mx = max_unkey(sg.acc_mx[c]);
     const uint32_t g = gid(ids, c);
     const size_t an = acc_n ? acc_n : n;   // acc rows: the full batch
     sv.acc[g] += p;
@@ -1984,7 +1975,7 @@ __global__ __launch_bounds__(256) void commit_kernel(StateView st, uint32_t n, S
                                                      uint32_t acc_n)
 {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n) return;   // the statistics: partials_reduce_kernel, launched before
+    if (c >= n) return;   // the statistics: stats_commit_kernel, launched before
     (void)sv;
     (void)acc_n;
     if (st.status[c] != 0) return;
@@ -2120,11 +2111,12 @@ StateView make_view(void* base, uint32_t n)
 }
 
 // plan: tab64 | tab32 | events | n_events | block descriptors
-uint32_t ev_cap(uint32_t n_steps) { return n_steps / 1800 + 64; }
+uint32_t ev_cap(uint32_t n_steps) { return n_steps / 3600 + 16; }   // = ev_cap_dev
 uint32_t nblk_of(uint32_t n_steps) { return (n_steps + BLOCK_STEPS - 1) / BLOCK_STEPS; }
-// next_cloud calls a chain makes per window: ~0.0045 / s on average, < 0.0085 / s
-// on the busiest chains (windy days); calls past the table are drawn in the walk
-uint32_t cand_cap(uint32_t n_steps) { return n_steps / 100 + 128; }
+// next_cloud calls a chain makes per day window (the oracle, 4,096 chain-days): mean 386,
+// p99 620, p99.9 692, max 744; n / 150 + 32 covers 608 a day (~98.5 %); calls past the
+// table are drawn in the walk
+uint32_t cand_cap(uint32_t n_steps) { return n_steps / 150 + 32; }
 
 struct PlanView {
     double* tab64;
@@ -2154,14 +2146,15 @@ size_t plan_layout(uint32_t n_steps, void* base, PlanView* v)
     return o;
 }
 
-// ~2.4x the mean next_cloud calls of a window (~400 a day, max 806 in 16,384
-// chain-days measured with the oracle; 931 a day), a multiple of 16; the pool takes the rest
+// segment records (one per call + the window-start one): 656 a day, a multiple of 16,
+// exceeded by ~0.3 % of the chain-days (above); the pool (one 256-record chunk per 16
+// chains) takes that tail
 uint32_t g_cap_override = 0, g_pool_override = 0;   // tmh_test_set_segment_capacity (tests only)
-uint32_t seg_cap(uint32_t n_steps) { return g_cap_override ? g_cap_override : (n_steps / 128 + 256 + 15) & ~15u; }
+uint32_t seg_cap(uint32_t n_steps) { return g_cap_override ? g_cap_override : (n_steps / 135 + 16 + 15) & ~15u; }
 uint32_t pool_chunks(uint32_t n) { return g_pool_override ? g_pool_override : n / 16 + 8; }
 // (chain, block)s with a guard-band second of the fp32 PV chain: ~1e-5 of the
-// chain-seconds are such seconds, ~1.3e-3 of the blocks; room for 1/16
-uint32_t fix_cap(uint32_t n, uint32_t n_steps) { return (uint32_t)((uint64_t)n * nblk_of(n_steps) / 16) + 1024; }
+// chain-seconds are such seconds, ~1.3e-3 of the blocks; room for 1/64
+uint32_t fix_cap(uint32_t n, uint32_t n_steps) { return (uint32_t)((uint64_t)n * nblk_of(n_steps) / 64) + 1024; }
 
 // rbytes: bytes per minute-table entry, the engine's real (4 in fp32 mode, 8 in fp64)
 size_t scratch_layout(uint32_t n, uint32_t n_steps, void* base, SegView* v, size_t rbytes)
@@ -2198,10 +2191,6 @@ size_t scratch_layout(uint32_t n, uint32_t n_steps, void* base, SegView* v, size
     o += align_up((size_t)n * 4);
     if (v) v->end_p1 = (double*)(b + o);
     o += align_up((size_t)n * 4 * 8);
-    if (v) v->end_p2 = (double*)(b + o);
-    o += align_up((size_t)n * 6 * 8);
-    if (v) v->part = (double*)(b + o);
-    o += align_up((size_t)n * nblk * 4 * 8);
     const uint32_t evc = ev_cap(n_steps);
     if (v) {
         v->evcap = evc;
@@ -2226,10 +2215,14 @@ size_t scratch_layout(uint32_t n, uint32_t n_steps, void* base, SegView* v, size
         v->fix = (FixRec*)(b + o);
     }
     o += align_up((size_t)fc * sizeof(FixRec));
-    if (v) v->nfix = (uint32_t*)(b + o);   // nfix | corr[2][n]: zeroed before each expansion
+    if (v) v->nfix = (uint32_t*)(b + o);   // nfix | corr[2][n] | acc_fx | acc_mx: reset before each expansion
     o += ALIGN;
     if (v) v->corr = (double*)(b + o);
     o += align_up((size_t)n * 2 * 8);
+    if (v) v->acc_fx = (long long*)(b + o);
+    o += align_up((size_t)n * 3 * 8);
+    if (v) v->acc_mx = (long long*)(b + o);
+    o += align_up((size_t)n * 8);
     return o;
 }
 
@@ -2685,6 +2678,12 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     }
     SegView sg;
     scratch_layout(n_chains, n_steps, scratch, &sg, f64 ? 8 : 4);
+    {   // fixed-point scale of the statistics: |a window's sum| <= (9,000 + max(Paco, 0)) W x n_steps < 2^62 / 2^k
+        const double bound = (9000.0 + std::max(eng->kp.inverter[0], 0.0) + 1.0) * (double)n_steps;
+        const int k = 62 - (int)std::ceil(std::log2(bound));
+        sg.fx_scale = std::ldexp(1.0, k);
+        sg.fx_inv = std::ldexp(1.0, -k);
+    }
     const uint32_t cb = (n_chains + 255) / 256;
     const int64_t utc0 = eng->gp.clock.utc0;
     hipEvent_t t_step = phases == PH_ALL ? eng->mark(s) : nullptr;
@@ -2724,18 +2723,15 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     {   // the window's minute draws, one work-item each (read by the expansion and the commit)
         const int64_t fmh = first_minute_host(utc0, step0);
         const uint32_t nm = fmh < (int64_t)n_steps ? (uint32_t)((n_steps - 1 - fmh) / 60 + 1) : 0;
-        if (!nm)   // minute_table_kernel zeroes the guard-band bookkeeping; a window without a minute boundary:
-            if (int rc = hip_check(hipMemsetAsync(sg.nfix, 0, (size_t)((char*)(sg.corr + 2 * (size_t)n_chains) - (char*)sg.nfix), s),
-                                   "hipMemsetAsync"))
-                return rc;
-        if (nm) {
-            if (f64)
-                hipLaunchKernelGGL(minute_table_kernel<double>, dim3(cb, nm), dim3(256), 0, s, eng->dp, v, chain0,
-                                   n_chains, step0, n_steps, fmh, pv.tab64, pv.events, pv.n_events, sg);
-            else
-                hipLaunchKernelGGL(minute_table_kernel<float>, dim3(cb, nm), dim3(256), 0, s, eng->dp, v, chain0,
-                                   n_chains, step0, n_steps, fmh, pv.tab64, pv.events, pv.n_events, sg);
-        }
+        // row 0 of the grid also resets the expansion's bookkeeping (guard-band records,
+        // corrections, the fixed-point statistics): launched even without a minute boundary
+        const uint32_t gy = std::max(nm, 1u);
+        if (f64)
+            hipLaunchKernelGGL(minute_table_kernel<double>, dim3(cb, gy), dim3(256), 0, s, eng->dp, v, chain0,
+                               n_chains, step0, n_steps, fmh, pv.tab64, pv.events, pv.n_events, sg);
+        else
+            hipLaunchKernelGGL(minute_table_kernel<float>, dim3(cb, gy), dim3(256), 0, s, eng->dp, v, chain0,
+                               n_chains, step0, n_steps, fmh, pv.tab64, pv.events, pv.n_events, sg);
     }
     }
     if (phases & PH_EXPAND) {
@@ -2787,8 +2783,8 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     }
     const MinuteCtx mc{eng->dp, chain0, step0, first_minute_host(utc0, step0), pv.events, 0, pv.tab64};
     if (sv.acc)
-        hipLaunchKernelGGL(partials_reduce_kernel, dim3((n_chains + RED_CH - 1) / RED_CH), dim3(RED_SEG * RED_CH), 0, s,
-                           n_chains, sg, sv, eng->dp.ids, eng->kp.ids ? eng->kp.ids_n : 0u);
+        hipLaunchKernelGGL(stats_commit_kernel, dim3(cb), dim3(256), 0, s, n_chains, sg, sv, eng->dp.ids,
+                           eng->kp.ids ? eng->kp.ids_n : 0u);
     if (f64)
         hipLaunchKernelGGL(commit_kernel<double>, dim3(cb), dim3(256), 0, s, v, n_chains, sg, sv, mc, pv.n_events,
                            pv.desc + nblk_of(n_steps), eng->dp.markov, eng->kp.ids ? eng->kp.ids_n : 0u);
