@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 TAG=${1:-c} BASE=${2:-nskip}
-[ -x scripts/micro/isa_rate ] && timeout -k 10 120 scripts/micro/isa_rate > gpurun_out/isa_rate.txt 2>&1; cat gpurun_out/isa_rate.txt
+if [ -x scripts/micro/isa_rate ]; then timeout -k 10 120 scripts/micro/isa_rate > gpurun_out/isa_rate_$TAG.txt 2>&1 || exit $?; cat gpurun_out/isa_rate_$TAG.txt; fi
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider -rf --timeout 400 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_$TAG.log
 [ $rc -eq 0 ] || exit $rc

@@ -43,7 +43,9 @@ __global__ __launch_bounds__(256) void kop(uint32_t* out, int iters, uint64_t* c
         if constexpr (OP == 18) asm volatile("v_max_f32 %0, %0, %1" : "+v"(a##j) : "v"(k));                   \
         if constexpr (OP == 19) asm volatile("v_med3_f32 %0, %0, %1, %1" : "+v"(a##j) : "v"(k));               \
         if constexpr (OP == 20) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a##j) : "v"(k));                    \
-        if constexpr (OP == 21) asm volatile("v_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(a##j));
+        if constexpr (OP == 21) asm volatile("v_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(a##j)); \
+        if constexpr (OP == 22) asm volatile("v_cmp_lt_u32_e32 vcc, %0, %1\n\tv_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(a##j) : "v"(k) : "vcc"); \
+        if constexpr (OP == 23) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(a##j) : "v"(t), "v"(k));
         REP8(STEP)
 #undef STEP
     }
@@ -71,7 +73,8 @@ int main()
     const char* names[] = {"v_fma_f32", "v_pk_fma_f32", "v_mad_u64_u32", "v_mul_hi_u32", "v_mul_lo_u32", "v_fma_f64",
                            "v_add_f64", "v_log_f32", "v_exp_f32", "v_rcp_f32", "v_bitop3_b32", "v_cndmask_b32",
                            "v_cvt_f32_u32", "v_mul_f64", "v_rcp_f64", "v_sqrt_f32", "v_cndmask_e64 s[]",
-                           "v_cmp+v_cndmask", "v_max_f32", "v_med3_f32", "v_add_u32", "v_mov_b32_dpp"};
+                           "v_cmp+v_cndmask", "v_max_f32", "v_med3_f32", "v_add_u32", "v_mov_b32_dpp",
+                           "v_cmp_e32+cndmask_e32", "v_fma_f32 distinct"};
     auto run = [&](int op, auto launch) {
         launch();
         hipDeviceSynchronize();
@@ -92,6 +95,6 @@ int main()
     };
 #define RUN(op) run(op, [&] { kop<op><<<blocks, threads>>>(o, iters, ck); });
     RUN(0) RUN(1) RUN(2) RUN(3) RUN(4) RUN(5) RUN(6) RUN(7) RUN(8) RUN(9) RUN(10) RUN(11) RUN(12) RUN(13) RUN(14) RUN(15)
-    RUN(16) RUN(17) RUN(18) RUN(19) RUN(20) RUN(21)
+    RUN(16) RUN(17) RUN(18) RUN(19) RUN(20) RUN(21) RUN(22) RUN(23)
     return 0;
 }
