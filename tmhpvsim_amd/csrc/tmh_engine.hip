@@ -1548,28 +1548,40 @@ __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t rs, uint32_t of
 // sampler pairs and does no fp64 work in fp32 mode.
 // 256-thread workgroups: one-wave workgroups (so the SIMDs take expansion waves
 // independently of a walk wave's footprint) measured +5 % alone, no gain beside the walks
+#ifndef TMH_STATS_CPL
+#define TMH_STATS_CPL 2
+#endif
+#ifndef TMH_SITES_WAVES
+#define TMH_SITES_WAVES 2
+#endif
+#ifndef TMH_STATS_WAVES
+#define TMH_STATS_WAVES 4
+#endif
+// chains per lane of an expansion instantiation: two in the fp32 single-site trace and
+// statistics kernels (packed fp32), one elsewhere
+template <typename R, int OUT, bool SITES>
+constexpr int exp_cpl()
+{
+    return (sizeof(R) == 4 && !SITES && (OUT == OUT_TRACE3 || (OUT == OUT_STATS && TMH_STATS_CPL == 2))) ? 2 : 1;
+}
+// threads per expansion workgroup: 256; 128 for two chains per lane with the LDS
+// histogram (its 16-bit bins count at most 128 x 2 x 128 = 32,768 chain-seconds)
 template <typename R, int OUT, bool SITES>
 constexpr int exp_wg()
 {
-    return 256;
+    return (OUT != OUT_TRACE3 && exp_cpl<R, OUT, SITES>() == 2) ? 128 : 256;
 }
 constexpr int PVF_VGPR = 8;   // leading PVF fields pinned in VGPRs in the fp32 single-site expansion
 // min waves per SIMD (__launch_bounds__) of each expansion instantiation:
-//  fp32 single-site trace (C2): 7 = at most 72 VGPRs (alone -4 % vs 6, no VGPR spills);
-//  fp32 statistics / other outputs (C3, C4): 6 = 80 VGPRs (the 16-bit-pair LDS histogram,
-//    8 KB, + 12 KB staging: 8 workgroups per CU; +6 % over 5 waves);
+//  fp32 single-site, two chains per lane (C2 trace, C3 / C4 statistics): 4 = 128 VGPRs
+//    (one chain per lane: trace 7, statistics 6);
+//  fp32 other outputs: 6 = 80 VGPRs;
 //  fp64 single-site: 4 = 128 VGPRs, 4-8 spilled (fp64 C2 6.2 -> 6.5e10, same box);
 //  per-chain sites (C5): 2 (a few spills) is 35 % faster than 1
 template <typename R, int OUT, bool SITES>
 constexpr int exp_waves()
 {
-    return SITES ? 2 : (sizeof(R) == 8 ? 4 : (OUT == OUT_TRACE3 ? 4 : 6));
-}
-// chains per lane of an expansion instantiation (exp_cpl): one
-template <typename R, int OUT, bool SITES>
-constexpr int exp_cpl()
-{
-    return (sizeof(R) == 4 && !SITES && OUT == OUT_TRACE3) ? 2 : 1;
+    return SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 4 : (exp_cpl<R, OUT, SITES>() == 2 ? (OUT == OUT_STATS ? TMH_STATS_WAVES : 4) : 6));
 }
 template <typename R, int OUT, bool SITES>
 __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0,

@@ -131,6 +131,11 @@ __device__ __forceinline__ float vsel(bool m, float a, float b) { return m ? a :
 __device__ __forceinline__ f2 vsel(i2 m, f2 a, f2 b) { return m ? a : b; }
 __device__ __forceinline__ f2 vsel(i2 m, f2 a, float b) { return m ? a : (f2)(b); }
 __device__ __forceinline__ f2 vsel(i2 m, float a, f2 b) { return m ? (f2)(a) : b; }
+// a scalar condition as a mask of T's width: a mask element is all ones or all zeros
+// (a bare bool would enter f2 masks as 1, whose sign bit is clear)
+template <typename T> __device__ __forceinline__ typename VecOf<T>::M vmask(bool b);
+template <> __device__ __forceinline__ bool vmask<float>(bool b) { return b; }
+template <> __device__ __forceinline__ i2 vmask<f2>(bool b) { return (i2)(b ? -1 : 0); }
 __device__ __forceinline__ bool vany(bool m) { return m; }
 __device__ __forceinline__ bool vany(i2 m) { return (m.x | m.y) != 0; }
 __device__ __forceinline__ float vcvt(uint32_t a) { return (float)a; }

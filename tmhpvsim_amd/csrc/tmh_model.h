@@ -1181,7 +1181,7 @@ __device__ __forceinline__ T pv_power_f(const PVF& k, const float* g, T csi, typ
     // exp(cc am) = exp2(cc * (am log2 e)): the fp32 row holds am log2 e (one rounding)
     const T dkn = vfma(b, vexp2(cc * g[G_AM]), a);
     T dni = (g[G_KNC] - dkn) * g[G_I0];
-    dni = vsel((g[G_DISCOK] != 0.0f) & (ghi >= 0.0f) & (dni >= 0.0f), dni, 0.0f);
+    dni = vsel(vmask<T>(g[G_DISCOK] != 0.0f) & (ghi >= 0.0f) & (dni >= 0.0f), dni, 0.0f);
     const T dhi = vfma(-dni, g[G_COSZ], ghi);
     const T AI = dni * g[G_DNIEXTRA];
     const T sky = vmax(dhi * vfma(AI, g[G_RB], (1.0f - AI) * g[G_TERM2]), 0.0f);
