@@ -14,6 +14,6 @@ for e in "$@"; do
   sed -i "$e" "$d"/csrc/tmh_engine.hip "$d"/csrc/tmh_model.h "$d"/csrc/tmh_math.h
   [ "$before" != "$(cat "$d"/csrc/* | md5sum)" ] || { echo "no change: $e" >&2; exit 1; }
 done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -I "$d/include" \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off ${EXTRA:-} -I "$d/include" \
   -o "tmhpvsim_amd/libtmh_$name.so" "$d/csrc/tmh_engine.hip"
 rm -rf "$d"

@@ -62,7 +62,19 @@ __global__ __launch_bounds__(256) void kop(uint32_t* out, int iters, uint64_t* c
         if constexpr (OP == 33) asm volatile("v_fma_f32 %0, %2, %3, %0\n\tv_fma_f32 %1, %2, %3, %1" : "+v"(a##j), "+v"(b##j) : "v"(t), "v"(k)); \
         if constexpr (OP == 34) asm volatile("v_fma_f32 %0, %2, %3, %0\n\tv_pk_fma_f32 %1, %4, %5, %1" : "+v"(a##j), "+v"(d##j) : "v"(t), "v"(k), "v"(dx), "v"(dy)); \
         if constexpr (OP == 35) asm volatile("v_fma_f32 %0, %2, %3, %0\n\tv_exp_f32 %1, %1" : "+v"(a##j), "+v"(b##j) : "v"(t), "v"(k)); \
-        if constexpr (OP == 36) asm volatile("v_cndmask_b32_e64 %0, %1, %0, %2" : "+v"(a##j) : "v"(t), "s"(msk));
+        if constexpr (OP == 36) asm volatile("v_cndmask_b32_e64 %0, %1, %0, %2" : "+v"(a##j) : "v"(t), "s"(msk)); \
+        if constexpr (OP == 37) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(d##j) : "v"(a##j), "v"(t) : "vcc"); \
+        if constexpr (OP == 38) asm volatile("v_mul_hi_u32 %0, %1, %0" : "+v"(a##j) : "v"(t)); \
+        if constexpr (OP == 39) asm volatile("v_cndmask_b32_e32 %0, %1, %0, vcc" : "+v"(a##j) : "v"(t)); \
+        if constexpr (OP == 40) asm volatile("v_max_f32 %0, %1, %0" : "+v"(a##j) : "v"(t)); \
+        if constexpr (OP == 41) asm volatile("v_bitop3_b32 %0, %1, %2, %0 bitop3:0x96" : "+v"(a##j) : "v"(t), "v"(k)); \
+        if constexpr (OP == 42) asm volatile("v_pk_mul_f32 %0, %1, %0" : "+v"(d##j) : "v"(dx)); \
+        if constexpr (OP == 43) asm volatile("v_fmaak_f32 %0, %1, %0, 0x3f800000" : "+v"(a##j) : "v"(t)); \
+        if constexpr (OP == 44) asm volatile("v_cmp_lt_f32_e32 vcc, %0, %1" : : "v"(a##j), "v"(t) : "vcc"); \
+        if constexpr (OP == 45) asm volatile("v_cvt_f32_u32 %0, %1" : "=v"(a##j) : "v"(b##j)); \
+        if constexpr (OP == 46) asm volatile("v_add_f64 %0, %1, %0" : "+v"(d##j) : "v"(dx)); \
+        if constexpr (OP == 47) asm volatile("v_med3_f32 %0, %1, %2, %0" : "+v"(a##j) : "v"(t), "v"(k)); \
+        if constexpr (OP == 48) asm volatile("v_mov_b32 %0, %1" : "=v"(a##j) : "v"(b##j));
         REP8(STEP)
 #undef STEP
     }
@@ -96,7 +108,10 @@ int main()
                            "fma+exp (pair)", "fma+add_u32 (pair)", "fma+s_add (pair)", "fma+pk_fma (pair)",
                            "fma+fma (pair)", "v_pk_fma_f32 distinct", "v_fma_f64 distinct", "v_add_u32 distinct",
                            "v_mul_f32 distinct", "fma+fma distinct (pair)", "fma+pk_fma distinct (pair)",
-                           "fma+exp distinct (pair)", "v_cndmask_e64 distinct"};
+                           "fma+exp distinct (pair)", "v_cndmask_e64 distinct", "v_mad_u64_u32 distinct",
+                           "v_mul_hi_u32 distinct", "v_cndmask_e32 vcc distinct", "v_max_f32 distinct",
+                           "v_bitop3 distinct", "v_pk_mul_f32 distinct", "v_fmaak_f32 literal", "v_cmp_lt_f32_e32",
+                           "v_cvt_f32_u32 distinct", "v_add_f64 distinct", "v_med3_f32 distinct", "v_mov_b32"};
     auto run = [&](int op, auto launch) {
         launch();
         hipDeviceSynchronize();
@@ -117,6 +132,6 @@ int main()
     };
 #define RUN(op) run(op, [&] { kop<op><<<blocks, threads>>>(o, iters, ck); });
     RUN(0) RUN(1) RUN(2) RUN(3) RUN(4) RUN(5) RUN(6) RUN(7) RUN(8) RUN(9) RUN(10) RUN(11) RUN(12) RUN(13) RUN(14) RUN(15)
-    RUN(16) RUN(17) RUN(18) RUN(19) RUN(20) RUN(21) RUN(22) RUN(23) RUN(24) RUN(25) RUN(26) RUN(27) RUN(28) RUN(29) RUN(30) RUN(31) RUN(32) RUN(33) RUN(34) RUN(35) RUN(36)
+    RUN(16) RUN(17) RUN(18) RUN(19) RUN(20) RUN(21) RUN(22) RUN(23) RUN(24) RUN(25) RUN(26) RUN(27) RUN(28) RUN(29) RUN(30) RUN(31) RUN(32) RUN(33) RUN(34) RUN(35) RUN(36) RUN(37) RUN(38) RUN(39) RUN(40) RUN(41) RUN(42) RUN(43) RUN(44) RUN(45) RUN(46) RUN(47) RUN(48)
     return 0;
 }

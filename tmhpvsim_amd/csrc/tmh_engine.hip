@@ -1548,40 +1548,22 @@ __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t rs, uint32_t of
 // sampler pairs and does no fp64 work in fp32 mode.
 // 256-thread workgroups: one-wave workgroups (so the SIMDs take expansion waves
 // independently of a walk wave's footprint) measured +5 % alone, no gain beside the walks
-#ifndef TMH_STATS_CPL
-#define TMH_STATS_CPL 2
-#endif
-#ifndef TMH_SITES_WAVES
-#define TMH_SITES_WAVES 2
-#endif
-#ifndef TMH_STATS_WAVES
-#define TMH_STATS_WAVES 4
-#endif
-// chains per lane of an expansion instantiation: two in the fp32 single-site trace and
-// statistics kernels (packed fp32), one elsewhere
-template <typename R, int OUT, bool SITES>
-constexpr int exp_cpl()
-{
-    return (sizeof(R) == 4 && !SITES && (OUT == OUT_TRACE3 || (OUT == OUT_STATS && TMH_STATS_CPL == 2))) ? 2 : 1;
-}
-// threads per expansion workgroup: 256; 128 for two chains per lane with the LDS
-// histogram (its 16-bit bins count at most 128 x 2 x 128 = 32,768 chain-seconds)
 template <typename R, int OUT, bool SITES>
 constexpr int exp_wg()
 {
-    return (OUT != OUT_TRACE3 && exp_cpl<R, OUT, SITES>() == 2) ? 128 : 256;
+    return 256;
 }
 constexpr int PVF_VGPR = 8;   // leading PVF fields pinned in VGPRs in the fp32 single-site expansion
 // min waves per SIMD (__launch_bounds__) of each expansion instantiation:
-//  fp32 single-site, two chains per lane (C2 trace, C3 / C4 statistics): 4 = 128 VGPRs
-//    (one chain per lane: trace 7, statistics 6);
-//  fp32 other outputs: 6 = 80 VGPRs;
+//  fp32 single-site trace (C2): 7 = at most 72 VGPRs (alone -4 % vs 6, no VGPR spills);
+//  fp32 statistics / other outputs (C3, C4): 6 = 80 VGPRs (the 16-bit-pair LDS histogram,
+//    8 KB, + 12 KB staging: 8 workgroups per CU; +6 % over 5 waves);
 //  fp64 single-site: 4 = 128 VGPRs, 4-8 spilled (fp64 C2 6.2 -> 6.5e10, same box);
 //  per-chain sites (C5): 2 (a few spills) is 35 % faster than 1
 template <typename R, int OUT, bool SITES>
 constexpr int exp_waves()
 {
-    return SITES ? TMH_SITES_WAVES : (sizeof(R) == 8 ? 4 : (exp_cpl<R, OUT, SITES>() == 2 ? (OUT == OUT_STATS ? TMH_STATS_WAVES : 4) : 6));
+    return SITES ? 2 : (sizeof(R) == 8 ? 4 : (OUT == OUT_TRACE3 ? 7 : 6));
 }
 template <typename R, int OUT, bool SITES>
 __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0,
@@ -1594,28 +1576,16 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
                                                      const BlockDesc* __restrict__ desc, SegView sg, TraceView tr,
                                                      StatsView sv)
 {
-    // CPL chains per lane: lane t of chain block y runs chains y 256 CPL + q 256 + t, q < CPL,
-    // through the same seconds (one geometry row, one clock), so their arithmetic pairs
-    // up in packed fp32 instructions
-    constexpr int CPL = exp_cpl<R, OUT, SITES>();
-    constexpr int WGT = exp_wg<R, OUT, SITES>();   // threads per workgroup
     extern __shared__ uint32_t lds_hist[];
-    const uint32_t b = blockIdx.x;                 // grid: x = time block, y = chain block
-    uint32_t c[CPL];
-    bool live[CPL];
-#pragma unroll
-    for (int q = 0; q < CPL; ++q) {
-        c[q] = blockIdx.y * (WGT * CPL) + q * WGT + threadIdx.x;
-        live[q] = c[q] < n;
-    }
+    const uint32_t c = blockIdx.y * blockDim.x + threadIdx.x;   // grid: x = time block, y = chain block
+    const uint32_t b = blockIdx.x;
+    const bool live = c < n;
     if (sv.hist) {
         for (uint32_t i = threadIdx.x; i < (sv.n_bins + 1) / 2; i += blockDim.x) lds_hist[i] = 0;   // 16-bit bin pairs
         __syncthreads();
     }
     const uint32_t j0 = b * BLOCK_STEPS, j1 = min(j0 + (uint32_t)BLOCK_STEPS, nsteps);
-    uint64_t chain[CPL];
-#pragma unroll
-    for (int q = 0; q < CPL; ++q) chain[q] = chain0 + gid(kp.ids, c[q]);
+    const uint64_t chain = chain0 + gid(kp.ids, c);
     const int64_t fm = first_minute(utc0, W0);
     // the fp32 PV constants as per-lane registers (VGPRs): held in SGPRs across
     // the loop they are spilled to VGPR lanes and read back by v_readlane each step
@@ -1625,68 +1595,58 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
 #pragma unroll
         for (int i = 0; i < PVF_VGPR; ++i) asm volatile("v_mov_b32 %0, %1" : "=v"(f[i]) : "s"(f[i]));
     }
-    Acc acc[CPL];
-    bool alive[CPL];
-    int32_t fault[CPL];
-    uint32_t jr[CPL];
-    FSamp<R> fs[CPL];
-    uint32_t evi = 0;   // the block's first event (chain-independent)
-    LaneSite ls{};      // per-chain sites (C5, one chain per lane): this chain's site constants
+    Acc acc{0.0, 0.0, 0.0, -INFINITY};
+    bool alive = false;
+    int32_t fault = INT_MAX;
+    uint32_t jr = 0, evi = 0;
+    FSamp<R> fs;
+    const MinuteCtx mc{dp, chain, W0, fm, events, (int)min(*n_events, ev_cap_dev(nsteps)), tab64};
+    LaneSite ls{};   // per-chain sites (C5): this chain's site constants
     bool blk_night = false;
     if constexpr (SITES) {
         static_assert(BLOCK_STEPS <= 128, "site_block_night's bound assumes blocks of <= 128 s");
-        static_assert(CPL == 1, "per-chain sites: one chain per lane");
-        ls.k = site_k(kp.sites + (size_t)(live[0] ? gid(kp.ids, c[0]) : 0) * 8);
-        ls.linke = kp.site_linke ? kp.site_linke + (size_t)(live[0] ? gid(kp.ids, c[0]) : 0) * 12 : nullptr;
+        ls.k = site_k(kp.sites + (size_t)(live ? gid(kp.ids, c) : 0) * 8);
+        ls.linke = kp.site_linke ? kp.site_linke + (size_t)(live ? gid(kp.ids, c) : 0) * 12 : nullptr;
         ls.tl_doy = -1;
         blk_night = site_block_night(ls.k, sun + (size_t)(b * BLOCK_STEPS) * SUN_W);
     }
-    const BlockDesc d = desc[b];
-    evi = (uint32_t)d.evi;
+    if (live) {
+        alive = st.status[c] == 0;
+        fault = sg.fault[c];
+        Samp s;
 #pragma unroll
-    for (int q = 0; q < CPL; ++q) {
-        acc[q] = Acc{0.0, 0.0, 0.0, -INFINITY};
-        alive[q] = false;
-        fault[q] = INT_MAX;
-        jr[q] = 0;
-        if (live[q]) {
-            const MinuteCtx mc{dp, chain[q], W0, fm, events, (int)min(*n_events, ev_cap_dev(nsteps)), tab64};
-            alive[q] = st.status[c[q]] == 0;
-            fault[q] = sg.fault[c[q]];
-            Samp s;
-#pragma unroll
-            for (int k = 0; k < 6; ++k) {
-                s.b[k] = st.sb[k][c[q]];
-                s.a[k] = st.sa[k][c[q]];
-            }
-            if constexpr (sizeof(R) == 4) load_fast_noise(st, c[q], s);
-            if (alive[q] && b > 0) samplers_at<R>(d, sg, n, c[q], s, mc, st);
-            to_real(fs[q], s);
+        for (int k = 0; k < 6; ++k) {
+            s.b[k] = st.sb[k][c];
+            s.a[k] = st.sa[k][c];
         }
+        if constexpr (sizeof(R) == 4) load_fast_noise(st, c, s);
+        const BlockDesc d = desc[b];
+        evi = (uint32_t)d.evi;
+        if (alive && b > 0) samplers_at<R>(d, sg, n, c, s, mc, st);
+        to_real(fs, s);
     }
     // The block's covered bits and its minute draws staged in LDS before the loop:
     // the per-second loop then issues no vector loads, so no s_waitcnt vmcnt in it
     // waits behind the trace stores (gfx9's vmcnt counts loads and stores alike;
     // per-second record loads cost 42 % of the waves' cycles in such waits, PMC
     // SQ_WAIT_ANY).  Word-major: lane-consecutive dwords, no bank conflicts.
-    __shared__ uint32_t cov_lds[4][WGT * CPL];
-    __shared__ R min_lds[4][WGT * CPL];   // minute boundaries mA, mA + 1 of the block: cloudy, clear noise
+    constexpr int WGT = exp_wg<R, OUT, SITES>();   // threads per workgroup
+    __shared__ uint32_t cov_lds[4][WGT];
+    __shared__ R min_lds[4][WGT];   // minute boundaries mA, mA + 1 of the block: cloudy, clear noise
     const int32_t s0i = (int32_t)(W0 + j0), s1i = (int32_t)(W0 + j1);
     const int32_t mA = (int32_t)j0 <= (int32_t)fm ? 0 : ((int32_t)j0 - (int32_t)fm + 59) / 60;
-#pragma unroll
-    for (int q = 0; q < CPL; ++q) {
-        const uint32_t li = q * WGT + threadIdx.x;   // the chain's LDS column
+    {
         uint32_t cw[4] = {0u, 0u, 0u, 0u};
-        if (alive[q]) {   // segment containing the block start: first record with next-call step > start
-            int lo = 0, hi = (int)sg.count[c[q]] - 1;
+        if (alive) {   // segment containing the block start: first record with next-call step > start
+            int lo = 0, hi = (int)sg.count[c] - 1;
             const int last = hi;
             while (lo < hi) {
                 const int mid = (lo + hi) >> 1;
-                if (rec_at(sg, c[q], mid).y > s0i) hi = mid;
+                if (rec_at(sg, c, mid).y > s0i) hi = mid;
                 else lo = mid + 1;
             }
             // covered iff step < x of the segment holding it: [start, min(x, y)) per segment
-            int2 r = rec_at(sg, c[q], lo);
+            int2 r = rec_at(sg, c, lo);
             int32_t a = s0i;
             for (;;) {
                 const int32_t e = min(min(r.x, r.y), s1i);
@@ -1699,59 +1659,35 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
                 }
                 if (r.y >= s1i || lo >= last) break;
                 a = max(a, r.y);
-                r = rec_at(sg, c[q], ++lo);
+                r = rec_at(sg, c, ++lo);
             }
-            jr[q] = (uint32_t)lo;   // the segment of the block's last step (fixup_kernel walks back from it)
+            jr = (uint32_t)lo;   // the segment of the block's last step (fixup_kernel walks back from it)
         }
 #pragma unroll
-        for (int w = 0; w < 4; ++w) cov_lds[w][li] = cw[w];
+        for (int w = 0; w < 4; ++w) cov_lds[w][threadIdx.x] = cw[w];
         const R* mt = reinterpret_cast<const R*>(sg.mtab);
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const int32_t m = mA + k;
-            const bool in = live[q] && (int32_t)fm + 60 * m < (int32_t)j1;
-            min_lds[2 * k][li] = in ? mt[(size_t)(2 * m) * n + c[q]] : R(0);
-            min_lds[2 * k + 1][li] = in ? mt[(size_t)(2 * m + 1) * n + c[q]] : R(0);
+            const bool in = live && (int32_t)fm + 60 * m < (int32_t)j1;
+            min_lds[2 * k][threadIdx.x] = in ? mt[(size_t)(2 * m) * n + c] : R(0);
+            min_lds[2 * k + 1][threadIdx.x] = in ? mt[(size_t)(2 * m + 1) * n + c] : R(0);
         }
     }
-    uint32_t cov_w[CPL];
-#pragma unroll
-    for (int q = 0; q < CPL; ++q) cov_w[q] = 0;
-    // two chains per lane: the samplers as packed pairs (element q = chain q)
-    FSamp<f2> fv;
-    if constexpr (CPL == 2) {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            fv.b[k] = f2{(float)fs[0].b[k], (float)fs[CPL - 1].b[k]};
-            fv.a[k] = f2{(float)fs[0].a[k], (float)fs[CPL - 1].a[k]};
-        }
-    }
-    // sampler k of chain q (the pair's element q when packed)
-    auto samp_push = [&](int q, int k, R v) __attribute__((always_inline)) {
-        if constexpr (CPL == 2) {
-            fv.b[k][q] = fv.a[k][q];
-            fv.a[k][q] = (float)v;
-        } else {
-            fs[q].b[k] = fs[q].a[k];
-            fs[q].a[k] = v;
-        }
-    };
-    // the guard-band seconds of the lane's blocks, a bit each, in LDS: no register carried through the loop
-    __shared__ uint4 held_lds[WGT * CPL];
-#pragma unroll
-    for (int q = 0; q < CPL; ++q) held_lds[q * WGT + threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t cov_w = 0;
+    const double* evd = sg.evd + c;
+    // the guard-band seconds of the lane's block, a bit each, in LDS: no register carried through the loop
+    __shared__ uint4 held_lds[WGT];
+    held_lds[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
     // Trace stores: one buffer resource per output for the block's rows (built here,
-    // not per store) and one running per-lane byte offset (chain q of the lane: + q 256
-    // elements); lanes past the last chain start at 2^31, out of the resource's range,
-    // so the stores need no exec mask.  (The host keeps a block's rows under 2 GiB:
-    // tmh_expand checks the trace's ld.)
+    // not per store) and one running per-lane byte offset; lanes past the last chain
+    // start at 2^31, out of the resource's range, so the stores need no exec mask.
+    // (The host keeps a block's rows under 2 GiB: tmh_expand checks the trace's ld.)
     constexpr int RW = sizeof(R) == 8 ? ROW : ROW32;   // geometry row: wave-uniform, scalar loads
     const R* rowp = (sizeof(R) == 8 ? reinterpret_cast<const R*>(tab64) : reinterpret_cast<const R*>(tab32)) +
                     (size_t)j0 * RW;
     __amdgpu_buffer_rsrc_t rs_pv, rs_m, rs_r;
-    uint32_t voff[CPL];
-#pragma unroll
-    for (int q = 0; q < CPL; ++q) voff[q] = live[q] ? c[q] * (uint32_t)sizeof(R) : 0x80000000u;
+    uint32_t voff = live ? c * (uint32_t)sizeof(R) : 0x80000000u;
     const uint32_t rowb = (uint32_t)(tr.ld * sizeof(R));
     if constexpr (OUT == OUT_TRACE3) {
         const size_t bo = (size_t)j0 * tr.ld * sizeof(R);
@@ -1760,38 +1696,32 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
         rs_m = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(tr.meter) + bo, 0, nb, 0x00020000);
         rs_r = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(tr.residual) + bo, 0, nb, 0x00020000);
     }
-    int32_t fault_eff[CPL];   // ok = j < fault_eff: one compare, no branch
-    bool any_fault = false;
-#pragma unroll
-    for (int q = 0; q < CPL; ++q) {
-        fault_eff[q] = alive[q] ? fault[q] : 0;
-        any_fault = any_fault || (live[q] && fault_eff[q] < (int32_t)j1);
-    }
-    const double* evd[CPL];
-#pragma unroll
-    for (int q = 0; q < CPL; ++q) evd[q] = sg.evd + c[q];
+    const int32_t fault_eff = alive ? fault : 0;   // ok = j < fault_eff: one compare, no branch
     // One second.  Every lane computes it; a lane whose chain is faulted (or not
-    // alive) emits NaN / no statistics.  un, um: the step's Philox words (noise, meter)
-    // of each chain.  wave_ok: no chain of the wave has a fault before the block's end
-    // (the common case), so a scalar branch skips the per-second NaN selects.  Lanes past
-    // the last chain store out of range (voff) and emit nothing: they never fault the wave.
-    const bool wave_ok = __builtin_amdgcn_ballot_w64(any_fault) == 0;
-    auto second = [&](uint32_t j, const uint32_t (&un)[CPL], const uint32_t (&um)[CPL]) __attribute__((always_inline)) {
+    // alive) emits NaN / no statistics.  un, um: the step's Philox words (noise, meter).
+    // wave_ok: no lane of the wave has a fault before the block's end (the common case),
+    // so a scalar branch skips the per-second NaN selects.
+    // lanes past the last chain store out of range (voff) and emit nothing: they never fault the wave
+    const bool wave_ok = __builtin_amdgcn_ballot_w64(live && fault_eff < (int32_t)j1) == 0;
+    auto second = [&](uint32_t j, uint32_t un, uint32_t um) __attribute__((always_inline)) {
         R row[row_w<R>()];
 #pragma unroll
         for (int i = 0; i < row_w<R>(); ++i) row[i] = rowp[i];
         rowp += RW;
         const uint32_t fl = sizeof(R) == 8 ? (uint32_t)(double)rowp[G_FLAGS - RW] : __float_as_uint(row[G_FLAGS + G32]);
+        const bool ok = wave_ok || (int32_t)j < fault_eff;
         if (fl & (FL_DAY | FL_HOUR)) {            // _next_day, _next_hour (rare: loads waited here)
             const size_t eo = (size_t)evi * 4 * n;
-#pragma unroll
-            for (int q = 0; q < CPL; ++q) {
-                if (live[q]) {
-                    if (fl & FL_DAY) samp_push(q, S_CLEAR_DAY, (R)evd[q][eo + 2 * (size_t)n]);
-                    if (fl & FL_HOUR) {
-                        samp_push(q, S_CC, (R)evd[q][eo]);
-                        samp_push(q, S_CLEAR_DAY, (R)evd[q][eo + 3 * (size_t)n]);
-                    }
+            if (live) {
+                if (fl & FL_DAY) {
+                    fs.b[S_CLEAR_DAY] = fs.a[S_CLEAR_DAY];
+                    fs.a[S_CLEAR_DAY] = (R)evd[eo + 2 * (size_t)n];
+                }
+                if (fl & FL_HOUR) {
+                    fs.b[S_CC] = fs.a[S_CC];
+                    fs.a[S_CC] = (R)evd[eo];
+                    fs.b[S_CLEAR_DAY] = fs.a[S_CLEAR_DAY];
+                    fs.a[S_CLEAR_DAY] = (R)evd[eo + 3 * (size_t)n];
                 }
             }
             __builtin_amdgcn_s_waitcnt(0);
@@ -1799,154 +1729,94 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
         }
         if (fl & FL_MIN) {                         // _next_min: staged minute draws
             const int32_t mi = ((int32_t)j - (int32_t)fm) / 60;
+            fs.b[S_CLOUDY_NOISE] = fs.a[S_CLOUDY_NOISE];
+            fs.b[S_CLEAR_NOISE] = fs.a[S_CLEAR_NOISE];
             const int32_t k = mi - mA;   // wave-uniform
             const int32_t kk = min(k, 1);
-#pragma unroll
-            for (int q = 0; q < CPL; ++q) {
-                const uint32_t li = q * WGT + threadIdx.x;
-                R ncl = min_lds[2 * kk][li], ncr = min_lds[2 * kk + 1][li];
-                if (k >= 2) {   // a third boundary in the block (its first within 8 s of the start): rare
-                    if (live[q]) {
-                        const R* mt = reinterpret_cast<const R*>(sg.mtab) + (size_t)(2 * mi) * n + c[q];
-                        ncl = mt[0];
-                        ncr = mt[n];
-                    }
-                    __builtin_amdgcn_s_waitcnt(0);   // wait here, not at the join every minute
+            R ncl = min_lds[2 * kk][threadIdx.x], ncr = min_lds[2 * kk + 1][threadIdx.x];
+            if (k >= 2) {   // a third boundary in the block (its first within 8 s of the start): rare
+                if (live) {
+                    const R* mt = reinterpret_cast<const R*>(sg.mtab) + (size_t)(2 * mi) * n + c;
+                    ncl = mt[0];
+                    ncr = mt[n];
                 }
-                samp_push(q, S_CLOUDY_NOISE, ncl);
-                samp_push(q, S_CLEAR_NOISE, ncr);
+                __builtin_amdgcn_s_waitcnt(0);   // wait here, not at the join every minute
             }
+            fs.a[S_CLOUDY_NOISE] = ncl;
+            fs.a[S_CLEAR_NOISE] = ncr;
         }
         const uint32_t jb = j - j0;   // wave-uniform
-        bool covered[CPL];
-#pragma unroll
-        for (int q = 0; q < CPL; ++q) {
-            if ((jb & 31) == 0) cov_w[q] = cov_lds[jb >> 5][q * WGT + threadIdx.x];
-            covered[q] = (cov_w[q] >> (jb & 31)) & 1u;
-        }
+        if ((jb & 31) == 0) cov_w = cov_lds[jb >> 5][threadIdx.x];
+        const bool covered = (cov_w >> (jb & 31)) & 1u;
         uint32_t flp = fl;
         if constexpr (SITES) {   // this chain's own site: geometry per chain-second (none in a night block)
             const bool night = blk_night || lane_row<R>(ls, sun + (size_t)j * SUN_W, kp.module, row);
             flp = night ? (fl | FL_NIGHT) : (fl & ~(uint32_t)FL_NIGHT);
         }
-        R csi[CPL], pv[CPL], meter[CPL], res[CPL];
-        bool held[CPL];
-        if constexpr (CPL == 2) {   // both chains in packed fp32 (second_body_f<f2>: the same bits as one by one)
-            const u2 wm = u2{um[0], um[CPL - 1]};
-            f2 vc, vp, vm, vr;
-            i2 risky = i2{0, 0};
-            if (OUT != OUT_ANY && (!kp.with_pv || (flp & FL_NIGHT))) {   // as below: pv = 0, no CSI
-                vc = f2{0.0f, 0.0f};
-                vp = f2{0.0f, 0.0f};
-                vm = meter_f<f2>(wm);
-                vr = vm - vp;
-            } else {
-                const i2 cov2 = i2{covered[0] ? -1 : 0, covered[CPL - 1] ? -1 : 0};
-                second_body_f<f2>(kp, pkv, row, flp, fv, cov2, ndtri_w<f2>(u2{un[0], un[CPL - 1]}), meter_f<f2>(wm), vc,
-                                  vp, vm, vr, risky);
-            }
-#pragma unroll
-            for (int q = 0; q < CPL; ++q) {
-                csi[q] = vc[q];
-                pv[q] = vp[q];
-                meter[q] = vm[q];
-                res[q] = vr[q];
-                held[q] = risky[q] != 0;
-            }
-        } else if (OUT != OUT_ANY && (!kp.with_pv || (flp & FL_NIGHT))) {
+        R csi, pv, meter, res;
+        bool held = false;   // fp32: PV in a guard band, recomputed in fp64 by fixup_kernel
+        if (OUT != OUT_ANY && (!kp.with_pv || (flp & FL_NIGHT))) {
             // the CSI is not an output (trace of pv / meter / residual, or statistics) and
             // pv = 0 whatever it is (second_body: night, or no PV): no noise quantile, no
             // samplers, no PV chain; the same values.  Wave-uniform for a single site.
-#pragma unroll
-            for (int q = 0; q < CPL; ++q) {
-                csi[q] = R(0);
-                pv[q] = R(0);
-                meter[q] = meter_w<R>(um[q]);
-                res[q] = meter[q] - pv[q];
-                held[q] = false;
-            }
+            csi = R(0);
+            pv = R(0);
+            meter = meter_w<R>(um);
+            res = meter - pv;
         } else {
-#pragma unroll
-            for (int q = 0; q < CPL; ++q) {
-                held[q] = false;   // fp32: PV in a guard band, recomputed in fp64 by fixup_kernel
-                second_body<R>(kp, pkv, row, flp, fs[q], covered[q], noise_z<R>(un[q]), meter_w<R>(um[q]), csi[q], pv[q],
-                               meter[q], res[q], held[q]);
+            second_body<R>(kp, pkv, row, flp, fs, covered, noise_z<R>(un), meter_w<R>(um), csi, pv, meter, res, held);
+        }
+        held = held && ok;
+        if constexpr (sizeof(R) == 4) {
+            if (held) {   // jb is wave-uniform: the word and the bit are scalars
+                uint32_t* hw = reinterpret_cast<uint32_t*>(&held_lds[threadIdx.x]) + (jb >> 5);
+                *hw |= 1u << (jb & 31);
             }
         }
-#pragma unroll
-        for (int q = 0; q < CPL; ++q) {
-            const bool ok = wave_ok || (int32_t)j < fault_eff[q];
-            held[q] = held[q] && ok;
-            if constexpr (sizeof(R) == 4) {
-                if (held[q]) {   // jb is wave-uniform: the word and the bit are scalars
-                    uint32_t* hw = reinterpret_cast<uint32_t*>(&held_lds[q * WGT + threadIdx.x]) + (jb >> 5);
-                    *hw |= 1u << (jb & 31);
-                }
-            }
-            if (!wave_ok) {
-                csi[q] = ok ? csi[q] : R(NAN);
-                pv[q] = ok ? pv[q] : R(NAN);
-                meter[q] = ok ? meter[q] : R(NAN);
-                res[q] = ok ? res[q] : R(NAN);
-            }
-            const uint8_t cov = ok ? (covered[q] ? 1 : 0) : 255;
-            if constexpr (OUT == OUT_TRACE3) {
-                row_store(rs_pv, voff[q], pv[q]);
-                row_store(rs_m, voff[q], meter[q]);
-                row_store(rs_r, voff[q], res[q]);
-                voff[q] += rowb;
-            } else if (live[q]) {
-                emit<R, OUT, true>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c[q], cov, csi[q], pv[q], meter[q], res[q],
-                                   acc[q], ok, held[q]);
-            }
+        if (!wave_ok) {
+            csi = ok ? csi : R(NAN);
+            pv = ok ? pv : R(NAN);
+            meter = ok ? meter : R(NAN);
+            res = ok ? res : R(NAN);
+        }
+        const uint8_t cov = ok ? (covered ? 1 : 0) : 255;
+        if constexpr (OUT == OUT_TRACE3) {
+            row_store(rs_pv, voff, pv);
+            row_store(rs_m, voff, meter);
+            row_store(rs_r, voff, res);
+            voff += rowb;
+        } else if (live) {
+            emit<R, OUT, true>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok, held);
         }
     };
-    // one Philox block per step pair and chain: (x, y) for the even step, (z, w) for the odd one
+    // one Philox block per step pair: (x, y) for the even step, (z, w) for the odd one
     if (((W0 + j0) & 1) == 0 && ((j1 - j0) & 1) == 0) {
         for (uint32_t j = j0; j < j1; j += 2) {
-            U4 pr[CPL];
-            uint32_t ua[CPL], ma[CPL], ub[CPL], mb[CPL];
-#pragma unroll
-            for (int q = 0; q < CPL; ++q) {
-                pr[q] = keyed_block(kp.seed, chain[q], (uint64_t)(W0 + j) >> 1, TAG_STEP2, 0);
-                ua[q] = pr[q].x;
-                ma[q] = pr[q].y;
-                ub[q] = pr[q].z;
-                mb[q] = pr[q].w;
-            }
-            second(j, ua, ma);
-            second(j + 1, ub, mb);
+            const U4 pr = keyed_block(kp.seed, chain, (uint64_t)(W0 + j) >> 1, TAG_STEP2, 0);
+            second(j, pr.x, pr.y);
+            second(j + 1, pr.z, pr.w);
         }
     } else {   // odd window start or length: one block per step (rare)
         for (uint32_t j = j0; j < j1; ++j) {
+            const U4 pr = keyed_block(kp.seed, chain, (uint64_t)(W0 + j) >> 1, TAG_STEP2, 0);
             const bool odd = (W0 + j) & 1;
-            uint32_t u[CPL], m[CPL];
-#pragma unroll
-            for (int q = 0; q < CPL; ++q) {
-                const U4 pr = keyed_block(kp.seed, chain[q], (uint64_t)(W0 + j) >> 1, TAG_STEP2, 0);
-                u[q] = odd ? pr.z : pr.x;
-                m[q] = odd ? pr.w : pr.y;
-            }
-            second(j, u, m);
+            second(j, odd ? pr.z : pr.x, odd ? pr.w : pr.y);
         }
     }
-#pragma unroll
-    for (int q = 0; q < CPL; ++q) {
-        if constexpr (sizeof(R) == 4) {
-            const uint4 hm = held_lds[q * WGT + threadIdx.x];
-            const bool held_any = (hm.x | hm.y | hm.z | hm.w) != 0;
-            if (held_any) {   // (chain, block, seconds) for fixup_kernel (outside the loop: no registers held across it)
-                const uint32_t k = atomicAdd(sg.nfix, 1u);
-                if (k < sg.fixcap) sg.fix[k] = FixRec{c[q], b, jr[q], 0u, hm};
-            }
+    if constexpr (sizeof(R) == 4) {
+        const uint4 hm = held_lds[threadIdx.x];
+        const bool held_any = (hm.x | hm.y | hm.z | hm.w) != 0;
+        if (held_any) {   // (chain, block, seconds) for fixup_kernel (outside the loop: no registers held across it)
+            const uint32_t k = atomicAdd(sg.nfix, 1u);
+            if (k < sg.fixcap) sg.fix[k] = FixRec{c, b, jr, 0u, hm};
         }
-        if (live[q] && sv.acc) {   // the block's sums into the chain's fixed-point window totals (order-free)
-            unsigned long long* fx = reinterpret_cast<unsigned long long*>(sg.acc_fx);
-            atomicAdd(fx + c[q], (unsigned long long)llrint(acc[q].pv * sg.fx_scale));
-            atomicAdd(fx + (size_t)n + c[q], (unsigned long long)llrint(acc[q].m * sg.fx_scale));
-            atomicAdd(fx + 2 * (size_t)n + c[q], (unsigned long long)llrint(acc[q].r * sg.fx_scale));
-            __hip_atomic_fetch_max(sg.acc_mx + c[q], max_key(acc[q].mx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+    }
+    if (live && sv.acc) {   // the block's sums into the chain's fixed-point window totals (order-free)
+        unsigned long long* fx = reinterpret_cast<unsigned long long*>(sg.acc_fx);
+        atomicAdd(fx + c, (unsigned long long)llrint(acc.pv * sg.fx_scale));
+        atomicAdd(fx + (size_t)n + c, (unsigned long long)llrint(acc.m * sg.fx_scale));
+        atomicAdd(fx + 2 * (size_t)n + c, (unsigned long long)llrint(acc.r * sg.fx_scale));
+        __hip_atomic_fetch_max(sg.acc_mx + c, max_key(acc.mx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (sv.hist) {
         __syncthreads();
@@ -2870,8 +2740,8 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     const int out = (no_stats && tv.pv && tv.meter && tv.residual && !tv.csi && !tv.covered) ? OUT_TRACE3
                     : (!tv.pv && !tv.meter && !tv.residual && !tv.csi && !tv.covered) ? OUT_STATS
                                                                                       : OUT_ANY;
-    auto exp_grid = [&](uint32_t wg, uint32_t cpl) {   // x = time block, y = chain block of wg x cpl chains
-        const uint32_t ecb = (n_chains + wg * cpl - 1) / (wg * cpl);
+    auto exp_grid = [&](uint32_t wg) {
+        const uint32_t ecb = (n_chains + wg - 1) / wg;
         return dim3(sg.nblk, ecb);
     };
     if (out == OUT_TRACE3 && tv.ld * (f64 ? 8u : 4u) * BLOCK_STEPS >= (1ull << 31))   // one block's rows: one buffer range
@@ -2879,7 +2749,7 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
                     (unsigned long long)tv.ld);
     const size_t lds_exp = stats && stats->hist ? (size_t)((stats->n_bins + 1) / 2) * 4 : 0;   // 16-bit bin pairs
 #define LAUNCH(R, O, S)                                                                                            \
-    hipLaunchKernelGGL((expand_kernel<R, O, S>), exp_grid(exp_wg<R, O, S>(), exp_cpl<R, O, S>()), dim3(exp_wg<R, O, S>()), lds_exp, s, eng->kp, eng->dp, v, chain0, n_chains,      \
+    hipLaunchKernelGGL((expand_kernel<R, O, S>), exp_grid(exp_wg<R, O, S>()), dim3(exp_wg<R, O, S>()), lds_exp, s, eng->kp, eng->dp, v, chain0, n_chains,      \
                        step0, n_steps, utc0, pv.tab64, pv.tab32, pv.sun, pv.events, pv.n_events, pv.desc, sg, tv, sv)
     if (eng->kp.sites) {   // per-chain sites: one instantiation per precision, any output
         if (f64) LAUNCH(double, OUT_ANY, true);

@@ -86,65 +86,6 @@ __device__ __forceinline__ U4 keyed_block(uint64_t seed, uint64_t chain, uint64_
                          (uint32_t)(chain >> 32), (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
-// --------------------------------------------------- scalar / packed-pair fp32
-// The fp32 per-second math is written once over T = float (one chain) or f2 (two chains
-// of a lane, the expansion's packed path): the same operations element by element, so
-// both forms give the same bits (IEEE fma / mul / add, no contraction), and f2's
-// fma / mul / add issue as v_pk_*_f32 (two chains per instruction).
-typedef float f2 __attribute__((ext_vector_type(2)));
-typedef int i2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-template <typename T> struct VecOf;
-template <> struct VecOf<float> { using M = bool; using U = uint32_t; using I = int32_t; };
-template <> struct VecOf<f2> { using M = i2; using U = u2; using I = i2; };
-
-__device__ __forceinline__ float vfma(float a, float b, float c) { return fmaf(a, b, c); }
-__device__ __forceinline__ f2 vfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ f2 vfma(f2 a, float b, float c) { return __builtin_elementwise_fma(a, (f2)(b), (f2)(c)); }
-__device__ __forceinline__ f2 vfma(f2 a, float b, f2 c) { return __builtin_elementwise_fma(a, (f2)(b), c); }
-__device__ __forceinline__ f2 vfma(float a, f2 b, f2 c) { return __builtin_elementwise_fma((f2)(a), b, c); }
-__device__ __forceinline__ f2 vfma(float a, f2 b, float c) { return __builtin_elementwise_fma((f2)(a), b, (f2)(c)); }
-__device__ __forceinline__ f2 vfma(f2 a, f2 b, float c) { return __builtin_elementwise_fma(a, b, (f2)(c)); }
-// per element (not packed on gfx950): min / max / med3, transcendentals, conversions
-__device__ __forceinline__ float vmin(float a, float b) { return fminf(a, b); }
-__device__ __forceinline__ f2 vmin(f2 a, float b) { return f2{fminf(a.x, b), fminf(a.y, b)}; }
-__device__ __forceinline__ float vmax(float a, float b) { return fmaxf(a, b); }
-__device__ __forceinline__ f2 vmax(f2 a, float b) { return f2{fmaxf(a.x, b), fmaxf(a.y, b)}; }
-__device__ __forceinline__ float vmed3(float a, float b, float c) { return __builtin_amdgcn_fmed3f(a, b, c); }
-__device__ __forceinline__ f2 vmed3(f2 a, float b, float c)
-{
-    return f2{__builtin_amdgcn_fmed3f(a.x, b, c), __builtin_amdgcn_fmed3f(a.y, b, c)};
-}
-__device__ __forceinline__ float vexp2(float a) { return __builtin_amdgcn_exp2f(a); }
-__device__ __forceinline__ f2 vexp2(f2 a) { return f2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)}; }
-__device__ __forceinline__ float vlog2(float a) { return __builtin_amdgcn_logf(a); }
-__device__ __forceinline__ f2 vlog2(f2 a) { return f2{__builtin_amdgcn_logf(a.x), __builtin_amdgcn_logf(a.y)}; }
-__device__ __forceinline__ float vrcp(float a) { return __builtin_amdgcn_rcpf(a); }
-__device__ __forceinline__ f2 vrcp(f2 a) { return f2{__builtin_amdgcn_rcpf(a.x), __builtin_amdgcn_rcpf(a.y)}; }
-__device__ __forceinline__ float vsqrt(float a) { return __builtin_amdgcn_sqrtf(a); }
-__device__ __forceinline__ f2 vsqrt(f2 a) { return f2{__builtin_amdgcn_sqrtf(a.x), __builtin_amdgcn_sqrtf(a.y)}; }
-__device__ __forceinline__ float vabs(float a) { return fabsf(a); }
-__device__ __forceinline__ f2 vabs(f2 a) { return f2{fabsf(a.x), fabsf(a.y)}; }
-__device__ __forceinline__ bool visnan(float a) { return isnan(a); }
-__device__ __forceinline__ i2 visnan(f2 a) { return a != a; }
-__device__ __forceinline__ float vsel(bool m, float a, float b) { return m ? a : b; }
-__device__ __forceinline__ f2 vsel(i2 m, f2 a, f2 b) { return m ? a : b; }
-__device__ __forceinline__ f2 vsel(i2 m, f2 a, float b) { return m ? a : (f2)(b); }
-__device__ __forceinline__ f2 vsel(i2 m, float a, f2 b) { return m ? (f2)(a) : b; }
-// a scalar condition as a mask of T's width: a mask element is all ones or all zeros
-// (a bare bool would enter f2 masks as 1, whose sign bit is clear)
-template <typename T> __device__ __forceinline__ typename VecOf<T>::M vmask(bool b);
-template <> __device__ __forceinline__ bool vmask<float>(bool b) { return b; }
-template <> __device__ __forceinline__ i2 vmask<f2>(bool b) { return (i2)(b ? -1 : 0); }
-__device__ __forceinline__ bool vany(bool m) { return m; }
-__device__ __forceinline__ bool vany(i2 m) { return (m.x | m.y) != 0; }
-__device__ __forceinline__ float vcvt(uint32_t a) { return (float)a; }
-__device__ __forceinline__ f2 vcvt(u2 a) { return f2{(float)a.x, (float)a.y}; }
-__device__ __forceinline__ float vcvt_i(uint32_t a) { return (float)(int32_t)a; }
-__device__ __forceinline__ f2 vcvt_i(u2 a) { return f2{(float)(int32_t)a.x, (float)(int32_t)a.y}; }
-__device__ __forceinline__ uint32_t vumin(uint32_t a, uint32_t b) { return a < b ? a : b; }
-__device__ __forceinline__ u2 vumin(u2 a, u2 b) { return u2{a.x < b.x ? a.x : b.x, a.y < b.y ? a.y : b.y}; }
-
 // ------------------------------------------------------------- variates
 // standard normal quantile (fp64).  ocml's ncdfinv, polished by one Halley
 // step on the erfc/erf residual so the result is within ~1 ulp of the exact
@@ -170,18 +111,18 @@ __device__ __noinline__ double ndtri_fast(double p) { return normcdfinv(p); }
 // Giles' single-precision erfinv ("Approximating the erfinv function", GPU
 // Computing Gems, 2011) as p(w), w = -log((1 - x)(1 + x)), erfinv(x) = p x:
 // central polynomial in w - 2.5 for w < 5 (99.66 % of draws) ...
-template <typename T>
-__device__ __forceinline__ T erfinv_central(T w0)
+__device__ __forceinline__ float erfinv_central(float w0)
 {
-    const T v = w0 - 2.5f;
-    T p = vfma(v, 2.81022636e-08f, 3.43273939e-07f);
-    p = vfma(p, v, -3.5233877e-06f);
-    p = vfma(p, v, -4.39150654e-06f);
-    p = vfma(p, v, 0.00021858087f);
-    p = vfma(p, v, -0.00125372503f);
-    p = vfma(p, v, -0.00417768164f);
-    p = vfma(p, v, 0.246640727f);
-    return vfma(p, v, 1.50140941f);
+    const float v = w0 - 2.5f;
+    float p = 2.81022636e-08f;
+    p = fmaf(p, v, 3.43273939e-07f);
+    p = fmaf(p, v, -3.5233877e-06f);
+    p = fmaf(p, v, -4.39150654e-06f);
+    p = fmaf(p, v, 0.00021858087f);
+    p = fmaf(p, v, -0.00125372503f);
+    p = fmaf(p, v, -0.00417768164f);
+    p = fmaf(p, v, 0.246640727f);
+    return fmaf(p, v, 1.50140941f);
 }
 
 // ... his tail polynomial in sqrt(w) - 3 for 5 <= w < 16, and for 16 <= w <= 21.5
@@ -189,26 +130,27 @@ __device__ __forceinline__ T erfinv_central(T w0)
 // fitted here (scripts/fit_ndtri_tail.py: 1.7e-7 relative; Giles' tail is 4e-4 off
 // there).  Straight-line code: no nested branch (the library quantile's nest of
 // exec-mask branches cost the per-second loop ~20 scalar instructions a step).
-template <typename T>
-__device__ __forceinline__ T erfinv_tail(T w0)
+__device__ __forceinline__ float erfinv_tail(float w0)
 {
-    const T s = vsqrt(w0);
-    const T v = s - 3.0f;
-    T p = vfma(v, -0.000200214257f, 0.000100950558f);
-    p = vfma(p, v, 0.00134934322f);
-    p = vfma(p, v, -0.00367342844f);
-    p = vfma(p, v, 0.00573950773f);
-    p = vfma(p, v, -0.0076224613f);
-    p = vfma(p, v, 0.00943887047f);
-    p = vfma(p, v, 1.00167406f);
-    p = vfma(p, v, 2.83297682f);
-    const T e = s - 4.3f;
-    T q = vfma(e, -5.854465416632593e-05f, 0.00019957200856879354f);
-    q = vfma(q, e, -0.000567059323657304f);
-    q = vfma(q, e, 0.000624575128313154f);
-    q = vfma(q, e, 1.010045051574707f);
-    q = vfma(q, e, 4.14272403717041f);
-    return vsel(w0 < 16.0f, p, q);
+    const float s = __builtin_amdgcn_sqrtf(w0);
+    const float v = s - 3.0f;
+    float p = -0.000200214257f;
+    p = fmaf(p, v, 0.000100950558f);
+    p = fmaf(p, v, 0.00134934322f);
+    p = fmaf(p, v, -0.00367342844f);
+    p = fmaf(p, v, 0.00573950773f);
+    p = fmaf(p, v, -0.0076224613f);
+    p = fmaf(p, v, 0.00943887047f);
+    p = fmaf(p, v, 1.00167406f);
+    p = fmaf(p, v, 2.83297682f);
+    const float e = s - 4.3f;
+    float q = -5.854465416632593e-05f;
+    q = fmaf(q, e, 0.00019957200856879354f);
+    q = fmaf(q, e, -0.000567059323657304f);
+    q = fmaf(q, e, 0.000624575128313154f);
+    q = fmaf(q, e, 1.010045051574707f);
+    q = fmaf(q, e, 4.14272403717041f);
+    return w0 < 16.0f ? p : q;
 }
 
 // standard normal quantile from a fp64 uniform in fp32 arithmetic:
@@ -219,14 +161,14 @@ __device__ __forceinline__ float ndtri_f(double u)
 {
     const float x = (float)(2.0 * u - 1.0);
     const float w0 = -__logf((float)(4.0 * u * (1.0 - u)));
-    float p = erfinv_central<float>(w0);
+    float p = erfinv_central(w0);
     if (w0 >= 5.0f) {
         if (w0 > 21.5f) {
             const double t = u < 0.5 ? u : 1.0 - u;
             const float z = normcdfinvf((float)t);
             return u < 0.5 ? z : -z;
         }
-        p = erfinv_tail<float>(w0);
+        p = erfinv_tail(w0);
     }
     return 1.41421356237309505f * (p * x);
 }
@@ -235,18 +177,15 @@ __device__ __forceinline__ float ndtri_f(double u)
 // all in fp32: t = min(u, 1 - u) = (min(w, ~w) + 1/2) 2^-32 keeps the tails'
 // relative precision, x = 2u - 1 comes from the signed word (per-second noise
 // of the fp32 path; the fp64 path uses ndtri(u32d(w)))
-// T = float (U = uint32_t) or the packed pair f2 (U = u2, one word per chain)
-template <typename T, typename U = typename VecOf<T>::U>
-__device__ __forceinline__ T ndtri_w(U w)
+__device__ __forceinline__ float ndtri_w(uint32_t w)
 {
-    const U m = vumin(w, ~w);   // w < 2^31 ? w : ~w
-    const T t = vfma(vcvt(m), 0x1p-32f, 0x1p-33f);
-    const T x = vfma(vcvt_i(w ^ 0x80000000u), 0x1p-31f, 0x1p-32f);
+    const uint32_t m = w < 0x80000000u ? w : ~w;
+    const float t = fmaf((float)m, 0x1p-32f, 0x1p-33f);
+    const float x = fmaf((float)(int32_t)(w ^ 0x80000000u), 0x1p-31f, 0x1p-32f);
     // -log((1 - x)(1 + x)) = -log(4 t (1 - t)); the argument is >= 2^-31: no denormal path needed
-    const T w0 = -0.693147180559945309f * vlog2(vfma(-4.0f * t, t, 4.0f * t));
-    T p = erfinv_central(w0);
-    const auto tail = w0 >= 5.0f;   // 0.34 % of draws; w0 <= 21.5 for 32-bit words
-    if (vany(tail)) p = vsel(tail, erfinv_tail(w0), p);
+    const float w0 = -0.693147180559945309f * __builtin_amdgcn_logf(fmaf(-4.0f * t, t, 4.0f * t));
+    float p = erfinv_central(w0);
+    if (w0 >= 5.0f) p = erfinv_tail(w0);   // 0.34 % of draws; w0 <= 21.5 for 32-bit words
     return 1.41421356237309505f * (p * x);
 }
 

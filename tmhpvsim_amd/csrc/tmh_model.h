@@ -1142,12 +1142,12 @@ constexpr Cubic DISC_A_LO{0.512, -1.56, 2.286, -2.222}, DISC_A_HI{-5.743, 21.77,
 constexpr Cubic DISC_B_LO{0.37, 0.962, 0.0, 0.0}, DISC_B_HI{41.4, -118.5, 66.05, 31.9};
 constexpr Cubic DISC_C_LO{-0.28, 0.932, -2.048, 0.0}, DISC_C_HI{-47.01, 184.2, -222.0, 73.81};
 
-template <int DEG, typename T>   // Horner over the shifted coefficients d_DEG .. d_0
-__device__ __forceinline__ T disc_poly(const Cubic& p, T t)
+template <int DEG>   // Horner over the shifted coefficients d_DEG .. d_0
+__device__ __forceinline__ float disc_poly(const Cubic& p, float t)
 {
-    T v = vfma(t, disc_shift(p, DEG), disc_shift(p, DEG - 1));
+    float v = disc_shift(p, DEG);
 #pragma unroll
-    for (int k = DEG - 2; k >= 0; --k) v = vfma(v, t, disc_shift(p, k));
+    for (int k = DEG - 1; k >= 0; --k) v = fmaf(v, t, disc_shift(p, k));
     return v;
 }
 
@@ -1162,54 +1162,52 @@ constexpr float KT_GUARD = 4e-6f, PDC_GUARD = 1e-4f;
 // fp32 PV chain: the model of pv_power<double>, with fused multiply-adds,
 // fp32 constants rounded once on the host (KParams::pvf) and the hardware
 // exp / log; within 1e-5 of the fp64 oracle.  `risky`: the second
-// lies in a guard band and must be recomputed in fp64.  T = float (one chain) or
-// f2 (two chains of a lane, packed: the same operations element by element).
-template <typename T>
-__device__ __forceinline__ T pv_power_f(const PVF& k, const float* g, T csi, typename VecOf<T>::M& risky)
+// lies in a guard band and must be recomputed in fp64.
+__device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float csi, bool& risky)
 {
-    const T c = vmin(csi, g[G_CSIMAX]);
-    const T ghi = c * g[G_GHICS];
-    const T kt = vmin(vmax(ghi * g[G_I0H], 0.0f), 1.0f);
+    const float c = fminf(csi, g[G_CSIMAX]);
+    const float ghi = c * g[G_GHICS];
+    const float kt = fminf(fmaxf(ghi * g[G_I0H], 0.0f), 1.0f);
     // DISC Kn: coefficient sets split at kt = 0.6 (compile-time constants, no
     // SGPRs).  Both sets are evaluated and the results selected: cheaper than
     // selecting twelve coefficient pairs per lane.
-    const auto lo = kt <= 0.6f;
-    const T t = kt - 0.6f;
-    const T a = vsel(lo, disc_poly<3>(DISC_A_LO, t), disc_poly<3>(DISC_A_HI, t));
-    const T b = vsel(lo, vfma(t, disc_shift(DISC_B_LO, 1), disc_shift(DISC_B_LO, 0)), disc_poly<3>(DISC_B_HI, t));
-    const T cc = vsel(lo, disc_poly<2>(DISC_C_LO, t), disc_poly<3>(DISC_C_HI, t));
+    const bool lo = kt <= 0.6f;
+    const float t = kt - 0.6f;
+    const float a = lo ? disc_poly<3>(DISC_A_LO, t) : disc_poly<3>(DISC_A_HI, t);
+    const float b = lo ? disc_poly<1>(DISC_B_LO, t) : disc_poly<3>(DISC_B_HI, t);
+    const float cc = lo ? disc_poly<2>(DISC_C_LO, t) : disc_poly<3>(DISC_C_HI, t);
     // exp(cc am) = exp2(cc * (am log2 e)): the fp32 row holds am log2 e (one rounding)
-    const T dkn = vfma(b, vexp2(cc * g[G_AM]), a);
-    T dni = (g[G_KNC] - dkn) * g[G_I0];
-    dni = vsel(vmask<T>(g[G_DISCOK] != 0.0f) & (ghi >= 0.0f) & (dni >= 0.0f), dni, 0.0f);
-    const T dhi = vfma(-dni, g[G_COSZ], ghi);
-    const T AI = dni * g[G_DNIEXTRA];
-    const T sky = vmax(dhi * vfma(AI, g[G_RB], (1.0f - AI) * g[G_TERM2]), 0.0f);
-    const T poa_direct = vmax(dni * g[G_COSAOI], 0.0f);
-    const T poa_diffuse = vfma(ghi, g[G_GFAC], sky);
-    const T poa_global = poa_direct + poa_diffuse;
-    const T tcell = vfma(poa_global, k.dt_1e3, vfma(poa_global, k.tmod_k, k.temp_air));
-    const T Ee = g[G_F1] * vfma(poa_direct, g[G_F2], k.fd * poa_diffuse) * 1e-3f;
-    const T Bvmpo = vfma(k.mbvmp, 1.0f - Ee, k.bvmpo);
-    const T delta = k.nkq * (tcell + 273.15f);
+    const float dkn = fmaf(b, __builtin_amdgcn_exp2f(cc * g[G_AM]), a);
+    float dni = (g[G_KNC] - dkn) * g[G_I0];
+    dni = (g[G_DISCOK] != 0.0f && ghi >= 0.0f && dni >= 0.0f) ? dni : 0.0f;
+    const float dhi = fmaf(-dni, g[G_COSZ], ghi);
+    const float AI = dni * g[G_DNIEXTRA];
+    const float sky = fmaxf(dhi * fmaf(AI, g[G_RB], (1.0f - AI) * g[G_TERM2]), 0.0f);
+    const float poa_direct = fmaxf(dni * g[G_COSAOI], 0.0f);
+    const float poa_diffuse = fmaf(ghi, g[G_GFAC], sky);
+    const float poa_global = poa_direct + poa_diffuse;
+    const float tcell = fmaf(poa_global, k.dt_1e3, fmaf(poa_global, k.tmod_k, k.temp_air));
+    const float Ee = g[G_F1] * fmaf(poa_direct, g[G_F2], k.fd * poa_diffuse) * 1e-3f;
+    const float Bvmpo = fmaf(k.mbvmp, 1.0f - Ee, k.bvmpo);
+    const float delta = k.nkq * (tcell + 273.15f);
     // the hardware log2 already gives -inf at +-0 and NaN below 0 or at NaN
-    const T logEe = vlog2(Ee) * 0.693147180559945309f;
-    const T dt25 = tcell - 25.0f;
-    const T imp = vfma(k.impo_c1, Ee, k.impo_c0) * Ee * vfma(k.aimp, dt25, 1.0f);
-    const T dl = delta * logEe;
-    T vmp = vfma(Bvmpo, dt25, vfma(k.c3ns, dl * dl, vfma(k.c2ns, dl, k.vmpo)));
-    vmp = vsel(visnan(vmp), vmp, vmax(vmp, 0.0f));
-    const T pdc = imp * vmp;
-    const T dv = vmp - k.vdco;
-    const T A = k.pdco * vfma(k.ic1, dv, 1.0f);
-    const T B = k.pso * vfma(k.ic2, dv, 1.0f);
-    const T C = k.ic0 * vfma(k.ic3, dv, 1.0f);
-    const T AmB = A - B, pmB = pdc - B;
-    const T ac = vfma(C, pmB * pmB, vfma(-C, AmB, k.paco * vrcp(AmB)) * pmB);
-    risky = (vabs(t) < KT_GUARD) | (vabs(pdc - k.pso) < PDC_GUARD * k.pso);
+    const float logEe = __builtin_amdgcn_logf(Ee) * 0.693147180559945309f;
+    const float dt25 = tcell - 25.0f;
+    const float imp = fmaf(k.impo_c1, Ee, k.impo_c0) * Ee * fmaf(k.aimp, dt25, 1.0f);
+    const float dl = delta * logEe;
+    float vmp = fmaf(Bvmpo, dt25, fmaf(k.c3ns, dl * dl, fmaf(k.c2ns, dl, k.vmpo)));
+    vmp = isnan(vmp) ? vmp : fmaxf(vmp, 0.0f);
+    const float pdc = imp * vmp;
+    const float dv = vmp - k.vdco;
+    const float A = k.pdco * fmaf(k.ic1, dv, 1.0f);
+    const float B = k.pso * fmaf(k.ic2, dv, 1.0f);
+    const float C = k.ic0 * fmaf(k.ic3, dv, 1.0f);
+    const float AmB = A - B, pmB = pdc - B;
+    const float ac = fmaf(C, pmB * pmB, fmaf(-C, AmB, k.paco * __builtin_amdgcn_rcpf(AmB)) * pmB);
+    risky = fabsf(t) < KT_GUARD || fabsf(pdc - k.pso) < PDC_GUARD * k.pso;
     // min(ac, Paco) unless NaN, -|Pnt| below the cut-in, .fillna(0), .clip(lower=0):
     // -|Pnt| <= 0 clips to 0 and a NaN fills to 0; the rest is one med3 into [0, Paco]
-    return vsel((pdc < k.pso) | visnan(ac), 0.0f, vmed3(ac, 0.0f, k.pacoc));
+    return (pdc < k.pso || isnan(ac)) ? 0.0f : __builtin_amdgcn_fmed3f(ac, 0.0f, k.pacoc);
 }
 
 // ------------------------------------------------------------ fused per-second body
@@ -1263,47 +1261,14 @@ __device__ __forceinline__ R noise_z(uint32_t w)
 {
     // fp64: ocml's ncdfinv alone, within 7e-16 of the exact quantile, far inside the fp64 bar
     if constexpr (sizeof(R) == 8) return ndtri_fast(u32d(w));
-    else return ndtri_w<float>(w);
-}
-
-// fp32 meter from the step's word: 9000 (w + 1/2) 2^-32, below 9000 (T = float or the pair f2)
-template <typename T, typename U = typename VecOf<T>::U>
-__device__ __forceinline__ T meter_f(U w)
-{
-    return vmin(vfma(vcvt(w), 9000.0f * 0x1p-32f, 9000.0f * 0x1p-33f), 8999.9990234375f);   // largest float < 9000
+    else return ndtri_w(w);
 }
 
 template <typename R>
 __device__ __forceinline__ R meter_w(uint32_t w)
 {
     if constexpr (sizeof(R) == 8) return 9000 * u32d(w);
-    else return meter_f<float>(w);
-}
-
-// the fp32 second of one chain (T = float) or of the two chains of a lane (T = f2,
-// packed): the same operations element by element as second_body<float>
-template <typename T>
-__device__ __forceinline__ T rinterp_pair(const FSamp<T>& f, int k, const float* row, int fi)
-{
-    const int pc = fi == G_MINF ? G32_MINF_C : (fi == G_HOURF ? G32_HOURF_C : G32_DAYF_C);
-    return row[pc + 1] * f.a[k] + row[pc] * f.b[k];
-}
-
-template <typename T, typename M = typename VecOf<T>::M>
-__device__ __forceinline__ void second_body_f(const KParams& kp, const PVF& pk, const float* row, uint32_t fl,
-                                              const FSamp<T>& fs, M covered, T z, T meter_in, T& csi, T& pv, T& meter,
-                                              T& res, M& risky)
-{
-    risky = M{};
-    const T cloudcover = rinterp_pair(fs, S_CC, row, G_HOURF);
-    const T eps = z * vfma(pk.eps1, cloudcover, pk.eps0);   // the scale as one FMA (z is never 0)
-    const T a_clear = rinterp_pair(fs, S_CLEAR_DAY, row, G_DAYF), a_cloudy = rinterp_pair(fs, S_CLOUDY_HOUR, row, G_HOURF);
-    const T n_clear = rinterp_pair(fs, S_CLEAR_NOISE, row, G_MINF), n_cloudy = rinterp_pair(fs, S_CLOUDY_NOISE, row, G_MINF);
-    csi = vsel(covered, a_clear, a_cloudy) * (vsel(covered, n_clear, n_cloudy) + eps);
-    if (kp.with_pv && !(fl & FL_NIGHT)) pv = pv_power_f<T>(pk, row + G32, csi, risky);
-    else pv = T(0.0f);
-    meter = meter_in;
-    res = meter - pv;
+    else return fminf(fmaf((float)w, 9000.0f * 0x1p-32f, 9000.0f * 0x1p-33f), 8999.9990234375f);   // largest float < 9000
 }
 
 // risky (fp32 only): pv lies in pv_power_f's guard band; the caller recomputes
@@ -1313,10 +1278,6 @@ __device__ __forceinline__ void second_body(const KParams& kp, const PVF& pk, co
                                             const FSamp<R>& fs, bool covered, R z, R meter_in, R& csi, R& pv, R& meter,
                                             R& res, bool& risky)
 {
-    if constexpr (sizeof(R) == 4) {
-        second_body_f<float>(kp, pk, row, fl, fs, covered, z, meter_in, csi, pv, meter, res, risky);
-        return;
-    }
     risky = false;
     const R cloudcover = rinterp_row(fs, S_CC, row, G_HOURF);   // == interp() bit for bit when R = double
     R eps;
@@ -1328,7 +1289,7 @@ __device__ __forceinline__ void second_body(const KParams& kp, const PVF& pk, co
     const R n_clear = rinterp_row(fs, S_CLEAR_NOISE, row, G_MINF), n_cloudy = rinterp_row(fs, S_CLOUDY_NOISE, row, G_MINF);
     csi = (covered ? a_clear : a_cloudy) * ((covered ? n_clear : n_cloudy) + eps);
     if constexpr (sizeof(R) == 8) pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power<R>(kp, row, csi) : R(0);
-    else pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power_f<float>(pk, row + G32, csi, risky) : 0.0f;
+    else pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power_f(pk, row + G32, csi, risky) : 0.0f;
     meter = meter_in;
     res = meter - pv;
 }
