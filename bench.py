@@ -162,6 +162,12 @@ def parse():
                          "that take the next chain when theirs is done")
     ap.add_argument("--walk-lanes", type=int, default=0,
                     help="lanes per chain in the segment walk (tmh_set_walk_lanes: 4, 8 or 16; 0 = by batch size: 16 up to 8,192 chains, else 4)")
+    ap.add_argument("--walk-cus", type=int, default=0,
+                    help="gated schedule: run the segment walks on CU-mask bits 0 .. K-1 only (a CU-masked HIP "
+                         "stream, tmh_stream_create_cus; 0 = all CUs)")
+    ap.add_argument("--other-cus", default="all", choices=["all", "rest"],
+                    help="with --walk-cus: the expansion, construction and commit streams on all CUs or on the "
+                         "CUs the walks do not use")
     ap.add_argument("--build-ahead", type=int, default=None,
                     help="gated schedule: when the walk of batch k ends, the construction of batch k + A is "
                          "released (default A = walks + 1; needs --pipeline >= A + 1)")
@@ -499,6 +505,14 @@ def main():
     W = max(1, args.walks)
     wsts = [torch.cuda.Stream(dev, priority=prio_hi if args.walk_priority == "high" else prio_lo) for _ in range(W)]
     bst = torch.cuda.Stream(dev, priority=prio_hi if args.build_priority == "high" else prio_lo)
+    cst = torch.cuda.Stream(dev)
+    if args.walk_cus:   # the walks on a share of every XCD's CUs (CU-masked streams)
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        wsts = [_lib.cu_stream(0, args.walk_cus, dev) for _ in range(W)]
+        if args.other_cus == "rest":
+            bst, cst = (_lib.cu_stream(args.walk_cus, ncu - args.walk_cus, dev) for _ in range(2))
+            estream = _lib.cu_stream(args.walk_cus, ncu - args.walk_cus, dev)
+            eptr = C.c_void_p(estream.cuda_stream)
     bst_p = C.c_void_p(bst.cuda_stream)
     A = args.build_ahead
 
@@ -531,8 +545,6 @@ def main():
                                    C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
                                    cx.scratch.numel(), None, 0, _lib.WALK_SEGMENTS, C.c_void_p(wst.cuda_stream)))
         cx.walked.record(wst)
-
-    cst = torch.cuda.Stream(dev)
 
     def g_expand(j):
         cx = ctxs[j % len(ctxs)]
@@ -718,7 +730,8 @@ def main():
                    "batches_in_flight": len(ctxs), "staggered": bool(args.stagger and nwin == 1),
                    "construction_on": args.build_on, "walk_priority": args.walk_priority,
                    "schedule": args.schedule if (args.stagger and nwin == 1 and len(ctxs) >= 3) else None,
-                   "walks_in_flight": W, "walk_chains_per_row": args.walk_cpr, "walk_lanes": args.walk_lanes or "auto", "build_ahead": A,
+                   "walks_in_flight": W, "walk_cus": args.walk_cus or "all", "other_cus": args.other_cus if args.walk_cus else "all",
+                   "walk_chains_per_row": args.walk_cpr, "walk_lanes": args.walk_lanes or "auto", "build_ahead": A,
                    "minutes_ahead": bool(args.minutes_ahead), "commit_stream": bool(args.commit_stream),
                    "compacted_windows": bool(args.compact and args.mode == "stats" and nwin > 1)},
         "roofline": roof,

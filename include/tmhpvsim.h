@@ -171,6 +171,14 @@ int tmh_set_walk_chains_per_row(struct tmh_engine* eng, uint32_t chains_per_row)
  * else 4).  Fewer lanes per chain: fewer instructions and registers per chain-call,
  * a longer chain of work per call.  Results do not depend on it. */
 int tmh_set_walk_lanes(struct tmh_engine* eng, uint32_t lanes);
+/* A HIP stream whose kernels run on a range of compute units only (no reference
+ * counterpart: a scheduling helper for callers that pipeline batches).  CU-mask
+ * bits cu_first .. cu_first + cu_count - 1 of the current device; the driver
+ * spreads consecutive mask bits over the XCDs, so a range is an even share of
+ * every XCD.  cu_count == 0: all CUs (a plain stream).  *stream receives the
+ * hipStream_t; release it with tmh_stream_destroy. */
+int tmh_stream_create_cus(uint32_t cu_first, uint32_t cu_count, void** stream);
+int tmh_stream_destroy(void* stream);
 /* Compaction (batches whose chains fault, e.g. the reference's markov-mode
  * AssertionError, cloud_cover_binary.py:91): run later windows on the live chains
  * only.  A launch slot then holds chain ids[slot] of a full batch of n_full chains:

@@ -65,7 +65,8 @@ EXPORTS = ["tmh_abi_version", "tmh_last_error", "tmh_state_bytes", "tmh_state_of
            "tmh_init", "tmh_run", "tmh_plan", "tmh_step", "tmh_probe", "tmh_profile_enable", "tmh_profile_read",
            "tmh_set_shape_tables", "tmh_set_sites", "tmh_walk", "tmh_expand",
            "tmh_walk_part", "tmh_expand_part", "tmh_set_clock", "tmh_test_set_segment_capacity",
-           "tmh_set_walk_chains_per_row", "tmh_set_walk_lanes", "tmh_set_chain_ids", "tmh_live_chains", "tmh_state_move"]
+           "tmh_set_walk_chains_per_row", "tmh_set_walk_lanes", "tmh_set_chain_ids", "tmh_live_chains", "tmh_state_move",
+           "tmh_stream_create_cus", "tmh_stream_destroy"]
 K_EXPAND, K_SEGMENTS, K_CANDIDATES, K_STEP = 0, 1, 2, 3
 WALK_DRAWS, WALK_SEGMENTS = 1, 2
 EXPAND_KERNEL, EXPAND_COMMIT, EXPAND_MINUTES, EXPAND_NO_MINUTES = 1, 2, 4, 8
@@ -109,6 +110,9 @@ def load():
         L.tmh_set_walk_chains_per_row.argtypes = [p, u32]
     if hasattr(L, "tmh_set_walk_lanes"):
         L.tmh_set_walk_lanes.argtypes = [p, u32]
+    if hasattr(L, "tmh_stream_create_cus"):
+        L.tmh_stream_create_cus.argtypes = [u32, u32, C.POINTER(p)]
+        L.tmh_stream_destroy.argtypes = [p]
     if hasattr(L, "tmh_set_chain_ids"):
         L.tmh_set_chain_ids.argtypes = [p, p, u32]
         L.tmh_live_chains.argtypes = [p, p, u32, p, p, p, p]
@@ -152,6 +156,16 @@ def check(rc):
     if rc != 0:
         raise TmhError(f"libtmhpvsim error {rc}: {load().tmh_last_error().decode()}")
     return rc
+
+
+def cu_stream(cu_first, cu_count, device):
+    """A torch stream over a HIP stream restricted to CU-mask bits cu_first ..
+    cu_first + cu_count - 1 (tmh_stream_create_cus; cu_count 0 = all CUs).  The
+    stream lives as long as the process."""
+    import torch
+    h = C.c_void_p()
+    check(load().tmh_stream_create_cus(cu_first, cu_count, C.byref(h)))
+    return torch.cuda.ExternalStream(h.value, device=device)
 
 
 def profile_read(eng, kernel):

@@ -35,6 +35,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -345,6 +346,7 @@ __global__ __launch_bounds__(256) void geom_kernel(GParams gp, int64_t step0, ui
     for (int i = 0; i < SUN_W; ++i) sun[(size_t)j * SUN_W + i] = sn[i];
     site_geom<true>(site_k(gp.site), sn, sn[SUN_TL], gp.module, g);
     if (g[G_GHICS] == 0.0) fl |= FL_NIGHT;   // ghi_cs = 0 -> pv = 0 whatever the csi
+    if (g[G_DISCOK] != 0.0) fl |= FL_DISCOK;
     g[G_FLAGS] = (double)fl;
     double* o64 = tab64 + (size_t)j * ROW;
     float* o32 = tab32 + (size_t)j * ROW32;
@@ -360,6 +362,7 @@ __global__ __launch_bounds__(256) void geom_kernel(GParams gp, int64_t step0, ui
     o32[G_I0H + G32] = (float)(1.0 / g[G_I0H]);   // fp32 path multiplies by reciprocals
     o32[G_DNIEXTRA + G32] = (float)(1.0 / g[G_DNIEXTRA]);
     o32[G_AM + G32] = (float)(g[G_AM] * LOG2E);   // exp(c am) = exp2(c * am log2 e)
+    o32[G_F1 + G32] = (float)(g[G_F1] * 1e-3);    // Ee = F1 (...) / 1000 with the division folded in
 }
 
 // Compact the window's day/hour boundary steps, in order (one workgroup).
@@ -827,7 +830,7 @@ __device__ __forceinline__ bool redo_second(const KParams& kp, const DrawParams&
         float csi, m, r;
         const uint32_t fl = __float_as_uint(row[G_FLAGS + G32]) & ~(uint32_t)FL_NIGHT;
         uint32_t flp = __float_as_uint(row[G_FLAGS + G32]);
-        if constexpr (SITES) flp = lane_row<float>(ls, sun + (size_t)j * SUN_W, kp.module, row) ? (fl | FL_NIGHT) : fl;
+        if constexpr (SITES) flp = lane_flags(fl, lane_row<float>(ls, sun + (size_t)j * SUN_W, kp.module, row), row);
         second_body<float>(kp, kp.pvf, row, flp, f, covered, noise_z<float>(odd ? pb.z : pb.x),
                            meter_w<float>(odd ? pb.w : pb.y), csi, pv32, m, r, risky);
         meter32 = m;
@@ -964,8 +967,7 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
                     cov = covered ? 1 : 0;
                     uint32_t flp = fl;
                     if (kp.sites) {   // this chain's own site
-                        const bool night = lane_row<R>(ls, sun + (size_t)j * SUN_W, kp.module, row);
-                        flp = night ? (fl | FL_NIGHT) : (fl & ~(uint32_t)FL_NIGHT);
+                        flp = lane_flags(fl, lane_row<R>(ls, sun + (size_t)j * SUN_W, kp.module, row), row);
                     }
                     bool risky;
                     second_body<R>(kp, kp.pvf, row, flp, fs, covered, z, mtr, csi, pv, meter, res, risky);
@@ -1702,14 +1704,18 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
     // wave_ok: no lane of the wave has a fault before the block's end (the common case),
     // so a scalar branch skips the per-second NaN selects.
     // lanes past the last chain store out of range (voff) and emit nothing: they never fault the wave
+    // The loops are instantiated twice: FF (fault-free, wave_ok) with ok = true and no
+    // NaN selects at all (if-converted, they cost a compare and three selects per second
+    // even when wave_ok holds), and the general one (below).
     const bool wave_ok = __builtin_amdgcn_ballot_w64(live && fault_eff < (int32_t)j1) == 0;
-    auto second = [&](uint32_t j, uint32_t un, uint32_t um) __attribute__((always_inline)) {
+    auto second = [&](uint32_t j, uint32_t un, uint32_t um, auto ff) __attribute__((always_inline)) {
+        constexpr bool FF = decltype(ff)::value;
         R row[row_w<R>()];
 #pragma unroll
         for (int i = 0; i < row_w<R>(); ++i) row[i] = rowp[i];
         rowp += RW;
         const uint32_t fl = sizeof(R) == 8 ? (uint32_t)(double)rowp[G_FLAGS - RW] : __float_as_uint(row[G_FLAGS + G32]);
-        const bool ok = wave_ok || (int32_t)j < fault_eff;
+        const bool ok = FF || (int32_t)j < fault_eff;
         if (fl & (FL_DAY | FL_HOUR)) {            // _next_day, _next_hour (rare: loads waited here)
             const size_t eo = (size_t)evi * 4 * n;
             if (live) {
@@ -1750,8 +1756,7 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
         const bool covered = (cov_w >> (jb & 31)) & 1u;
         uint32_t flp = fl;
         if constexpr (SITES) {   // this chain's own site: geometry per chain-second (none in a night block)
-            const bool night = blk_night || lane_row<R>(ls, sun + (size_t)j * SUN_W, kp.module, row);
-            flp = night ? (fl | FL_NIGHT) : (fl & ~(uint32_t)FL_NIGHT);
+            flp = lane_flags(fl, blk_night || lane_row<R>(ls, sun + (size_t)j * SUN_W, kp.module, row), row);
         }
         R csi, pv, meter, res;
         bool held = false;   // fp32: PV in a guard band, recomputed in fp64 by fixup_kernel
@@ -1773,7 +1778,7 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
                 *hw |= 1u << (jb & 31);
             }
         }
-        if (!wave_ok) {
+        if constexpr (!FF) {
             csi = ok ? csi : R(NAN);
             pv = ok ? pv : R(NAN);
             meter = ok ? meter : R(NAN);
@@ -1790,19 +1795,25 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
         }
     };
     // one Philox block per step pair: (x, y) for the even step, (z, w) for the odd one
-    if (((W0 + j0) & 1) == 0 && ((j1 - j0) & 1) == 0) {
-        for (uint32_t j = j0; j < j1; j += 2) {
-            const U4 pr = keyed_block(kp.seed, chain, (uint64_t)(W0 + j) >> 1, TAG_STEP2, 0);
-            second(j, pr.x, pr.y);
-            second(j + 1, pr.z, pr.w);
+    auto loops = [&](auto ff) __attribute__((always_inline)) {
+        if (((W0 + j0) & 1) == 0 && ((j1 - j0) & 1) == 0) {
+            for (uint32_t j = j0; j < j1; j += 2) {
+                const U4 pr = keyed_block(kp.seed, chain, (uint64_t)(W0 + j) >> 1, TAG_STEP2, 0);
+                second(j, pr.x, pr.y, ff);
+                second(j + 1, pr.z, pr.w, ff);
+            }
+        } else {   // odd window start or length: one block per step (rare)
+            for (uint32_t j = j0; j < j1; ++j) {
+                const U4 pr = keyed_block(kp.seed, chain, (uint64_t)(W0 + j) >> 1, TAG_STEP2, 0);
+                const bool odd = (W0 + j) & 1;
+                second(j, odd ? pr.z : pr.x, odd ? pr.w : pr.y, ff);
+            }
         }
-    } else {   // odd window start or length: one block per step (rare)
-        for (uint32_t j = j0; j < j1; ++j) {
-            const U4 pr = keyed_block(kp.seed, chain, (uint64_t)(W0 + j) >> 1, TAG_STEP2, 0);
-            const bool odd = (W0 + j) & 1;
-            second(j, odd ? pr.z : pr.x, odd ? pr.w : pr.y);
-        }
-    }
+    };
+    // (fp32 single-site only: in the fp64 and per-site kernels, which sit at their
+    // register bounds, the second copy adds spills)
+    if (sizeof(R) == 4 && !SITES && wave_ok) loops(std::true_type{});
+    else loops(std::false_type{});
     if constexpr (sizeof(R) == 4) {
         const uint4 hm = held_lds[threadIdx.x];
         const bool held_any = (hm.x | hm.y | hm.z | hm.w) != 0;
@@ -2388,7 +2399,7 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
         f.fd = (float)m[TMH_MOD_FD];
         f.bvmpo = (float)m[TMH_MOD_BVMPO];
         f.mbvmp = (float)m[TMH_MOD_MBVMP];
-        f.nkq = (float)(m[TMH_MOD_N] * (1.38066e-23 / 1.60218e-19));
+        f.nkq = (float)(m[TMH_MOD_N] * (1.38066e-23 / 1.60218e-19) * 0.693147180559945309);   // x ln 2: pv_power_f takes log2(Ee)
         f.impo_c0 = (float)(m[TMH_MOD_IMPO] * m[TMH_MOD_C0]);
         f.impo_c1 = (float)(m[TMH_MOD_IMPO] * m[TMH_MOD_C1]);
         f.aimp = (float)m[TMH_MOD_AIMP];
@@ -2505,6 +2516,35 @@ int tmh_set_walk_lanes(struct tmh_engine* eng, uint32_t lanes)
     if (lanes != 0 && lanes != 4 && lanes != 8 && lanes != 16) return fail(TMH_E_INVAL, "walk lanes %u: 4, 8 or 16", lanes);
     eng->walk_lanes = lanes;
     return TMH_OK;
+}
+
+int tmh_stream_create_cus(uint32_t cu_first, uint32_t cu_count, void** stream)
+{
+    if (!stream) return fail(TMH_E_INVAL, "NULL stream out");
+    *stream = nullptr;
+    hipStream_t s = nullptr;
+    if (cu_count == 0) {
+        if (int rc = hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate")) return rc;
+        *stream = s;
+        return TMH_OK;
+    }
+    int dev = 0, ncu = 0;
+    if (int rc = hip_check(hipGetDevice(&dev), "hipGetDevice")) return rc;
+    if (int rc = hip_check(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev), "CU count")) return rc;
+    if ((uint64_t)cu_first + cu_count > (uint64_t)ncu)
+        return fail(TMH_E_INVAL, "CU range %u + %u past the device's %d CUs", cu_first, cu_count, ncu);
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    for (uint32_t i = cu_first; i < cu_first + cu_count; ++i) mask[i >> 5] |= 1u << (i & 31);
+    if (int rc = hip_check(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()), "hipExtStreamCreateWithCUMask"))
+        return rc;
+    *stream = s;
+    return TMH_OK;
+}
+
+int tmh_stream_destroy(void* stream)
+{
+    if (!stream) return TMH_OK;
+    return hip_check(hipStreamDestroy((hipStream_t)stream), "hipStreamDestroy");
 }
 
 int tmh_set_chain_ids(struct tmh_engine* eng, const uint32_t* ids, uint32_t n_full)

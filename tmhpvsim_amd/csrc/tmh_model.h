@@ -53,7 +53,9 @@ struct GParams {
     tmh_clock clock;
 };
 
-enum : uint32_t { FL_DAY = 1, FL_HOUR = 2, FL_MIN = 4, FL_NIGHT = 8 };
+// FL_DISCOK: DISC's zenith test passes (pvlib irradiance.disc max_zenith, the row's
+// G_DISCOK as a flag bit, so the fp32 chain tests a scalar instead of a float per lane)
+enum : uint32_t { FL_DAY = 1, FL_HOUR = 2, FL_MIN = 4, FL_NIGHT = 8, FL_DISCOK = 16 };
 // clock/geometry table row (TMH_GEOM_FIELDS = 20)
 enum {
     G_MINF = 0, G_HOURF = 1, G_DAYF = 2, G_FLAGS = 3, G_COSZ = 4, G_CSIMAX = 5, G_GHICS = 6,
@@ -993,6 +995,7 @@ __device__ __forceinline__ void site_row(const double* g, const double* sun, R* 
         row[G_I0H] = (float)(1.0 / g[G_I0H]);
         row[G_DNIEXTRA] = (float)sun[SUN_RDNIX];
         row[G_AM] = (float)(g[G_AM] * LOG2E);
+        row[G_F1] = (float)(g[G_F1] * 1e-3);   // pv_power_f: Ee = F1 (...) without the / 1000
     }
 }
 
@@ -1036,6 +1039,16 @@ __device__ __forceinline__ bool lane_row(LaneSite& ls, const double* sun, const 
     if (site_geom<false, sizeof(R) == 4>(ls.k, sun, tl, module, g)) return true;
     site_row<R>(g, sun, row);
     return g[G_GHICS] == 0.0;
+}
+
+// the flags of a per-chain-site second: the table's day / hour / minute bits, then
+// night and DISC's zenith test from the lane's own row (lane_row's result and row)
+template <typename R>
+__device__ __forceinline__ uint32_t lane_flags(uint32_t fl, bool night, const R* row)
+{
+    fl &= ~(uint32_t)(FL_NIGHT | FL_DISCOK);
+    if (night) return fl | FL_NIGHT;
+    return row[row_off<R>() + G_DISCOK] != R(0) ? (fl | FL_DISCOK) : fl;
 }
 
 
@@ -1163,9 +1176,10 @@ constexpr float KT_GUARD = 4e-6f, PDC_GUARD = 1e-4f;
 // fp32 constants rounded once on the host (KParams::pvf) and the hardware
 // exp / log; within 1e-5 of the fp64 oracle.  `risky`: the second
 // lies in a guard band and must be recomputed in fp64.
-__device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float csi, bool& risky)
+__device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float csi, bool discok, bool& risky)
 {
-    const float c = fminf(csi, g[G_CSIMAX]);
+    // min(csi, csimax) as a median with -inf: no canonicalising max of the row's value first
+    const float c = __builtin_amdgcn_fmed3f(csi, -INFINITY, g[G_CSIMAX]);
     const float ghi = c * g[G_GHICS];
     const float kt = fminf(fmaxf(ghi * g[G_I0H], 0.0f), 1.0f);
     // DISC Kn: coefficient sets split at kt = 0.6 (compile-time constants, no
@@ -1179,7 +1193,7 @@ __device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float 
     // exp(cc am) = exp2(cc * (am log2 e)): the fp32 row holds am log2 e (one rounding)
     const float dkn = fmaf(b, __builtin_amdgcn_exp2f(cc * g[G_AM]), a);
     float dni = (g[G_KNC] - dkn) * g[G_I0];
-    dni = (g[G_DISCOK] != 0.0f && ghi >= 0.0f && dni >= 0.0f) ? dni : 0.0f;
+    dni = (discok && ghi >= 0.0f && dni >= 0.0f) ? dni : 0.0f;
     const float dhi = fmaf(-dni, g[G_COSZ], ghi);
     const float AI = dni * g[G_DNIEXTRA];
     const float sky = fmaxf(dhi * fmaf(AI, g[G_RB], (1.0f - AI) * g[G_TERM2]), 0.0f);
@@ -1187,16 +1201,17 @@ __device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float 
     const float poa_diffuse = fmaf(ghi, g[G_GFAC], sky);
     const float poa_global = poa_direct + poa_diffuse;
     const float tcell = fmaf(poa_global, k.dt_1e3, fmaf(poa_global, k.tmod_k, k.temp_air));
-    const float Ee = g[G_F1] * fmaf(poa_direct, g[G_F2], k.fd * poa_diffuse) * 1e-3f;
+    const float Ee = g[G_F1] * fmaf(poa_direct, g[G_F2], k.fd * poa_diffuse);   // the row's F1 holds F1 / 1000
     const float Bvmpo = fmaf(k.mbvmp, 1.0f - Ee, k.bvmpo);
-    const float delta = k.nkq * (tcell + 273.15f);
+    const float delta = k.nkq * (tcell + 273.15f);   // k.nkq holds n k / q ln 2: delta log2(Ee) = delta_ref ln(Ee)
     // the hardware log2 already gives -inf at +-0 and NaN below 0 or at NaN
-    const float logEe = __builtin_amdgcn_logf(Ee) * 0.693147180559945309f;
+    const float logEe = __builtin_amdgcn_logf(Ee);
     const float dt25 = tcell - 25.0f;
     const float imp = fmaf(k.impo_c1, Ee, k.impo_c0) * Ee * fmaf(k.aimp, dt25, 1.0f);
     const float dl = delta * logEe;
-    float vmp = fmaf(Bvmpo, dt25, fmaf(k.c3ns, dl * dl, fmaf(k.c2ns, dl, k.vmpo)));
-    vmp = isnan(vmp) ? vmp : fmaxf(vmp, 0.0f);
+    // max(vmp, 0) unless NaN in the reference; a NaN vmp there gives p_dc NaN and pv 0
+    // (.fillna), here vmp 0 gives p_dc 0 < Pso and pv 0: the same pv, one op less
+    const float vmp = fmaxf(fmaf(Bvmpo, dt25, fmaf(k.c3ns, dl * dl, fmaf(k.c2ns, dl, k.vmpo))), 0.0f);
     const float pdc = imp * vmp;
     const float dv = vmp - k.vdco;
     const float A = k.pdco * fmaf(k.ic1, dv, 1.0f);
@@ -1249,7 +1264,8 @@ __device__ __forceinline__ R rinterp_row(const FSamp<R>& f, int k, const R* row,
     if constexpr (sizeof(R) == 8) return rinterp(f, k, row[fi]);
     else {
         const int pc = fi == G_MINF ? G32_MINF_C : (fi == G_HOURF ? G32_HOURF_C : G32_DAYF_C);
-        return row[pc + 1] * f.a[k] + row[pc] * f.b[k];
+        // a multiply and an FMA (2 fast-rate ops) rather than a packed multiply and an add
+        return fmaf(row[pc + 1], f.a[k], row[pc] * f.b[k]);
     }
 }
 
@@ -1289,7 +1305,7 @@ __device__ __forceinline__ void second_body(const KParams& kp, const PVF& pk, co
     const R n_clear = rinterp_row(fs, S_CLEAR_NOISE, row, G_MINF), n_cloudy = rinterp_row(fs, S_CLOUDY_NOISE, row, G_MINF);
     csi = (covered ? a_clear : a_cloudy) * ((covered ? n_clear : n_cloudy) + eps);
     if constexpr (sizeof(R) == 8) pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power<R>(kp, row, csi) : R(0);
-    else pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power_f(pk, row + G32, csi, risky) : 0.0f;
+    else pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power_f(pk, row + G32, csi, (fl & FL_DISCOK) != 0, risky) : 0.0f;
     meter = meter_in;
     res = meter - pv;
 }
