@@ -68,6 +68,9 @@ def test_probe_math():
     w = np.random.default_rng(1).integers(0, 2 ** 32, 20000, dtype=np.uint64)
     u32 = (w.astype(np.float64) + 0.5) * 2.0 ** -32            # the fp64 per-second noise's uniforms
     np.testing.assert_allclose(probe(8, 0, u32), O.ndtri(u32), rtol=2e-15)
+    # pv_power_f's final clamp relies on v_med3_f32(NaN, 0, Paco) = 0 (min3 on a NaN operand)
+    x = np.array([np.nan, -5.0, 0.5, 3000.0, 1e9])
+    np.testing.assert_array_equal(probe(9, 2500.0, x), [0.0, 0.0, 0.5, 2500.0, 2500.0])
 
 
 # ------------------------------------------------------------------ reference fixtures

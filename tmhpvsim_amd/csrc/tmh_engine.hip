@@ -363,6 +363,7 @@ __global__ __launch_bounds__(256) void geom_kernel(GParams gp, int64_t step0, ui
     o32[G_DNIEXTRA + G32] = (float)(1.0 / g[G_DNIEXTRA]);
     o32[G_AM + G32] = (float)(g[G_AM] * LOG2E);   // exp(c am) = exp2(c * am log2 e)
     o32[G_F1 + G32] = (float)(g[G_F1] * 1e-3);    // Ee = F1 (...) / 1000 with the division folded in
+    o32[G_RB + G32] = (float)(g[G_RB] - g[G_TERM2]);   // sky = dhi (term2 + AI (Rb - term2))
 }
 
 // Compact the window's day/hour boundary steps, in order (one workgroup).
@@ -2048,6 +2049,7 @@ __global__ void probe_kernel(int fn, double a, const double* x, double* out, uin
         }
         case 6: v = dpp_f64<0x138>(a, x[i]); break;            // wave_shr:1, lane 0 <- a
         case 7: v = readlane_f64(x[i], 63); break;
+        case 9: v = (double)__builtin_amdgcn_fmed3f((float)x[i], 0.0f, (float)a); break;   // pv_power_f's final clamp
         default: v = NAN;
     }
     out[i] = v;
@@ -2393,13 +2395,18 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
         PVF& f = k.pvf;
         const double* m = k.module;
         const double* iv = k.inverter;
-        f.tmod_k = (float)k.tmod_k;
+        const double nkq = m[TMH_MOD_N] * (1.38066e-23 / 1.60218e-19) * 0.693147180559945309;   // x ln 2: log2(Ee)
+        const double vdco = iv[2];
+        const double a1 = iv[1] * iv[5], a0 = iv[1] * (1.0 - iv[5] * vdco);   // A = Pdco (1 + C1 (vmp - Vdco))
+        const double b1 = iv[3] * iv[6], b0 = iv[3] * (1.0 - iv[6] * vdco);   // B = Pso (1 + C2 (vmp - Vdco))
+        const double c1 = iv[4] * iv[7], c0 = iv[4] * (1.0 - iv[7] * vdco);   // C = C0 (1 + C3 (vmp - Vdco))
+        f.tk = (float)(k.tmod_k + m[TMH_MOD_TEMP_DT] * 1e-3);
         f.temp_air = (float)k.temp_air;
-        f.dt_1e3 = (float)(m[TMH_MOD_TEMP_DT] * 1e-3);
         f.fd = (float)m[TMH_MOD_FD];
-        f.bvmpo = (float)m[TMH_MOD_BVMPO];
-        f.mbvmp = (float)m[TMH_MOD_MBVMP];
-        f.nkq = (float)(m[TMH_MOD_N] * (1.38066e-23 / 1.60218e-19) * 0.693147180559945309);   // x ln 2: pv_power_f takes log2(Ee)
+        f.nmbvmp = (float)(-m[TMH_MOD_MBVMP]);
+        f.bvmpo1 = (float)(m[TMH_MOD_BVMPO] + m[TMH_MOD_MBVMP]);
+        f.nkq = (float)nkq;
+        f.nkq273 = (float)(nkq * 273.15);
         f.impo_c0 = (float)(m[TMH_MOD_IMPO] * m[TMH_MOD_C0]);
         f.impo_c1 = (float)(m[TMH_MOD_IMPO] * m[TMH_MOD_C1]);
         f.aimp = (float)m[TMH_MOD_AIMP];
@@ -2407,14 +2414,13 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
         f.c2ns = (float)(m[TMH_MOD_C2] * m[TMH_MOD_NS]);
         f.c3ns = (float)(m[TMH_MOD_C3] * m[TMH_MOD_NS]);
         f.paco = (float)iv[0];
-        f.pdco = (float)iv[1];
-        f.vdco = (float)iv[2];
         f.pso = (float)iv[3];
-        f.ic0 = (float)iv[4];
-        f.ic1 = (float)iv[5];
-        f.ic2 = (float)iv[6];
-        f.ic3 = (float)iv[7];
-        f.pnt = (float)iv[8];
+        f.ab1 = (float)(a1 - b1);
+        f.ab0 = (float)(a0 - b0);
+        f.b1 = (float)b1;
+        f.b0 = (float)b0;
+        f.c1 = (float)c1;
+        f.c0 = (float)c0;
         f.pacoc = (float)(iv[0] > 0.0 ? iv[0] : 0.0);
         f.eps0 = (float)(k.sqrt6 * 0.001);
         f.eps1 = (float)(k.sqrt6 * (0.0015 * 8));

@@ -15,9 +15,15 @@ namespace tmh {
 
 // ------------------------------------------------------------ parameters
 // fp32 constants of the PV chain (pvmodel.py:53-80), rounded once on the host
+// in the forms pv_power_f evaluates (each an affine map in one variable, so one FMA):
+//   tcell = poa (tmod_k + dT / 1000) + temp_air          tk, temp_air
+//   Bvmpo = bvmpo + mbvmp (1 - Ee)                        nmbvmp = -mbvmp, bvmpo1 = bvmpo + mbvmp
+//   delta log2(Ee) = n k / q (tcell + 273.15) ln(Ee)     nkq = n k / q ln 2, nkq273 = 273.15 nkq
+//   A - B, B, C of the SNL inverter, affine in vmp:       (ab1, ab0), (b1, b0), (c1, c0)
 struct PVF {
-    float tmod_k, temp_air, dt_1e3, fd, bvmpo, mbvmp, nkq, impo_c0, impo_c1, aimp, vmpo, c2ns, c3ns;
-    float paco, pdco, vdco, pso, ic0, ic1, ic2, ic3, pnt;
+    float tk, temp_air, fd, nmbvmp, bvmpo1, nkq, nkq273, impo_c0;   // the first PVF_VGPR: pinned in VGPRs
+    float impo_c1, aimp, vmpo, c2ns, c3ns;
+    float paco, pso, ab1, ab0, b1, b0, c1, c0;
     float pacoc;        // max(Paco, 0): the upper bound of the final clamp
     float eps0, eps1;   // sqrt(6) 0.001, sqrt(6) 0.0015 * 8: the noise scale is eps0 + eps1 cc
 };
@@ -996,6 +1002,7 @@ __device__ __forceinline__ void site_row(const double* g, const double* sun, R* 
         row[G_DNIEXTRA] = (float)sun[SUN_RDNIX];
         row[G_AM] = (float)(g[G_AM] * LOG2E);
         row[G_F1] = (float)(g[G_F1] * 1e-3);   // pv_power_f: Ee = F1 (...) without the / 1000
+        row[G_RB] = (float)(g[G_RB] - g[G_TERM2]);   // pv_power_f: sky = dhi (term2 + AI (Rb - term2))
     }
 }
 
@@ -1196,14 +1203,15 @@ __device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float 
     dni = (discok && ghi >= 0.0f && dni >= 0.0f) ? dni : 0.0f;
     const float dhi = fmaf(-dni, g[G_COSZ], ghi);
     const float AI = dni * g[G_DNIEXTRA];
-    const float sky = fmaxf(dhi * fmaf(AI, g[G_RB], (1.0f - AI) * g[G_TERM2]), 0.0f);
+    // AI Rb + (1 - AI) term2 = term2 + AI (Rb - term2): the fp32 row's G_RB holds Rb - term2
+    const float sky = fmaxf(dhi * fmaf(AI, g[G_RB], g[G_TERM2]), 0.0f);
     const float poa_direct = fmaxf(dni * g[G_COSAOI], 0.0f);
     const float poa_diffuse = fmaf(ghi, g[G_GFAC], sky);
     const float poa_global = poa_direct + poa_diffuse;
-    const float tcell = fmaf(poa_global, k.dt_1e3, fmaf(poa_global, k.tmod_k, k.temp_air));
+    const float tcell = fmaf(poa_global, k.tk, k.temp_air);
     const float Ee = g[G_F1] * fmaf(poa_direct, g[G_F2], k.fd * poa_diffuse);   // the row's F1 holds F1 / 1000
-    const float Bvmpo = fmaf(k.mbvmp, 1.0f - Ee, k.bvmpo);
-    const float delta = k.nkq * (tcell + 273.15f);   // k.nkq holds n k / q ln 2: delta log2(Ee) = delta_ref ln(Ee)
+    const float Bvmpo = fmaf(k.nmbvmp, Ee, k.bvmpo1);
+    const float delta = fmaf(k.nkq, tcell, k.nkq273);   // delta log2(Ee) = delta_ref ln(Ee)
     // the hardware log2 already gives -inf at +-0 and NaN below 0 or at NaN
     const float logEe = __builtin_amdgcn_logf(Ee);
     const float dt25 = tcell - 25.0f;
@@ -1213,16 +1221,15 @@ __device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float 
     // (.fillna), here vmp 0 gives p_dc 0 < Pso and pv 0: the same pv, one op less
     const float vmp = fmaxf(fmaf(Bvmpo, dt25, fmaf(k.c3ns, dl * dl, fmaf(k.c2ns, dl, k.vmpo))), 0.0f);
     const float pdc = imp * vmp;
-    const float dv = vmp - k.vdco;
-    const float A = k.pdco * fmaf(k.ic1, dv, 1.0f);
-    const float B = k.pso * fmaf(k.ic2, dv, 1.0f);
-    const float C = k.ic0 * fmaf(k.ic3, dv, 1.0f);
-    const float AmB = A - B, pmB = pdc - B;
+    const float AmB = fmaf(k.ab1, vmp, k.ab0), B = fmaf(k.b1, vmp, k.b0), C = fmaf(k.c1, vmp, k.c0);
+    const float pmB = pdc - B;
     const float ac = fmaf(C, pmB * pmB, fmaf(-C, AmB, k.paco * __builtin_amdgcn_rcpf(AmB)) * pmB);
     risky = fabsf(t) < KT_GUARD || fabsf(pdc - k.pso) < PDC_GUARD * k.pso;
     // min(ac, Paco) unless NaN, -|Pnt| below the cut-in, .fillna(0), .clip(lower=0):
-    // -|Pnt| <= 0 clips to 0 and a NaN fills to 0; the rest is one med3 into [0, Paco]
-    return (pdc < k.pso || isnan(ac)) ? 0.0f : __builtin_amdgcn_fmed3f(ac, 0.0f, k.pacoc);
+    // -|Pnt| <= 0 clips to 0 and a NaN fills to 0; the rest is one med3 into [0, Paco].
+    // v_med3_f32 with a NaN operand returns min3 of its operands, so a NaN ac gives
+    // min(0, max(Paco, 0)) = 0 with no separate NaN test (tmh_probe fn 9, test_probe_math)
+    return pdc < k.pso ? 0.0f : __builtin_amdgcn_fmed3f(ac, 0.0f, k.pacoc);
 }
 
 // ------------------------------------------------------------ fused per-second body
@@ -1284,7 +1291,10 @@ template <typename R>
 __device__ __forceinline__ R meter_w(uint32_t w)
 {
     if constexpr (sizeof(R) == 8) return 9000 * u32d(w);
-    else return fminf(fmaf((float)w, 9000.0f * 0x1p-32f, 9000.0f * 0x1p-33f), 8999.9990234375f);   // largest float < 9000
+    // 9000 u = 9000 (w + 1/2) 2^-32 with the scale shrunk by 2^-23 relative: w = 2^32 - 1
+    // converts to 2^32 and then lands on 8999.999 (the largest float < 9000), so no clamp
+    // is needed to keep [0, 9000); 1.2e-7 relative, far inside the fp32 bar
+    else return fmaf((float)w, 9000.0f * 0x1p-32f * (1.0f - 0x1p-23f), 9000.0f * 0x1p-33f);
 }
 
 // risky (fp32 only): pv lies in pv_power_f's guard band; the caller recomputes
