@@ -171,6 +171,11 @@ int tmh_set_walk_chains_per_row(struct tmh_engine* eng, uint32_t chains_per_row)
  * else 4).  Fewer lanes per chain: fewer instructions and registers per chain-call,
  * a longer chain of work per call.  Results do not depend on it. */
 int tmh_set_walk_lanes(struct tmh_engine* eng, uint32_t lanes);
+/* Walk rows in the order of the chains' wind over the window, windiest first (on
+ * by default): the chains of one walk wavefront then make similar numbers of
+ * next_cloud calls.  Set it before a window's draws (TMH_WALK_DRAWS: they compute the
+ * order and store the candidate table by it).  Results do not depend on it. */
+int tmh_set_walk_order(struct tmh_engine* eng, int on);
 /* A HIP stream whose kernels run on a range of compute units only (no reference
  * counterpart: a scheduling helper for callers that pipeline batches).  CU-mask
  * bits cu_first .. cu_first + cu_count - 1 of the current device; the driver

@@ -496,7 +496,8 @@ def test_walk_lanes_invariance(window, markov, start):
     entries spread over fewer lanes, more register chunks per lane; entries past
     the registers in the chain's global row) gives bit-identical results -- covered
     bit, PV, status, call counts and the window-end sigma arrays -- alone and with
-    groups that take queued chains, in one window or in chained windows.  2,000
+    groups that take queued chains, with the rows in wind order (tmh_set_walk_order) or
+    in chain order, in one window or in chained windows.  2,000
     chain-days reach sigma lengths past 64 (~0.5 % of the calls) on every path.  Markov
     cloud cover with per-site tables (C5's walk inputs) too, and chained windows across the
     DST fall-back (the walk's clock shift)."""
@@ -507,11 +508,12 @@ def test_walk_lanes_invariance(window, markov, start):
     mp = ModelParams(cc_mode=CC_MARKOV, seed=0x7AB1E) if markov else None
     tab = site_shape_tables(n) if markov else None
     outs = []
-    for lanes, cpr in ((16, 1), (8, 1), (4, 1), (4, 3), (8, 2)):
+    for lanes, cpr, order in ((16, 1, 1), (16, 1, 0), (8, 1, 1), (4, 1, 1), (4, 3, 1), (4, 3, 0), (8, 2, 1)):
         s = _sim(n, start, tz="Europe/Berlin", mp=mp, prec="fp32", kernel_path="time_parallel", horizon=steps,
                  tables=tab)
         _lib.check(L.tmh_set_walk_lanes(s._eng, lanes))
         _lib.check(L.tmh_set_walk_chains_per_row(s._eng, cpr))
+        _lib.check(L.tmh_set_walk_order(s._eng, order))   # rows windiest chain first, or in chain order
         out = s.run(steps, trace=("covered", "pv"), window=window)
         torch.cuda.synchronize()
         outs.append((s.status(), _np(out["covered"]), _np(out["pv"]), s.state_field("ncalls").cpu().numpy(),

@@ -66,7 +66,7 @@ EXPORTS = ["tmh_abi_version", "tmh_last_error", "tmh_state_bytes", "tmh_state_of
            "tmh_set_shape_tables", "tmh_set_sites", "tmh_walk", "tmh_expand",
            "tmh_walk_part", "tmh_expand_part", "tmh_set_clock", "tmh_test_set_segment_capacity",
            "tmh_set_walk_chains_per_row", "tmh_set_walk_lanes", "tmh_set_chain_ids", "tmh_live_chains", "tmh_state_move",
-           "tmh_stream_create_cus", "tmh_stream_destroy"]
+           "tmh_stream_create_cus", "tmh_stream_destroy", "tmh_set_walk_order"]
 K_EXPAND, K_SEGMENTS, K_CANDIDATES, K_STEP = 0, 1, 2, 3
 WALK_DRAWS, WALK_SEGMENTS = 1, 2
 EXPAND_KERNEL, EXPAND_COMMIT, EXPAND_MINUTES, EXPAND_NO_MINUTES = 1, 2, 4, 8
@@ -110,6 +110,8 @@ def load():
         L.tmh_set_walk_chains_per_row.argtypes = [p, u32]
     if hasattr(L, "tmh_set_walk_lanes"):
         L.tmh_set_walk_lanes.argtypes = [p, u32]
+    if hasattr(L, "tmh_set_walk_order"):
+        L.tmh_set_walk_order.argtypes = [p, C.c_int]
     if hasattr(L, "tmh_stream_create_cus"):
         L.tmh_stream_create_cus.argtypes = [u32, u32, C.POINTER(p)]
         L.tmh_stream_destroy.argtypes = [p]

@@ -78,6 +78,8 @@ struct SegView {                   // P1 -> P2 scratch
     uint32_t* pool_n;              // chunks handed out (zeroed by the draws phase)
     uint32_t* walk_q;              // the walk's chain queue: chains taken past the first `rows` (zeroed likewise)
     uint32_t* pool_short;          // some chain found the pool exhausted (zeroed likewise)
+    uint32_t* order;               // [n] walk row -> chain (windiest first, walk_order_kernel); NULL: row r is chain r
+    uint32_t* rank;                // [n] chain -> walk row (the inverse; cand is stored by row)
     int32_t* ovf_first;            // [n] window-relative step of the chain's record `cap` (INT_MAX: none)
     uint32_t* count;               // [n]
     int32_t* fault;                // [n] window-relative fault step (INT_MAX = none)
@@ -1070,7 +1072,59 @@ __global__ __launch_bounds__(256) void candidates_kernel(DrawParams dp, StateVie
     }
     if (c >= n || (prev.status ? prev.status[c] : st.status[c]) != 0) return;
     const U4 b = keyed_block(dp.seed, chain0 + gid(dp.ids, c), (uint64_t)(st.ncalls[c] + k), TAG_CLOUD, 0);
-    sg.cand[(size_t)k * n + c] = pow_d(dp.alpha + dp.delta * u52(b.x, b.y), dp.expo);
+    // stored by walk row: the chains of a walk wavefront read adjacent words
+    sg.cand[(size_t)k * n + (sg.rank ? sg.rank[c] : c)] = pow_d(dp.alpha + dp.delta * u52(b.x, b.y), dp.expo);
+}
+
+// Walk rows ordered by the chain's wind over the window, windiest first.  A chain's
+// next_cloud calls per window grow with its wind speed (the cloud lengths are x / ws;
+// correlation 0.84 between calls and the window-start wind pair's sum over 4,096 oracle
+// chain-days), and a walk wavefront runs as many iterations as the busiest of its 4
+// (16) chains: grouping chains of similar wind cuts the wavefronts' iterations by 11 %
+// (17 % at 16 chains per wavefront), and the busiest wavefronts are dispatched first.
+// Faulted chains last.  Bitonic sort of (key, chain) per tile of ORDER_TILE rows in LDS.
+// The walk's results do not depend on the order (each group walks its own chain).  The
+// try-0 candidate table is stored by walk row (candidates_kernel writes row rank[c]), so
+// a wavefront's candidate loads stay on shared cache lines as in chain order (read by
+// chain, the scattered rows made the 16-chain C3 walk 3.7x slower).
+constexpr uint32_t ORDER_TILE = 4096;
+__global__ __launch_bounds__(1024) void walk_order_kernel(StateView st, uint32_t n, SegView sg, PrevView prev)
+{
+    __shared__ unsigned long long v[ORDER_TILE];
+    const uint32_t t0 = blockIdx.x * ORDER_TILE;
+    for (uint32_t i = threadIdx.x; i < ORDER_TILE; i += blockDim.x) {
+        const uint32_t c = t0 + i;
+        uint32_t kb = 0;   // positive floats order as their bit patterns; 0 = faulted or padding
+        if (c < n) {
+            const bool ok = (prev.status ? prev.status[c] : st.status[c]) == 0;
+            const double w = prev.status ? prev.end_p1[2 * (size_t)n + c] + prev.end_p1[3 * (size_t)n + c]
+                                         : st.sb[S_WS][c] + st.sa[S_WS][c];
+            kb = ok && w > 0.0 ? __float_as_uint((float)w) : 0u;
+        }
+        // ascending order of the complement: larger key first, then the lower chain
+        v[i] = ~(((unsigned long long)kb << 32) | (0xFFFFFFFFu - c));
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= ORDER_TILE; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < ORDER_TILE; i += blockDim.x) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const unsigned long long a = v[i], b = v[l];
+                    if (((i & k) == 0) ? a > b : a < b) {
+                        v[i] = b;
+                        v[l] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    // the tile's real chains sort ahead of its padding (key 0, chain ids >= n)
+    for (uint32_t i = threadIdx.x; i < ORDER_TILE && t0 + i < n; i += blockDim.x) {
+        const uint32_t c = 0xFFFFFFFFu - (uint32_t)~v[i];
+        sg.order[t0 + i] = c;
+        sg.rank[c] = t0 + i;
+    }
 }
 
 // ---- lane-group primitives (DPP inside groups of G = 4, 8 or 16 lanes: one chain per group)
@@ -1174,8 +1228,10 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
     // behind the windiest chain of their wave (its duration is the longest chain's
     // call count either way; its footprint on the CUs shrinks).  Everything below
     // is the group's current chain, group-uniform.
-    uint32_t c = (blockIdx.x * blockDim.x + threadIdx.x) >> GSH;
-    bool live = c < n;
+    const uint32_t* order = sg.order;   // walk row -> chain (walk_order_kernel), or the identity
+    uint32_t r = (blockIdx.x * blockDim.x + threadIdx.x) >> GSH;   // the group's walk row
+    bool live = r < n;
+    uint32_t c = live && order ? order[r] : r;
     uint32_t status = 0xFFFFFFFFu;
     double ccb = 0.0, cca = 0.0, wsb = 0.0, wsa = 0.0;   // window-start cloud-cover and wind pairs
     int32_t fault = INT_MAX;
@@ -1243,7 +1299,7 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
     // call ncall0 + k's try-0 length: the table, or past it (the windiest chains) drawn here,
     // one per lane of the group per refill, as candidates_kernel would have
     auto cand_at = [&](uint32_t k) {
-        if (k < sg.kcap) return sg.cand[(size_t)k * n + c];
+        if (k < sg.kcap) return sg.cand[(size_t)k * n + r];   // stored by walk row
         const U4 b = keyed_block(dp.seed, chain0 + gid(dp.ids, c), (uint64_t)(ncall0 + k), TAG_CLOUD, 0);
         return pow_d(dp.alpha + dp.delta * u52(b.x, b.y), dp.expo);
     };
@@ -1353,8 +1409,9 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
                 finish_chain();
                 int v = 0;
                 if (p == 0) v = (int)atomicAdd(sg.walk_q, 1u);
-                c = groups + (uint32_t)__builtin_amdgcn_ds_bpermute(row0 << 2, v);   // the whole group is active here
-                live = c < n;
+                r = groups + (uint32_t)__builtin_amdgcn_ds_bpermute(row0 << 2, v);   // the whole group is active here
+                live = r < n;
+                c = live && order ? order[r] : r;
                 if (live) start_chain();
             }
         }
@@ -2194,6 +2251,10 @@ size_t scratch_layout(uint32_t n, uint32_t n_steps, void* base, SegView* v, size
         v->pool_short = v->pool_n + 2;
     }
     o += ALIGN;
+    if (v) v->order = (uint32_t*)(b + o);
+    o += align_up((size_t)n * 4);
+    if (v) v->rank = (uint32_t*)(b + o);
+    o += align_up((size_t)n * 4);
     if (v) v->ovf_first = (int32_t*)(b + o);
     o += align_up((size_t)n * 4);
     if (v) v->count = (uint32_t*)(b + o);
@@ -2252,6 +2313,7 @@ struct tmh_engine {
     uint32_t n_sites = 0;   // rows of the per-chain sites (0: the engine's one site)
     uint32_t walk_cpr = 1;  // chains per walk row (tmh_set_walk_chains_per_row)
     uint32_t walk_lanes = 0;  // lanes per chain in the walk (tmh_set_walk_lanes; 0: by batch size)
+    bool walk_order = true;   // walk rows windiest chain first (tmh_set_walk_order)
     // kernel timing (tmh_profile_*): event pairs per kernel, read and recycled
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[TMH_K_COUNT];
@@ -2524,6 +2586,13 @@ int tmh_set_walk_lanes(struct tmh_engine* eng, uint32_t lanes)
     return TMH_OK;
 }
 
+int tmh_set_walk_order(struct tmh_engine* eng, int on)
+{
+    if (!eng) return fail(TMH_E_INVAL, "NULL engine");
+    eng->walk_order = on != 0;
+    return TMH_OK;
+}
+
 int tmh_stream_create_cus(uint32_t cu_first, uint32_t cu_count, void** stream)
 {
     if (!stream) return fail(TMH_E_INVAL, "NULL stream out");
@@ -2739,6 +2808,13 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
         if (eng->dp.markov)
             hipLaunchKernelGGL(markov_cc_kernel, dim3(cb), dim3(256), 0, s, eng->kp, v, chain0, n_chains, n_steps,
                                pv.events, pv.n_events, sg.evd, prev);
+        // the walk rows' order (read by the candidates table's layout and the walk): set
+        // tmh_set_walk_order before a window's draws
+        if (eng->walk_order)
+            hipLaunchKernelGGL(walk_order_kernel, dim3((n_chains + ORDER_TILE - 1) / ORDER_TILE), dim3(1024), 0, s, v,
+                               n_chains, sg, prev);
+        else
+            sg.order = sg.rank = nullptr;
         hipEvent_t t_cand = eng->mark(s);
         hipLaunchKernelGGL(candidates_kernel, dim3(cb, sg.kcap), dim3(256), 0, s, eng->dp, v, chain0, n_chains, sg,
                            prev);
@@ -2756,6 +2832,7 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
 #define WALK(Q, GG)                                                                                           \
     hipLaunchKernelGGL((segments_kernel<Q, GG>), wg, wt, wlds, s, eng->dp, v, chain0, n_chains, step0, n_steps, \
                        eng->gp.clock, pv.events, pv.n_events, sg, prev)
+    if (!eng->walk_order) sg.order = sg.rank = nullptr;   // (the draws phase wrote order / rank)
     const bool q = rows < n_chains;   // groups take queued chains
     if (G == 4) { if (q) WALK(true, 4); else WALK(false, 4); }
     else if (G == 8) { if (q) WALK(true, 8); else WALK(false, 8); }
