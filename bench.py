@@ -41,6 +41,12 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+# HIP maps streams round-robin onto GPU_MAX_HW_QUEUES hardware queues (4 by default), and
+# a queue runs its packets in order across the streams that share it: with 4, the
+# expansion stream shared a queue with the commit stream and every expansion waited for
+# the previous batch's fixup + commit (kernel trace: 120-140 us gaps between expansions;
+# same box: 1.74-1.76 ms per C2 batch with 4 queues, 1.49-1.51 with 8, 1.47-1.51 with 16).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -162,6 +168,8 @@ def parse():
                          "that take the next chain when theirs is done")
     ap.add_argument("--walk-lanes", type=int, default=0,
                     help="lanes per chain in the segment walk (tmh_set_walk_lanes: 4, 8 or 16; 0 = by batch size: 16 up to 8,192 chains, else 4)")
+    ap.add_argument("--walk-order", type=int, default=1,
+                    help="walk rows windiest chain first (tmh_set_walk_order, 1) or in chain order (0)")
     ap.add_argument("--walk-cus", type=int, default=0,
                     help="gated schedule: run the segment walks on CU-mask bits 0 .. K-1 only (a CU-masked HIP "
                          "stream, tmh_stream_create_cus; 0 = all CUs)")
@@ -329,18 +337,38 @@ def main():
         _lib.check(L.tmh_set_walk_chains_per_row(sim._eng, args.walk_cpr))
     if args.walk_lanes:
         _lib.check(L.tmh_set_walk_lanes(sim._eng, args.walk_lanes))
+    if hasattr(L, "tmh_set_walk_order"):
+        _lib.check(L.tmh_set_walk_order(sim._eng, args.walk_order))
 
     nwin = (secs + win - 1) // win
     prio_lo, prio_hi = torch.cuda.Stream.priority_range()
 
     class Ctx:   # one batch in flight: its own state, plan, scratch, outputs and HIP streams
+        # The context's own streams are created on first use: the gated schedule runs on
+        # shared streams, and every extra stream shares one of HIP's few hardware queues
+        # with a busy one (a queue runs its packets in order, across streams).
+        @property
+        def stream(self):
+            if self._stream is None:
+                self._stream = torch.cuda.Stream(dev)
+            return self._stream
+
+        @property
+        def sptr(self):
+            return C.c_void_p(self.stream.cuda_stream)
+
+        @property
+        def wstream(self):   # the walk runs on a stream of its own, high priority by default
+            if self._wstream is None:
+                self._wstream = torch.cuda.Stream(dev, priority=prio_hi if args.walk_priority == "high" else prio_lo)
+            return self._wstream
+
+        @property
+        def wptr(self):
+            return C.c_void_p(self.wstream.cuda_stream)
+
         def __init__(self):
-            self.stream = torch.cuda.Stream(dev)
-            self.sptr = C.c_void_p(self.stream.cuda_stream)
-            # the walk runs on a stream of its own, high priority by default: its
-            # long-lived workgroups take CU slots as the expansion's short ones retire
-            self.wstream = torch.cuda.Stream(dev, priority=prio_hi if args.walk_priority == "high" else prio_lo)
-            self.wptr = C.c_void_p(self.wstream.cuda_stream)
+            self._stream = self._wstream = None
             self.walked = torch.cuda.Event()
             self.done = torch.cuda.Event()
             self.kernel_done = torch.cuda.Event()
@@ -610,9 +638,10 @@ def main():
     def exchange():
         """stats mode: the one cross-GPU step, an RCCL all-reduce of the aggregate statistics"""
         estream.synchronize()
-        for cx in ctxs:
-            cx.stream.synchronize()
-            cx.wstream.synchronize()
+        for cx in ctxs:   # (streams a schedule never created have nothing to wait for)
+            for st_ in (cx._stream, cx._wstream):
+                if st_ is not None:
+                    st_.synchronize()
         hist = sum(cx.hist for cx in ctxs)
         acc = torch.stack([cx.acc for cx in ctxs])
         tot = dict(energy_pv=acc[:, 0].sum(), energy_meter=acc[:, 1].sum(), energy_residual=acc[:, 2].sum(),
@@ -730,7 +759,7 @@ def main():
                    "batches_in_flight": len(ctxs), "staggered": bool(args.stagger and nwin == 1),
                    "construction_on": args.build_on, "walk_priority": args.walk_priority,
                    "schedule": args.schedule if (args.stagger and nwin == 1 and len(ctxs) >= 3) else None,
-                   "walks_in_flight": W, "walk_cus": args.walk_cus or "all", "other_cus": args.other_cus if args.walk_cus else "all",
+                   "walks_in_flight": W, "walk_order": bool(args.walk_order), "walk_cus": args.walk_cus or "all", "other_cus": args.other_cus if args.walk_cus else "all",
                    "walk_chains_per_row": args.walk_cpr, "walk_lanes": args.walk_lanes or "auto", "build_ahead": A,
                    "minutes_ahead": bool(args.minutes_ahead), "commit_stream": bool(args.commit_stream),
                    "compacted_windows": bool(args.compact and args.mode == "stats" and nwin > 1)},
