@@ -41,12 +41,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-# HIP maps streams round-robin onto GPU_MAX_HW_QUEUES hardware queues (4 by default), and
-# a queue runs its packets in order across the streams that share it: with 4, the
-# expansion stream shared a queue with the commit stream and every expansion waited for
-# the previous batch's fixup + commit (kernel trace: 120-140 us gaps between expansions;
-# same box: 1.74-1.76 ms per C2 batch with 4 queues, 1.49-1.51 with 8, 1.47-1.51 with 16).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -168,6 +163,12 @@ def parse():
                          "that take the next chain when theirs is done")
     ap.add_argument("--walk-lanes", type=int, default=0,
                     help="lanes per chain in the segment walk (tmh_set_walk_lanes: 4, 8 or 16; 0 = by batch size: 16 up to 8,192 chains, else 4)")
+    ap.add_argument("--hw-queues", type=int, default=16,
+                    help="GPU_MAX_HW_QUEUES for this process (set before HIP starts; 0 = leave the environment's). "
+                         "HIP maps streams round-robin onto that many hardware queues and a queue runs its "
+                         "packets in order across the streams sharing it: with HIP's default 4 the expansion "
+                         "stream shares a queue with another pipeline stream and waits for its kernels (same "
+                         "box: 1.74-1.76 ms per C2 batch with 4 queues, 1.49-1.51 with 8, 1.47-1.51 with 16)")
     ap.add_argument("--walk-order", type=int, default=1,
                     help="walk rows windiest chain first (tmh_set_walk_order, 1) or in chain order (0)")
     ap.add_argument("--walk-cus", type=int, default=0,
@@ -284,6 +285,8 @@ def pmc_record(args, n, launch_secs):
 
 def main():
     args = parse()
+    if args.hw_queues:   # before anything starts the HIP runtime (it reads this once)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return launch_ranks(args.gpus, sys.argv[1:])
     import torch
@@ -759,7 +762,7 @@ def main():
                    "batches_in_flight": len(ctxs), "staggered": bool(args.stagger and nwin == 1),
                    "construction_on": args.build_on, "walk_priority": args.walk_priority,
                    "schedule": args.schedule if (args.stagger and nwin == 1 and len(ctxs) >= 3) else None,
-                   "walks_in_flight": W, "walk_order": bool(args.walk_order), "walk_cus": args.walk_cus or "all", "other_cus": args.other_cus if args.walk_cus else "all",
+                   "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"), "walks_in_flight": W, "walk_order": bool(args.walk_order), "walk_cus": args.walk_cus or "all", "other_cus": args.other_cus if args.walk_cus else "all",
                    "walk_chains_per_row": args.walk_cpr, "walk_lanes": args.walk_lanes or "auto", "build_ahead": A,
                    "minutes_ahead": bool(args.minutes_ahead), "commit_stream": bool(args.commit_stream),
                    "compacted_windows": bool(args.compact and args.mode == "stats" and nwin > 1)},
