@@ -169,6 +169,9 @@ def parse():
                          "packets in order across the streams sharing it: with HIP's default 4 the expansion "
                          "stream shares a queue with another pipeline stream and waits for its kernels (same "
                          "box: 1.74-1.76 ms per C2 batch with 4 queues, 1.49-1.51 with 8, 1.47-1.51 with 16)")
+    ap.add_argument("--timeline", action="store_true",
+                    help="gated schedule: time each batch's build, walk and expansion with HIP events and add the "
+                         "expansion stream's idle gaps (and what it waited for) to the JSON line")
     ap.add_argument("--walk-order", type=int, default=1,
                     help="walk rows windiest chain first (tmh_set_walk_order, 1) or in chain order (0)")
     ap.add_argument("--walk-cus", type=int, default=0,
@@ -567,32 +570,46 @@ def main():
         if args.minutes_ahead:   # the minute table needs the draws, not the walk
             _lib.check(L.tmh_expand_part(*expand_args(cx), _lib.EXPAND_MINUTES, bst_p))
         cx.done.record(bst)
+        tl_mark("built", j, bst)
+
+    tl = {}   # --timeline: per-batch HIP timing events (build done, walk start / end, expansion start / end)
+
+    def tl_mark(key, j, stream):
+        if args.timeline:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(stream)
+            tl.setdefault(key, {})[j] = e
 
     def g_walk(j):
         cx = ctxs[j % len(ctxs)]
         wst = wsts[j % W]
         wst.wait_event(cx.done)
+        tl_mark("walk0", j, wst)
         _lib.check(L.tmh_walk_part(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs,
                                    C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
                                    cx.scratch.numel(), None, 0, _lib.WALK_SEGMENTS, C.c_void_p(wst.cuda_stream)))
         cx.walked.record(wst)
+        tl_mark("walk1", j, wst)
 
     def g_expand(j):
         cx = ctxs[j % len(ctxs)]
-        estream.wait_event(cx.walked)
+        es, ep = estream, eptr
+        es.wait_event(cx.walked)
         args_ = expand_args(cx)
+        tl_mark("exp0", j, es)
         _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_KERNEL | (_lib.EXPAND_NO_MINUTES if args.minutes_ahead else 0),
-                                     eptr))
+                                     ep))
+        tl_mark("exp1", j, es)
         if cx.expanded is None:
             cx.expanded = torch.cuda.Event()
         if args.commit_stream:   # fixup + commit beside the next expansion
-            cx.kernel_done.record(estream)
+            cx.kernel_done.record(es)
             cst.wait_event(cx.kernel_done)
             _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_COMMIT, C.c_void_p(cst.cuda_stream)))
             cx.expanded.record(cst)
         else:
-            _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_COMMIT, eptr))
-            cx.expanded.record(estream)
+            _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_COMMIT, ep))
+            cx.expanded.record(es)
 
     def run_gated(k0, cnt):
         """W walks in flight (W + 2 contexts): when the walk of batch k ends, the
@@ -640,7 +657,7 @@ def main():
 
     def exchange():
         """stats mode: the one cross-GPU step, an RCCL all-reduce of the aggregate statistics"""
-        estream.synchronize()
+        torch.cuda.synchronize()
         for cx in ctxs:   # (streams a schedule never created have nothing to wait for)
             for st_ in (cx._stream, cx._wstream):
                 if st_ is not None:
@@ -773,6 +790,14 @@ def main():
         "effective_trace_gbs": (TB * n * secs / (elapsed / args.steps) / 1e9) if args.mode == "trace" else None,
         "faulted_chains": bad,
     }
+    if args.timeline and "exp0" in tl:
+        ks = sorted(k for k in tl["exp0"] if k >= args.warmup and k in tl["exp1"] and k + 1 in tl.get("exp0", {}))
+        gaps = [tl["exp1"][k].elapsed_time(tl["exp0"][k + 1]) for k in ks]
+        late = [tl["exp1"][k].elapsed_time(tl["walk1"][k + 1]) for k in ks if k + 1 in tl.get("walk1", {})]
+        wdur = [tl["walk0"][k].elapsed_time(tl["walk1"][k]) for k in ks if k in tl.get("walk0", {})]
+        bwait = [tl["built"][k].elapsed_time(tl["walk0"][k]) for k in ks if k in tl.get("built", {}) and k in tl.get("walk0", {})]
+        line["timeline"] = {"expansion_gap_ms": gaps, "walk_end_after_prev_expansion_ms": late,
+                            "walk_ms": wdur, "walk_start_after_build_ms": bwait}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args, kw)
     if rank == 0:
