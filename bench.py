@@ -169,6 +169,10 @@ def parse():
                          "packets in order across the streams sharing it: with HIP's default 4 the expansion "
                          "stream shares a queue with another pipeline stream and waits for its kernels (same "
                          "box: 1.74-1.76 ms per C2 batch with 4 queues, 1.49-1.51 with 8, 1.47-1.51 with 16)")
+    ap.add_argument("--secondary", default=None,
+                    help="after the headline measurement (one GPU only), run the other configurations in child "
+                         "processes and add their lines under 'secondary': all | none | a comma list of "
+                         "c2_fp64,c3,c4,c5 (default: all for the C2 fp32 run with its CPU baseline, else none)")
     ap.add_argument("--timeline", action="store_true",
                     help="gated schedule: time each batch's build, walk and expansion with HIP events and add the "
                          "expansion stream's idle gaps (and what it waited for) to the JSON line")
@@ -218,6 +222,9 @@ def parse():
     if a.commit_stream is None:
         a.commit_stream = int(a.walks > 1)
     a.mode = a.mode or ("trace" if a.workload == "c2" else "stats")
+    if a.secondary is None:
+        # the full report (the default C2 run with its CPU baseline) carries them; quick runs do not
+        a.secondary = "all" if (a.workload == "c2" and a.precision == "fp32" and not a.no_cpu_baseline) else "none"
     a.cc = a.cc or ("markov" if c5 else "faithful")
     a.window = min(a.window or (86400 if (c5 or c4) else a.seconds), a.seconds)
     a.start = a.start or ("2019-01-01 00:00:00" if c4 else "2019-09-05 00:00:00")
@@ -226,6 +233,41 @@ def parse():
     a.build_on = a.build_on or ("walk" if a.workload == "c2" else "expand")
     a.walk_priority = a.walk_priority or ("normal" if a.workload == "c2" else "high")
     return a
+
+
+SECONDARY = {   # --secondary: the other BASELINE.json configs, each in a child process of its own
+    "c2_fp64": ["--precision", "fp64", "--steps", "10", "--warmup", "3"],
+    "c3": ["--workload", "c3", "--steps", "2", "--warmup", "1"],
+    "c4": ["--workload", "c4", "--steps", "1", "--warmup", "1"],
+    "c5": ["--workload", "c5", "--steps", "1", "--warmup", "1"],
+}
+
+
+def secondary_lines(args):
+    """The fp64 C2 line (the reference's precision) and the C3 / C4 / C5 stats-mode lines,
+    each a fresh bench.py process on this GPU after the headline measurement, so the
+    default run reports every configuration's rate and roofline.  A failed one reports
+    its error; the headline line is printed either way."""
+    import subprocess
+    out = {}
+    for name, extra in SECONDARY.items():
+        if args.secondary != "all" and name not in args.secondary.split(","):
+            continue
+        cmd = [sys.executable, os.path.abspath(__file__), "--no-cpu-baseline", "--secondary", "none",
+               "--hw-queues", str(args.hw_queues)] + extra
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+            d = json.loads(r.stdout.strip().splitlines()[-1])
+            roof = d.get("roofline", {})
+            out[name] = {"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"],
+                         "steps": d["steps"], "dtype": d["dtype"], "workload": d["config"]["workload"],
+                         "roofline": {k: roof.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
+                                                               "kernel_ms")},
+                         "roofline_alone": roof.get("alone"), "faulted_chains": d.get("faulted_chains"),
+                         "chain_seconds_live": d.get("chain_seconds_live")}
+        except Exception as e:   # noqa: BLE001 - report, never lose the headline line
+            out[name] = {"error": f"{type(e).__name__}: {e}"[:300]}
+    return out
 
 
 def cpu_baseline(args, kw):
@@ -800,6 +842,10 @@ def main():
                             "walk_ms": wdur, "walk_start_after_build_ms": bwait}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args, kw)
+    if rank == 0 and world == 1 and args.secondary != "none":
+        del ctxs   # the children need the memory
+        torch.cuda.empty_cache()
+        line["secondary"] = secondary_lines(args)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
