@@ -237,9 +237,9 @@ def parse():
 
 SECONDARY = {   # --secondary: the other BASELINE.json configs, each in a child process of its own
     "c2_fp64": ["--precision", "fp64", "--steps", "10", "--warmup", "3"],
-    "c3": ["--workload", "c3", "--steps", "2", "--warmup", "1"],
-    "c4": ["--workload", "c4", "--steps", "1", "--warmup", "1"],
-    "c5": ["--workload", "c5", "--steps", "1", "--warmup", "1"],
+    "c3": ["--workload", "c3", "--steps", "4", "--warmup", "1"],
+    "c4": ["--workload", "c4", "--steps", "2", "--warmup", "1"],
+    "c5": ["--workload", "c5", "--steps", "2", "--warmup", "1"],
 }
 
 
