@@ -256,7 +256,7 @@ def test_geometry_table_vs_oracle():
         g = np.zeros(16)
         O.lib().orc_geometry(C.byref(P), int(utc[s]), int(cal[s, 4]), int(cal[s, 5]), g.ctypes.data_as(C.c_void_p))
         # oracle geom_t order: cosz csi_max ghi_cs i0h i0 knc am disc_ok cos_zen rb dni_extra term2 gfac cos_aoi f1 f2
-        mine = tab[s, [4, 5, 6, 7, 8, 9, 10, 11, 4, 12, 13, 14, 15, 16, 17, 18]]
+        mine = tab[s, [4, 5, 6, 7, 8, 9, 10, 18, 4, 12, 13, 14, 15, 16, 17, 11]]   # G_DISCOK 18, G_F2 11
         m = np.isfinite(g)
         np.testing.assert_allclose(mine[m], g[m], rtol=1e-11, atol=1e-13)
     np.testing.assert_array_equal(tab[:, 0], cal[:, 3] / 60.0)

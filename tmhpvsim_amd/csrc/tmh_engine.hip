@@ -359,7 +359,7 @@ __global__ __launch_bounds__(256) void geom_kernel(GParams gp, int64_t step0, ui
         o32[fc[i]] = 1.0f - f;
         o32[fc[i] + 1] = f;
     }
-    for (int i = G_COSZ; i <= G_F2; ++i) o32[i + G32] = (float)g[i];
+    for (int i = G_COSZ; i <= G_LAST; ++i) o32[i + G32] = (float)g[i];
     o32[G_FLAGS + G32] = __uint_as_float(fl);
     o32[G_I0H + G32] = (float)(1.0 / g[G_I0H]);   // fp32 path multiplies by reciprocals
     o32[G_DNIEXTRA + G32] = (float)(1.0 / g[G_DNIEXTRA]);

@@ -65,20 +65,22 @@ enum : uint32_t { FL_DAY = 1, FL_HOUR = 2, FL_MIN = 4, FL_NIGHT = 8, FL_DISCOK =
 // clock/geometry table row (TMH_GEOM_FIELDS = 20)
 enum {
     G_MINF = 0, G_HOURF = 1, G_DAYF = 2, G_FLAGS = 3, G_COSZ = 4, G_CSIMAX = 5, G_GHICS = 6,
-    G_I0H = 7, G_I0 = 8, G_KNC = 9, G_AM = 10, G_DISCOK = 11, G_RB = 12, G_DNIEXTRA = 13,
-    G_TERM2 = 14, G_GFAC = 15, G_COSAOI = 16, G_F1 = 17, G_F2 = 18
+    G_I0H = 7, G_I0 = 8, G_KNC = 9, G_AM = 10, G_F2 = 11, G_RB = 12, G_DNIEXTRA = 13,
+    G_TERM2 = 14, G_GFAC = 15, G_COSAOI = 16, G_F1 = 17, G_DISCOK = 18,
+    G_LAST = 18   // DISC's zenith test last: the fp32 single-site kernels read it as FL_DISCOK, so their
+                  // scalar loads of a row stop one field early (3 s_loads a second, not 6 around a hole)
 };
 // fp32 row (ROW32 = 22 floats, the kernels' scalar loads): each clock fraction
 // beside its complement 1 - f (rounded in fp32 exactly as the kernels would),
 // 8-byte aligned pairs, so an interpolation f a + (1 - f) b is one packed
-// multiply on an SGPR pair plus an add; then flags and G_COSZ..G_F2, i.e. the
+// multiply on an SGPR pair plus an add; then flags and G_COSZ..G_LAST, i.e. the
 // fp64 row's field G_X (X >= FLAGS) sits at G_X + G32.  Kept compact: every
 // field is held in SGPRs through the step.
 enum { G32_MINF_C = 0, G32_MINF = 1, G32_HOURF_C = 2, G32_HOURF = 3, G32_DAYF_C = 4, G32_DAYF = 5, G32 = 3 };
 #define ROW32 22
 template <typename R>
 constexpr int row_w() { return sizeof(R) == 8 ? ROW : ROW32; }
-template <typename R>   // the row as the fp64 field layout (G_FLAGS..G_F2) sees it
+template <typename R>   // the row as the fp64 field layout (G_FLAGS..G_LAST) sees it
 constexpr int row_off() { return sizeof(R) == 8 ? 0 : G32; }
 
 enum { S_CC = 0, S_CLEAR_DAY = 1, S_CLOUDY_HOUR = 2, S_CLOUDY_NOISE = 3, S_CLEAR_NOISE = 4, S_WS = 5 };
@@ -887,7 +889,7 @@ __device__ __forceinline__ SiteK site_k(const double* site)
     return k;
 }
 
-// geometry row fields G_COSZ..G_F2 of one site and step (fp64); returns true
+// geometry row fields G_COSZ..G_LAST of one site and step (fp64); returns true
 // when the clear-sky GHI is 0 (pv = 0 whatever the csi).  FULL = false stops
 // there at night (the per-chain-second path); FULL fills every field.
 template <bool FULL, bool F32 = false>
@@ -996,7 +998,7 @@ __device__ __forceinline__ void site_row(const double* g, const double* sun, R* 
 {
     R* row = row_base + row_off<R>();
 #pragma unroll
-    for (int i = G_COSZ; i <= G_F2; ++i) row[i] = (R)g[i];
+    for (int i = G_COSZ; i <= G_LAST; ++i) row[i] = (R)g[i];
     if constexpr (sizeof(R) == 4) {
         row[G_I0H] = (float)(1.0 / g[G_I0H]);
         row[G_DNIEXTRA] = (float)sun[SUN_RDNIX];
