@@ -659,6 +659,11 @@ def main():
         of k + W + 1 are released together."""
         end = k0 + cnt
         for j in range(k0, min(k0 + A, end)):
+            # the run's first walk is the pipeline's fill latency (its expansion waits for it with
+            # nothing else to do): chain order, whose windiest wavefront is shorter than the wind
+            # order's (four windy chains); the wind order for the rest, which run beside expansions
+            if args.walk_order and hasattr(L, "tmh_set_walk_order"):
+                _lib.check(L.tmh_set_walk_order(sim._eng, 0 if (j == k0 and W > 1) else 1))
             g_build(j, None)
         for j in range(k0, min(k0 + W, end)):
             g_walk(j)

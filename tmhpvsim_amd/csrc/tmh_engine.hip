@@ -1042,7 +1042,23 @@ __device__ __forceinline__ WinClock win_clock(const tmh_clock& ck, int64_t W0)
     return w;
 }
 
-__device__ __forceinline__ void fractions_at(const WinClock& w, int32_t j, double& hour_f, double& day_f)
+// hour_f for every second of an hour (minute 60 + second): the walk's table in LDS
+constexpr int HOUR_S = 3600;
+__device__ __forceinline__ void hour_fractions(double* tab)
+{
+    for (int i = threadIdx.x; i < HOUR_S; i += blockDim.x) {
+        double mf, hf, df;
+        clock_fractions(0, i / 60, i % 60, mf, hf, df);   // hour_f depends on (minute, second) only
+        tab[i] = hf;
+    }
+    __syncthreads();
+}
+
+// hour_f from the table (hf_tab, hour_fractions), day_f = div_exact(hour + hour_f, 24)
+// as clock_fractions computes it: the same bits, without the minute / second split and
+// the first two exact divisions per call
+__device__ __forceinline__ void fractions_at(const WinClock& w, int32_t j, const double* hf_tab, double& hour_f,
+                                             double& day_f)
 {
     int32_t sod = w.sod0 + j;
     if (w.shifts) {   // wave-uniform: most windows (no DST change ahead) skip the shift table
@@ -1052,9 +1068,9 @@ __device__ __forceinline__ void fractions_at(const WinClock& w, int32_t j, doubl
     }
     sod %= 86400;
     if (sod < 0) sod += 86400;
-    const int hour = sod / 3600, minute = (sod / 60) % 60, second = sod % 60;
-    double min_f;
-    clock_fractions(hour, minute, second, min_f, hour_f, day_f);
+    const int hour = sod / HOUR_S;
+    hour_f = hf_tab[sod - HOUR_S * hour];
+    day_f = div_exact(hour + hour_f, 24.0, 1.0 / 24.0);
 }
 
 // try-0 candidate lengths of the next kcap next_cloud calls of every chain:
@@ -1222,6 +1238,8 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
     const int64_t W1 = W0 + nsteps;
     const uint32_t nev = min(*n_events, ev_cap_dev(nsteps));
     const WinClock wck = win_clock(ck, W0);
+    __shared__ double hf_tab[HOUR_S];   // 28.8 KB: the calls' hour fractions by table
+    hour_fractions(hf_tab);
     // Groups take chains: group r starts with chain r, and a group whose chain is done
     // takes the next unstarted one from the window's queue (chains groups.. n - 1), so
     // with fewer groups than chains the walk's waves stay busy instead of idling
@@ -1435,7 +1453,7 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
             fetch_event();
         }
         double hf, df;
-        fractions_at(wck, (int32_t)(e - W0), hf, df);
+        fractions_at(wck, (int32_t)(e - W0), hf_tab, hf, df);
         const double hh = interp(ccb, cca, hf);
         const double h = 0.95 < hh ? 0.95 : hh;   // update_parameters
         const double ws = interp(wsb, wsa, df);
