@@ -14,6 +14,7 @@ TICK=$!
 trap "kill $TICK" EXIT
 if [ "$WHAT" = c2 ]; then
   bash scripts/pmc_workload.sh ${TAG}_c2 c2 4096 86400 fp32 trace faithful -- --steps 1 --warmup 1 --pipeline 1 || exit 1
+  bash scripts/pmc_workload.sh ${TAG}_c2f64 c2 4096 86400 fp64 trace faithful -- --precision fp64 --steps 1 --warmup 1 --pipeline 1 || exit 1
   cp gpurun_out/pmc_kernels.json profiles/pmc_kernels.json
   timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/bench_${TAG}_c2.json 2> gpurun_out/bench_${TAG}_c2.err || exit 1
   cat gpurun_out/bench_${TAG}_c2.json
@@ -25,7 +26,7 @@ if [ "$WHAT" = c2 ]; then
   rm -rf gpurun_out/prof_$TAG
 else
   bash scripts/pmc_workload.sh ${TAG}_c3 c3 1048576 86400 fp32 stats faithful -- --workload c3 --steps 1 --warmup 1 || exit 1
-  bash scripts/pmc_workload.sh ${TAG}_c5 c5 65536 86400 fp32 stats markov -- --workload c5 --steps 1 --warmup 1 || exit 1
+  bash scripts/pmc_workload.sh ${TAG}_c5 c5 65536 86400 fp32 stats markov compact=1 -- --workload c5 --steps 1 --warmup 1 || exit 1
   PMC_PASS_TIMEOUT=240 bash scripts/pmc_workload.sh ${TAG}_c4 c4 16384 86400 fp32 stats faithful -- --workload c4 --steps 1 --warmup 1 || exit 1
   cp gpurun_out/pmc_kernels.json profiles/pmc_kernels.json
   for wl in "c3 --steps 4 --warmup 1" "c4 --steps 2 --warmup 1" "c5 --steps 2 --warmup 1"; do
