@@ -28,13 +28,14 @@ W1 = np.uint32(0xBB67AE85)
 MASK32 = np.uint64(0xFFFFFFFF)
 
 # keyed-mode draw families (ctr1 = tag << 28 | sub)
-TAG_STEP = 1        # injected-mode bookkeeping only (per-second draws are TAG_STEP2)
+TAG_STEP = 1        # injected-mode bookkeeping only (per-second draws are TAG_METER4 / TAG_NOISE4)
 TAG_BOUNDARY = 2    # sub 0 day (clear_day, ws), 1 hour (cc, clear_day), 2 minute (cloudy, clear noise)
 TAG_CLOUD = 3       # ctr0 = next_cloud call number (0 = ctor), sub = try >> 1, half = try & 1
 TAG_INIT = 4        # step 0, sub = draw >> 1, half = draw & 1 (14 ctor draws)
 TAG_INIT_CLOUD = 5  # ctor next_cloud (call 0): ctr0 = 0, sub = try >> 1, half = try & 1
 TAG_INIT_SEC = 6    # ctor start offset draw: sub 0, half 0
-TAG_STEP2 = 7       # per-second draws: ctr0 = step >> 1, words (x, y) = (noise, meter) of the even step, (z, w) of the odd; u = (w + 1/2) 2^-32
+TAG_METER4 = 8      # per-second meter draws: ctr0 = step >> 2, word step & 3; u = (w + 1/2) 2^-32
+TAG_NOISE4 = 9      # per-second noise draws: the same layout (a night second draws no noise word)
 
 
 def philox4x32_10(ctr, key):

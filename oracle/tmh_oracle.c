@@ -51,7 +51,7 @@ void orc_T_hist(uint64_t* out, int reset)
 
 enum { ST_OK = 0, ST_NAMEERROR_INIT = 1, ST_ASSERT_BINARY = 2, ST_SIGMA_OVERFLOW = 3,
        ST_U_EXHAUSTED = 4 };
-enum { TAG_STEP = 1, TAG_BOUNDARY = 2, TAG_CLOUD = 3, TAG_INIT = 4, TAG_INIT_CLOUD = 5, TAG_STEP2 = 7,
+enum { TAG_STEP = 1, TAG_BOUNDARY = 2, TAG_CLOUD = 3, TAG_INIT = 4, TAG_INIT_CLOUD = 5, TAG_METER4 = 8, TAG_NOISE4 = 9,
        TAG_INIT_SEC = 6 };
 enum { S_CC = 0, S_CLEAR_DAY = 1, S_CLOUDY_HOUR = 2, S_CLOUDY_NOISE = 3, S_CLEAR_NOISE = 4,
        S_WS = 5 };
@@ -124,16 +124,21 @@ static double keyed_u(uint64_t seed, uint64_t chain, uint64_t step, uint32_t tag
     return half ? u52(o[2], o[3]) : u52(o[0], o[1]);
 }
 
-/* per-second draws: one block per step pair p = step >> 1, 32-bit midpoint
- * uniforms (w + 1/2) 2^-32; (x, y) = (noise, meter) of step 2p, (z, w) of 2p + 1 */
-static void step_u(uint64_t seed, uint64_t chain, uint64_t step, double* ue, double* um)
+/* per-second draws: two streams, the noise's (TAG_NOISE4) and the meter's (TAG_METER4),
+ * one block per four steps g = step >> 2, word step & 3; 32-bit midpoint uniforms
+ * (w + 1/2) 2^-32 (the device's keyed_block + word_of, tmh_math.h) */
+static uint32_t step_word(uint64_t seed, uint64_t chain, uint64_t step, uint32_t tag)
 {
-    uint32_t c[4] = {(uint32_t)(step >> 1), (uint32_t)TAG_STEP2 << 28, (uint32_t)chain, (uint32_t)(chain >> 32)};
+    uint32_t c[4] = {(uint32_t)(step >> 2), tag << 28, (uint32_t)chain, (uint32_t)(chain >> 32)};
     uint32_t k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)}, o[4];
     philox4x32_10(c, k, o);
-    const int odd = (int)(step & 1);
-    *ue = ((double)o[odd ? 2 : 0] + 0.5) * 0x1p-32;
-    *um = ((double)o[odd ? 3 : 1] + 0.5) * 0x1p-32;
+    return o[step & 3];
+}
+
+static void step_u(uint64_t seed, uint64_t chain, uint64_t step, double* ue, double* um)
+{
+    *ue = ((double)step_word(seed, chain, step, TAG_NOISE4) + 0.5) * 0x1p-32;
+    *um = ((double)step_word(seed, chain, step, TAG_METER4) + 0.5) * 0x1p-32;
 }
 
 /* --------------------------------------------------------------- variates */

@@ -815,8 +815,9 @@ __device__ __forceinline__ bool redo_second(const KParams& kp, const DrawParams&
     uint32_t k = jr_end;   // the segment holding the step: first next-call step > step, at or before the block's last
     while (k > 0 && (int64_t)rec_at(sg, c, k - 1).y > step) --k;
     const bool covered = step < (int64_t)rec_at(sg, c, k).x;
-    const U4 pb = keyed_block(kp.seed, chain0 + gid(kp.ids, c), (uint64_t)step >> 1, TAG_STEP2, 0);
-    const bool odd = step & 1;
+    const uint64_t gch = chain0 + gid(kp.ids, c);   // the step's noise and meter words (TAG_NOISE4 / TAG_METER4)
+    const uint32_t wn = word_of(keyed_block(kp.seed, gch, (uint64_t)step >> 2, TAG_NOISE4, 0), (uint32_t)step & 3u);
+    const uint32_t wm = word_of(keyed_block(kp.seed, gch, (uint64_t)step >> 2, TAG_METER4, 0), (uint32_t)step & 3u);
     LaneSite ls{};
     if constexpr (SITES) {
         ls.k = site_k(kp.sites + (size_t)gid(kp.ids, c) * 8);
@@ -834,8 +835,8 @@ __device__ __forceinline__ bool redo_second(const KParams& kp, const DrawParams&
         const uint32_t fl = __float_as_uint(row[G_FLAGS + G32]) & ~(uint32_t)FL_NIGHT;
         uint32_t flp = __float_as_uint(row[G_FLAGS + G32]);
         if constexpr (SITES) flp = lane_flags(fl, lane_row<float>(ls, sun + (size_t)j * SUN_W, kp.module, row), row);
-        second_body<float>(kp, kp.pvf, row, flp, f, covered, noise_z<float>(odd ? pb.z : pb.x),
-                           meter_w<float>(odd ? pb.w : pb.y), csi, pv32, m, r, risky);
+        second_body<float>(kp, kp.pvf, row, flp, f, covered, noise_z<float>(wn), meter_w<float>(wm), csi, pv32, m, r,
+                           risky);
         meter32 = m;
     }
     if (!risky) return false;
@@ -847,7 +848,7 @@ __device__ __forceinline__ bool redo_second(const KParams& kp, const DrawParams&
         for (int i = 0; i < ROW; ++i) row[i] = tab64[(size_t)j * ROW + i];
         if constexpr (SITES) lane_row<double>(ls, sun + (size_t)j * SUN_W, kp.module, row);
         double csi, pv, m, r;
-        second_body<double>(kp, kp.pvf, row, 0u, f, covered, noise_z<double>(odd ? pb.z : pb.x), 0.0, csi, pv, m, r,
+        second_body<double>(kp, kp.pvf, row, 0u, f, covered, noise_z<double>(wn), 0.0, csi, pv, m, r,
                             risky);
         pv64 = (float)pv;
     }
@@ -902,6 +903,8 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
         ls.linke = kp.site_linke ? kp.site_linke + (size_t)(live ? gid(kp.ids, c) : 0) * 12 : nullptr;
         ls.tl_doy = -1;
     }
+    uint64_t grp = ~0ull;   // the per-second draws' current four-step group and its two blocks
+    U4 bn{0u, 0u, 0u, 0u}, bm{0u, 0u, 0u, 0u};
     for (uint32_t j = 0; j < nsteps; ++j) {
         const uint64_t step = (uint64_t)(step0 + j);
         const float* r32 = tab32 + (size_t)j * ROW32;
@@ -950,13 +953,18 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
                 else ch.sec += 1;
             }
             if (ch.status == 0) {
-                // keyed: one Philox block per step pair, 32-bit words;
-                // the meter is its own process in the reference: always keyed
-                const U4 pb = keyed_block(kp.seed, chain, (uint64_t)step >> 1, TAG_STEP2, 0);
-                const bool odd = step & 1;
-                R z = noise_z<R>(odd ? pb.z : pb.x);
+                // keyed: the noise's and the meter's streams, one Philox block per four
+                // steps each, 32-bit words; the meter is its own process in the
+                // reference: always keyed.  Drawn again when the step's group changes.
+                if ((uint64_t)step >> 2 != grp) {
+                    grp = (uint64_t)step >> 2;
+                    bn = keyed_block(kp.seed, chain, grp, TAG_NOISE4, 0);
+                    bm = keyed_block(kp.seed, chain, grp, TAG_METER4, 0);
+                }
+                const uint32_t wn = word_of(bn, (uint32_t)step & 3u);
+                R z = noise_z<R>(wn);
                 double z64 = 0.0;   // fp32: the fp64 quantile for the guard-band recomputation
-                const R mtr = meter_w<R>(odd ? pb.w : pb.y);
+                const R mtr = meter_w<R>(word_of(bm, (uint32_t)step & 3u));
                 if constexpr (RNG == TMH_RNG_INJECTED) {
                     const double ue = dr.one(ch, step, TAG_STEP, 0, 0);
                     if constexpr (sizeof(R) == 8) z = ndtri(ue);
@@ -981,7 +989,7 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
                             double row64[ROW];
                             for (int i = 0; i < ROW; ++i) row64[i] = r64[i];
                             if (kp.sites) lane_row<double>(ls, sun + (size_t)j * SUN_W, kp.module, row64);
-                            const double zz = RNG == TMH_RNG_INJECTED ? ndtri(z64) : noise_z<double>(odd ? pb.z : pb.x);
+                            const double zz = RNG == TMH_RNG_INJECTED ? ndtri(z64) : noise_z<double>(wn);
                             double c64, p64, m64, r64s;
                             bool rk;
                             second_body<double>(kp, kp.pvf, row64, flp, f64, covered, zz, 0.0, c64, p64, m64, r64s, rk);
@@ -1054,9 +1062,10 @@ __device__ __forceinline__ void hour_fractions(double* tab)
     __syncthreads();
 }
 
-// hour_f from the table (hf_tab, hour_fractions), day_f = div_exact(hour + hour_f, 24)
+// hour_f from the table (hf_tab, hour_fractions; TAB), day_f = div_exact(hour + hour_f, 24)
 // as clock_fractions computes it: the same bits, without the minute / second split and
-// the first two exact divisions per call
+// the first two exact divisions per call.  Without TAB, clock_fractions itself.
+template <bool TAB>
 __device__ __forceinline__ void fractions_at(const WinClock& w, int32_t j, const double* hf_tab, double& hour_f,
                                              double& day_f)
 {
@@ -1068,9 +1077,14 @@ __device__ __forceinline__ void fractions_at(const WinClock& w, int32_t j, const
     }
     sod %= 86400;
     if (sod < 0) sod += 86400;
-    const int hour = sod / HOUR_S;
-    hour_f = hf_tab[sod - HOUR_S * hour];
-    day_f = div_exact(hour + hour_f, 24.0, 1.0 / 24.0);
+    if constexpr (TAB) {
+        const int hour = sod / HOUR_S;
+        hour_f = hf_tab[sod - HOUR_S * hour];
+        day_f = div_exact(hour + hour_f, 24.0, 1.0 / 24.0);
+    } else {
+        double min_f;
+        clock_fractions(sod / 3600, (sod / 60) % 60, sod % 60, min_f, hour_f, day_f);
+    }
 }
 
 // try-0 candidate lengths of the next kcap next_cloud calls of every chain:
@@ -1238,8 +1252,13 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
     const int64_t W1 = W0 + nsteps;
     const uint32_t nev = min(*n_events, ev_cap_dev(nsteps));
     const WinClock wck = win_clock(ck, W0);
-    __shared__ double hf_tab[HOUR_S];   // 28.8 KB: the calls' hour fractions by table
-    hour_fractions(hf_tab);
+    // the calls' hour fractions by table (28.8 KB of LDS) in the 16-lane walk, whose 256-thread
+    // workgroups are one per CU or two; the 4- and 8-lane walks run one-wave workgroups, many
+    // per CU (C3: 262,144 waves), where the table's LDS would cap the waves per CU (walk
+    // 62 -> 114 ms per 1 M-chain day): they compute the fractions
+    constexpr bool HTAB = G == 16;
+    __shared__ double hf_tab[HTAB ? HOUR_S : 1];
+    if constexpr (HTAB) hour_fractions(hf_tab);
     // Groups take chains: group r starts with chain r, and a group whose chain is done
     // takes the next unstarted one from the window's queue (chains groups.. n - 1), so
     // with fewer groups than chains the walk's waves stay busy instead of idling
@@ -1453,7 +1472,7 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
             fetch_event();
         }
         double hf, df;
-        fractions_at(wck, (int32_t)(e - W0), hf_tab, hf, df);
+        fractions_at<HTAB>(wck, (int32_t)(e - W0), hf_tab, hf, df);
         const double hh = interp(ccb, cca, hf);
         const double h = 0.95 < hh ? 0.95 : hh;   // update_parameters
         const double ws = interp(wsb, wsa, df);
@@ -1631,7 +1650,7 @@ constexpr int exp_wg()
 {
     return 256;
 }
-constexpr int PVF_VGPR = 8;   // leading PVF fields pinned in VGPRs in the fp32 single-site expansion
+constexpr int PVF_VGPR = 0;   // leading PVF fields pinned in VGPRs in the fp32 single-site expansion
 // min waves per SIMD (__launch_bounds__) of each expansion instantiation:
 //  fp32 single-site trace (C2): 7 = at most 72 VGPRs (alone -4 % vs 6, no VGPR spills);
 //  fp32 statistics / other outputs (C3, C4): 6 = 80 VGPRs (the 16-bit-pair LDS histogram,
@@ -1870,20 +1889,39 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
             emit<R, OUT, true>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok, held);
         }
     };
-    // one Philox block per step pair: (x, y) for the even step, (z, w) for the odd one
+    // The per-second draws: the meter's and the noise's streams, one Philox block per four
+    // steps each (word step & 3).  A four-second group draws its noise block only when
+    // one of its seconds needs the noise (the CSI is an output, per-chain sites, or a
+    // daylight second with PV: the rows' night bits, wave-uniform), so a night second
+    // costs a quarter of a block instead of half.
     auto loops = [&](auto ff) __attribute__((always_inline)) {
-        if (((W0 + j0) & 1) == 0 && ((j1 - j0) & 1) == 0) {
-            for (uint32_t j = j0; j < j1; j += 2) {
-                const U4 pr = keyed_block(kp.seed, chain, (uint64_t)(W0 + j) >> 1, TAG_STEP2, 0);
-                second(j, pr.x, pr.y, ff);
-                second(j + 1, pr.z, pr.w, ff);
+        uint32_t j = j0;
+        if (((W0 + j0) & 3) == 0) {
+            for (; j + 4 <= j1; j += 4) {
+                const uint64_t g = (uint64_t)(W0 + j) >> 2;
+                const U4 pm = keyed_block(kp.seed, chain, g, TAG_METER4, 0);
+                bool need = OUT == OUT_ANY || SITES || !kp.with_pv;
+                if (!need) {   // any daylight second among the four (scalar loads of their flags)
+                    uint32_t nf = FL_NIGHT;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        nf &= sizeof(R) == 8 ? (uint32_t)(double)rowp[q * RW + G_FLAGS]
+                                             : __float_as_uint((float)rowp[q * RW + G_FLAGS + G32]);
+                    need = nf == 0;
+                }
+                U4 pn{0u, 0u, 0u, 0u};
+                if (need) pn = keyed_block(kp.seed, chain, g, TAG_NOISE4, 0);
+                second(j, pn.x, pm.x, ff);
+                second(j + 1, pn.y, pm.y, ff);
+                second(j + 2, pn.z, pm.z, ff);
+                second(j + 3, pn.w, pm.w, ff);
             }
-        } else {   // odd window start or length: one block per step (rare)
-            for (uint32_t j = j0; j < j1; ++j) {
-                const U4 pr = keyed_block(kp.seed, chain, (uint64_t)(W0 + j) >> 1, TAG_STEP2, 0);
-                const bool odd = (W0 + j) & 1;
-                second(j, odd ? pr.z : pr.x, odd ? pr.w : pr.y, ff);
-            }
+        }
+        for (; j < j1; ++j) {   // a window start off the four-step grid, or a short last block (rare)
+            const uint64_t g = (uint64_t)(W0 + j) >> 2;
+            const uint32_t q = (uint32_t)(W0 + j) & 3u;
+            second(j, word_of(keyed_block(kp.seed, chain, g, TAG_NOISE4, 0), q),
+                   word_of(keyed_block(kp.seed, chain, g, TAG_METER4, 0), q), ff);
         }
     };
     // (fp32 single-site only: in the fp64 and per-site kernels, which sit at their

@@ -76,8 +76,17 @@ enum : uint32_t {
     TAG_INIT = 4,
     TAG_INIT_CLOUD = 5,
     TAG_INIT_SEC = 6,
-    TAG_STEP2 = 7   // per step pair p = step >> 1: (x, y) = (noise, meter) of step 2p, (z, w) of 2p + 1
+    // per-second draws, two streams of one block per four steps g = step >> 2, word step & 3
+    // (x, y, z, w): the meter's and the noise's.  A night second needs only its meter word,
+    // so four night seconds cost one block (round 2's one block per step pair held both).
+    TAG_METER4 = 8,
+    TAG_NOISE4 = 9
 };
+
+__device__ __forceinline__ uint32_t word_of(const struct U4& b, uint32_t q)   // b.x, .y, .z, .w for q = 0..3
+{
+    return q == 0 ? b.x : (q == 1 ? b.y : (q == 2 ? b.z : b.w));
+}
 
 __device__ __forceinline__ U4 keyed_block(uint64_t seed, uint64_t chain, uint64_t step, uint32_t tag,
                                           uint32_t sub)
