@@ -113,3 +113,32 @@ def test_stale_pmc_record_never_reaches_a_bench_line(tmp_path, monkeypatch):
     assert bench.pmc_record(args, 4096, 86400) is None
     write(build_stamp())
     assert bench.pmc_record(args, 4096, 86400)["traffic_bytes_per_launch"] == 1.0
+
+
+@pytest.mark.parametrize("argv,want", [([], "all"), (["--no-cpu-baseline"], "none"),
+                                       (["--workload", "c3"], "none"), (["--precision", "fp64"], "none"),
+                                       (["--secondary", "c3,c5"], "c3,c5")])
+def test_secondary_lines_default_to_the_full_report_only(monkeypatch, argv, want):
+    """The default C2 fp32 run (with its CPU baseline) adds the other configurations'
+    lines; quick runs, other workloads and explicit choices do not change."""
+    monkeypatch.setattr(sys, "argv", ["bench.py"] + argv)
+    a = bench.parse()
+    assert a.secondary == want
+    assert set(bench.SECONDARY) == {"c2_fp64", "c3", "c4", "c5"}
+
+
+def test_secondary_lines_report_a_failed_child(monkeypatch):
+    """A secondary configuration that fails reports its error; nothing raises."""
+    import argparse
+
+    class R:
+        stdout = "not json"
+
+    monkeypatch.setattr(subprocess, "run", lambda *a, **k: R())
+    out = bench.secondary_lines(argparse.Namespace(secondary="c3", hw_queues=16))
+    assert list(out) == ["c3"] and "error" in out["c3"]
+
+
+def test_hw_queues_flag_defaults_to_sixteen(monkeypatch):
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    assert bench.parse().hw_queues == 16
