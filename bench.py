@@ -191,10 +191,10 @@ def parse():
                     help="gated schedule: HIP stream priority of the construction stream")
     ap.add_argument("--minutes-ahead", type=int, default=None,
                     help="gated schedule: build each batch's minute table with its construction (1) instead of "
-                         "before its expansion on the expansion stream (0); default 1 when --walks > 1")
+                         "before its expansion on the expansion stream (0, the default)")
     ap.add_argument("--commit-stream", type=int, default=None,
                     help="gated schedule: each batch's fixup + commit on a stream of their own beside the next "
-                         "expansion (1) or after its expansion on the expansion stream (0); default 1 when --walks > 1")
+                         "expansion (1) or after its expansion on the expansion stream (0, the default)")
     ap.add_argument("--compact", type=int, default=None,
                     help="multi-window stats workloads: run each window after the first on the chains still "
                          "live (faulted chains, e.g. C5's markov AssertionError, drop out); default 1 for c5")
@@ -217,10 +217,14 @@ def parse():
     a.build_ahead = a.build_ahead or max(1, a.walks) + 1
     # c3: two 1 M-chain batches in flight (2 x 83 GB of state + scratch): +3 % over one (r02)
     a.pipeline = a.pipeline or (2 if a.workload == "c3" else a.build_ahead + 1)
+    # round 3, 16 hardware queues, same box, 3 reps: the minute table before its expansion
+    # and the fixup + commit after it, both on the expansion stream, 1.485-1.490 ms per C2
+    # batch against 1.528-1.552 with both on streams of their own (round 2's choice, made
+    # when 4 queues serialised the streams anyway); either one alone 1.49-1.52
     if a.minutes_ahead is None:
-        a.minutes_ahead = int(a.walks > 1)
+        a.minutes_ahead = 0
     if a.commit_stream is None:
-        a.commit_stream = int(a.walks > 1)
+        a.commit_stream = 0
     a.mode = a.mode or ("trace" if a.workload == "c2" else "stats")
     if a.secondary is None:
         # the full report (the default C2 run with its CPU baseline) carries them; quick runs do not

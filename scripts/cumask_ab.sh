@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 TAG="$1"; shift
-for rep in 1 2; do
+for rep in ${REPS:-1 2}; do
 i=0
 for o in "$@"; do
   i=$((i + 1))
