@@ -186,7 +186,7 @@ def parse():
                          "CUs the walks do not use")
     ap.add_argument("--build-ahead", type=int, default=None,
                     help="gated schedule: when the walk of batch k ends, the construction of batch k + A is "
-                         "released (default A = walks + 1; needs --pipeline >= A + 1)")
+                         "released (default A = walks + 2 with two or more walks, else walks + 1; needs --pipeline >= A + 1)")
     ap.add_argument("--build-priority", default="normal", choices=["high", "normal"],
                     help="gated schedule: HIP stream priority of the construction stream")
     ap.add_argument("--minutes-ahead", type=int, default=None,
@@ -214,7 +214,9 @@ def parse():
     # C5's compacted windows walk and expand in turn (latency-bound walk): 16 lanes per
     # chain (1.76e10 against 1.73e10 with the batch-size default, r02 same box)
     a.walk_lanes = a.walk_lanes or (16 if c5 else 0)
-    a.build_ahead = a.build_ahead or max(1, a.walks) + 1
+    # construction released walks + 2 batches ahead (round 3, 16 queues, same box, 3 reps:
+    # 1.41-1.44 ms per C2 batch at 4, 5 or 6 ahead against 1.48-1.55 at 3, 1.86-1.90 at 2)
+    a.build_ahead = a.build_ahead or max(1, a.walks) + (2 if a.walks > 1 else 1)
     # c3: two 1 M-chain batches in flight (2 x 83 GB of state + scratch): +3 % over one (r02)
     a.pipeline = a.pipeline or (2 if a.workload == "c3" else a.build_ahead + 1)
     # round 3, 16 hardware queues, same box, 3 reps: the minute table before its expansion
