@@ -302,8 +302,8 @@ def cpu_baseline(args, kw):
     dt1 = timed(n1, 1)
     what = 'C5 sites/tables, ' + args.cc if c5 else 'C2 site/day'
     return {"value": n * secs / dt, "unit": "chain-seconds/s", "cores": threads, "kind": "port",
-            "sample": f"{n} chains x {secs} s ({what}, fp64 C oracle, {threads} OpenMP threads of nproc={nproc}, "
-                      f"{dt:.1f} s wall)",
+            "sample": f"{n} chains x {secs} s ({what}, fp64 C oracle, {threads} OpenMP threads = the GPU box's CPU "
+                      f"share for one GPU (nproc={nproc} counts the whole machine), {dt:.1f} s wall)",
             "single_thread": {"value": n1 * secs / dt1, "cores": 1,
                               "sample": f"{n1} chains x {secs} s, 1 thread, {dt1:.1f} s wall"},
             "reference_python_per_core": {"value": 4.0e4, "source": "BASELINE.md (timed in the build container; "
