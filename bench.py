@@ -122,7 +122,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
                     help="c2: the headline (BASELINE.json configs[1]); c3: 1,048,576 chains x 1 day, stats, two "
-                         "batches in flight (74 GB of scratch each); c4: 16,384 chains x the year 2019 "
+                         "batches in flight (~33 GB of state + scratch each); c4: 16,384 chains x the year 2019 "
                          "(Europe/Berlin wall clock, stats, day windows); c5: the lat/lon sweep (65,536 sites x 1 "
                          "week, markov cc with per-site tables, per-site PV geometry, stats mode, day windows)")
     ap.add_argument("--gpus", type=int, default=1)
@@ -204,40 +204,32 @@ def parse():
     a = ap.parse_args()
     if a.gpus < 1:
         ap.error("--gpus must be >= 1")
+    from tmhpvsim_amd.pipeline import pipeline_defaults
     c5, c4 = a.workload == "c5", a.workload == "c4"
     a.chains = a.chains or DEFAULT_CHAINS[a.workload]
     a.seconds = a.seconds or {"c2": 86400, "c3": 86400, "c4": 365 * 86400, "c5": 604800}[a.workload]
-    if a.compact is None:
-        a.compact = int(c5)
-    # C2: two walks in flight (r02, same-box A/B: 1.71-1.72 ms per batch against 1.81 with one)
-    a.walks = a.walks if a.walks is not None else (2 if a.workload == "c2" else 1)
+    # the schedule (contexts, walks in flight, construction ahead, streams): the measured-best
+    # defaults of each workload, shared with the tests that run the timed schedule
+    a.cfg = pipeline_defaults(a.workload, a.precision, seconds=a.seconds, window=a.window, walks=a.walks,
+                              build_ahead=a.build_ahead, pipeline=a.pipeline, compact=a.compact, mode=a.mode,
+                              stagger=a.stagger, schedule=a.schedule, build_on=a.build_on,
+                              walk_priority=a.walk_priority, expand_priority=a.expand_priority,
+                              build_priority=a.build_priority,
+                              minutes_ahead=None if a.minutes_ahead is None else bool(a.minutes_ahead),
+                              commit_stream=None if a.commit_stream is None else bool(a.commit_stream),
+                              walk_order=bool(a.walk_order), walk_cus=a.walk_cus, other_cus=a.other_cus,
+                              timeline=a.timeline)
+    for k in ("mode", "window", "pipeline", "walks", "build_ahead", "build_on", "walk_priority", "compact",
+              "minutes_ahead", "commit_stream"):
+        setattr(a, k, getattr(a.cfg, k))
     # C5's compacted windows walk and expand in turn (latency-bound walk): 16 lanes per
     # chain (1.76e10 against 1.73e10 with the batch-size default, r02 same box)
     a.walk_lanes = a.walk_lanes or (16 if c5 else 0)
-    # construction released walks + 2 batches ahead (round 3, 16 queues, same box, 3 reps:
-    # 1.41-1.44 ms per C2 batch at 4, 5 or 6 ahead against 1.48-1.55 at 3, 1.86-1.90 at 2)
-    a.build_ahead = a.build_ahead or max(1, a.walks) + (2 if a.walks > 1 else 1)
-    # c3: two 1 M-chain batches in flight (2 x 83 GB of state + scratch): +3 % over one (r02)
-    a.pipeline = a.pipeline or (2 if a.workload == "c3" else a.build_ahead + 1)
-    # round 3, 16 hardware queues, same box, 3 reps: the minute table before its expansion
-    # and the fixup + commit after it, both on the expansion stream, 1.485-1.490 ms per C2
-    # batch against 1.528-1.552 with both on streams of their own (round 2's choice, made
-    # when 4 queues serialised the streams anyway); either one alone 1.49-1.52
-    if a.minutes_ahead is None:
-        a.minutes_ahead = 0
-    if a.commit_stream is None:
-        a.commit_stream = 0
-    a.mode = a.mode or ("trace" if a.workload == "c2" else "stats")
     if a.secondary is None:
         # the full report (the default C2 run with its CPU baseline) carries them; quick runs do not
         a.secondary = "all" if (a.workload == "c2" and a.precision == "fp32" and not a.no_cpu_baseline) else "none"
     a.cc = a.cc or ("markov" if c5 else "faithful")
-    a.window = min(a.window or (86400 if (c5 or c4) else a.seconds), a.seconds)
     a.start = a.start or ("2019-01-01 00:00:00" if c4 else "2019-09-05 00:00:00")
-    # C2 (same-box A/B, r01): construction on the walk stream at normal priority
-    # 1.94e11 chain-s/s vs 1.82e11 on the expansion stream with high-priority walks
-    a.build_on = a.build_on or ("walk" if a.workload == "c2" else "expand")
-    a.walk_priority = a.walk_priority or ("normal" if a.workload == "c2" else "high")
     return a
 
 
@@ -386,7 +378,6 @@ def main():
         kw = dict(shape_tables=site_shape_tables(n, site0=shard0), sites=grid[shard0:shard0 + n])
     sim = BatchedSim(n, args.start, tz="Europe/Berlin", params=ModelParams(cc_mode=CC_MARKOV if args.cc == "markov" else 0),
                      precision=args.precision, chain0=shard0, device=dev, horizon=secs, kernel_path=args.path, **kw)
-    real = sim.real
     if args.walk_cpr != 1:
         _lib.check(L.tmh_set_walk_chains_per_row(sim._eng, args.walk_cpr))
     if args.walk_lanes:
@@ -394,340 +385,22 @@ def main():
     if hasattr(L, "tmh_set_walk_order"):
         _lib.check(L.tmh_set_walk_order(sim._eng, args.walk_order))
 
-    nwin = (secs + win - 1) // win
-    prio_lo, prio_hi = torch.cuda.Stream.priority_range()
-
-    class Ctx:   # one batch in flight: its own state, plan, scratch, outputs and HIP streams
-        # The context's own streams are created on first use: the gated schedule runs on
-        # shared streams, and every extra stream shares one of HIP's few hardware queues
-        # with a busy one (a queue runs its packets in order, across streams).
-        @property
-        def stream(self):
-            if self._stream is None:
-                self._stream = torch.cuda.Stream(dev)
-            return self._stream
-
-        @property
-        def sptr(self):
-            return C.c_void_p(self.stream.cuda_stream)
-
-        @property
-        def wstream(self):   # the walk runs on a stream of its own, high priority by default
-            if self._wstream is None:
-                self._wstream = torch.cuda.Stream(dev, priority=prio_hi if args.walk_priority == "high" else prio_lo)
-            return self._wstream
-
-        @property
-        def wptr(self):
-            return C.c_void_p(self.wstream.cuda_stream)
-
-        def __init__(self):
-            self._stream = self._wstream = None
-            self.walked = torch.cuda.Event()
-            self.done = torch.cuda.Event()
-            self.kernel_done = torch.cuda.Event()
-            self.expanded = None   # recorded after this context's last expansion
-            self.state = torch.zeros(L.tmh_state_bytes(n), dtype=torch.uint8, device=dev)
-            self.plan = torch.empty(L.tmh_plan_bytes(win), dtype=torch.uint8, device=dev)
-            self.scratch = torch.empty(L.tmh_engine_scratch_bytes(sim._eng, n, win), dtype=torch.uint8, device=dev)
-            if args.compact and args.mode == "stats" and nwin > 1:   # compacted windows: a working state
-                self.work = torch.empty_like(self.state)
-                self.ids = torch.empty(n, dtype=torch.int32, device=dev)
-                self.nlive = torch.zeros(1, dtype=torch.int32, device=dev)
-            if nwin > 1:   # second plan + scratch: window w+1's walk beside window w's expansion
-                self.plan2 = torch.empty_like(self.plan)
-                self.scratch2 = torch.empty_like(self.scratch)
-                self.wev = [torch.cuda.Event(), torch.cuda.Event()]
-                self.eev = [torch.cuda.Event(), torch.cuda.Event()]
-            self.trace = {f: torch.empty(win, n, dtype=real, device=dev) for f in ("pv", "meter", "residual")} \
-                if args.mode == "trace" else {}
-            self.tr = _lib.Trace(None, None, *(self.trace[f].data_ptr() if f in self.trace else None
-                                               for f in ("pv", "meter", "residual")), n)
-            self.st = None
-            if args.mode == "stats":
-                self.hist = torch.zeros(4096, dtype=torch.int64, device=dev)
-                self.acc = torch.zeros(4, n, dtype=torch.float64, device=dev)
-                self.acc[3].fill_(-float("inf"))
-                self.st = _lib.Stats(self.hist.data_ptr(), 4096, 0, -300.0, 9000.0, self.acc.data_ptr())
-
-    ctxs = [Ctx() for _ in range(max(1, args.pipeline))]
-    # one stream for every batch's expansion: expansions run back to back, in order
-    # (they fill the chip on their own), while the walks of the next batches run on
-    # their contexts' high-priority streams beside them
-    estream = torch.cuda.Stream(dev, priority=prio_hi if args.expand_priority == "high" else prio_lo)
-    eptr = C.c_void_p(estream.cuda_stream)
+    from tmhpvsim_amd.pipeline import BatchPipeline
+    pipe = BatchPipeline(sim, n, secs, args.cfg, batch_chain0, dev)
+    nwin = pipe.nwin
     torch.cuda.synchronize()
     L.tmh_profile_enable(sim._eng, 1)
-
-    def one_step(k):   # a whole batch on its context's streams
-        cx = ctxs[k % len(ctxs)]
-        chain0 = batch_chain0(k)                          # fresh global chains every batch
-        _lib.check(L.tmh_init(sim._eng, C.c_void_p(cx.state.data_ptr()), chain0, n, None, cx.sptr))
-        if nwin == 1 or sim.path != "time_parallel":
-            for s0 in range(0, secs, win):   # windows: a trace window is overwritten by the next
-                w = min(win, secs - s0)
-                _lib.check(L.tmh_plan(sim._eng, s0, w, C.c_void_p(cx.plan.data_ptr()), cx.sptr))
-                _lib.check(L.tmh_step(sim._eng, C.c_void_p(cx.state.data_ptr()), chain0, n, s0, w, None,
-                                      C.byref(cx.tr), C.byref(cx.st) if cx.st is not None else None,
-                                      C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
-                                      cx.scratch.numel(), cx.sptr))
-            return
-        if args.compact and args.mode == "stats":   # windows in order, the live chains of each only
-            sp = C.c_void_p(cx.state.data_ptr())
-            for s0 in range(0, secs, win):
-                w = min(win, secs - s0)
-                nl, cur = n, cx.state
-                if s0 > 0:
-                    _lib.check(L.tmh_live_chains(sim._eng, sp, n, None, C.c_void_p(cx.ids.data_ptr()),
-                                                 C.c_void_p(cx.nlive.data_ptr()), cx.sptr))
-                    cx.stream.synchronize()                # n_live was written on the batch's stream
-                    nl = int(cx.nlive.item())
-                    if nl < n:
-                        cur = cx.work
-                        if nl:
-                            _lib.check(L.tmh_state_move(sim._eng, sp, n, C.c_void_p(cx.work.data_ptr()), nl,
-                                                        C.c_void_p(cx.ids.data_ptr()), C.c_void_p(cx.nlive.data_ptr()),
-                                                        nl, 0, cx.sptr))
-                            _lib.check(L.tmh_set_chain_ids(sim._eng, C.c_void_p(cx.ids.data_ptr()), n))
-                if nl:
-                    _lib.check(L.tmh_plan(sim._eng, s0, w, C.c_void_p(cx.plan.data_ptr()), cx.sptr))
-                    _lib.check(L.tmh_step(sim._eng, C.c_void_p(cur.data_ptr()), chain0, nl, s0, w, None,
-                                          C.byref(cx.tr), C.byref(cx.st), C.c_void_p(cx.plan.data_ptr()),
-                                          C.c_void_p(cx.scratch.data_ptr()), cx.scratch.numel(), cx.sptr))
-                if nl and cur is cx.work:
-                    _lib.check(L.tmh_state_move(sim._eng, C.c_void_p(cx.work.data_ptr()), nl, sp, n,
-                                                C.c_void_p(cx.ids.data_ptr()), C.c_void_p(cx.nlive.data_ptr()),
-                                                nl, 1, cx.sptr))
-                _lib.check(L.tmh_set_chain_ids(sim._eng, None, 0))
-            return
-        # multi-window: the segment walk of window w+1 (high-priority stream) beside the
-        # expansion of window w; plans and draws on the expansion's stream (as BatchedSim.run)
-        bufs = [(cx.plan, cx.scratch), (cx.plan2, cx.scratch2)]
-        wins = [(s0, min(win, secs - s0)) for s0 in range(0, secs, win)]
-        sp = C.c_void_p(cx.state.data_ptr())
-
-        def views(w):
-            return tuple(C.c_void_p(t.data_ptr()) for t in bufs[w & 1])
-
-        def prev_of(w):
-            return (views(w - 1)[1], wins[w - 1][1]) if w > 0 else (None, 0)
-
-        def draws(w):
-            pl, sc = views(w)
-            _lib.check(L.tmh_plan(sim._eng, wins[w][0], wins[w][1], pl, cx.sptr))
-            _lib.check(L.tmh_walk_part(sim._eng, sp, chain0, n, wins[w][0], wins[w][1], pl, sc, cx.scratch.numel(),
-                                       *prev_of(w), _lib.WALK_DRAWS, cx.sptr))
-            cx.wev[w & 1].record(cx.stream)
-
-        def segments(w):
-            pl, sc = views(w)
-            cx.wstream.wait_event(cx.wev[w & 1])
-            _lib.check(L.tmh_walk_part(sim._eng, sp, chain0, n, wins[w][0], wins[w][1], pl, sc, cx.scratch.numel(),
-                                       *prev_of(w), _lib.WALK_SEGMENTS, cx.wptr))
-            cx.eev[w & 1].record(cx.wstream)
-
-        draws(0)
-        segments(0)
-        for w in range(len(wins)):
-            cx.stream.wait_event(cx.eev[w & 1])
-            if w + 1 < len(wins):
-                draws(w + 1)
-                segments(w + 1)
-            pl, sc = views(w)
-            _lib.check(L.tmh_expand(sim._eng, sp, chain0, n, wins[w][0], wins[w][1], None,
-                                    C.byref(cx.tr), C.byref(cx.st) if cx.st is not None else None, pl, sc,
-                                    cx.scratch.numel(), cx.sptr))
-
-    def build(k):      # construction of batch k's chains, its plan and draws
-        cx = ctxs[k % len(ctxs)]
-        cx.chain0 = batch_chain0(k)
-        if args.build_on == "walk":   # on the batch's walk stream, after the expansion
-            bs, bp = cx.wstream, cx.wptr   # that last used this context: beside the running expansion
-            if cx.expanded is not None:
-                bs.wait_event(cx.expanded)
-        else:                          # in order on the expansion stream
-            bs, bp = estream, eptr
-        _lib.check(L.tmh_init(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, None, bp))
-        _lib.check(L.tmh_plan(sim._eng, 0, secs, C.c_void_p(cx.plan.data_ptr()), bp))
-        _lib.check(L.tmh_walk_part(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs,
-                                   C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
-                                   cx.scratch.numel(), None, 0, _lib.WALK_DRAWS, bp))
-        cx.done.record(bs)
-
-    def start(k):      # the segment walk of batch k, on its context's walk stream
-        cx = ctxs[k % len(ctxs)]
-        cx.wstream.wait_event(cx.done)
-        _lib.check(L.tmh_walk_part(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs,
-                                   C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
-                                   cx.scratch.numel(), None, 0, _lib.WALK_SEGMENTS, cx.wptr))
-        cx.walked.record(cx.wstream)
-
-    def finish(k):     # second half: the expansion (trace / stats) on the expansion stream, then its
-        cx = ctxs[k % len(ctxs)]   # commit (fp32 guard-band fixup + state) on the batch's walk stream,
-        estream.wait_event(cx.walked)   # beside the next batch's expansion (tmh_expand_part)
-        args_ = (sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs, None, C.byref(cx.tr),
-                 C.byref(cx.st) if cx.st is not None else None, C.c_void_p(cx.plan.data_ptr()),
-                 C.c_void_p(cx.scratch.data_ptr()), cx.scratch.numel())
-        _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_KERNEL, eptr))
-        cx.kernel_done.record(estream)
-        cx.wstream.wait_event(cx.kernel_done)
-        _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_COMMIT, cx.wptr))
-        if cx.expanded is None:
-            cx.expanded = torch.cuda.Event()
-        cx.expanded.record(cx.wstream)
-
-    # gated schedule: one walk stream and one construction stream for all batches.
-    # When the walk of batch k ends, three streams are released together: the
-    # expansion of k, the walk of k + 1 and the construction of k + 2.  Their
-    # workgroups are then dispatched interleaved, so the walk (one long-lived wave
-    # per SIMD) and the construction kernels are resident beside the expansion
-    # instead of queueing behind its 10,800 workgroups (a kernel launched while an
-    # expansion fills the CUs waits for its tail: the walks then ran three at a time,
-    # between expansions, rocprofv3 kernel trace r02).
-    W = max(1, args.walks)
-    wsts = [torch.cuda.Stream(dev, priority=prio_hi if args.walk_priority == "high" else prio_lo) for _ in range(W)]
-    bst = torch.cuda.Stream(dev, priority=prio_hi if args.build_priority == "high" else prio_lo)
-    cst = torch.cuda.Stream(dev)
-    if args.walk_cus:   # the walks on a share of every XCD's CUs (CU-masked streams)
-        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-        wsts = [_lib.cu_stream(0, args.walk_cus, dev) for _ in range(W)]
-        if args.other_cus == "rest":
-            bst, cst = (_lib.cu_stream(args.walk_cus, ncu - args.walk_cus, dev) for _ in range(2))
-            estream = _lib.cu_stream(args.walk_cus, ncu - args.walk_cus, dev)
-            eptr = C.c_void_p(estream.cuda_stream)
-    bst_p = C.c_void_p(bst.cuda_stream)
-    A = args.build_ahead
-
-    def expand_args(cx):
-        return (sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs, None, C.byref(cx.tr),
-                C.byref(cx.st) if cx.st is not None else None, C.c_void_p(cx.plan.data_ptr()),
-                C.c_void_p(cx.scratch.data_ptr()), cx.scratch.numel())
-
-    def g_build(j, gate):
-        cx = ctxs[j % len(ctxs)]
-        cx.chain0 = batch_chain0(j)
-        if gate is not None:
-            bst.wait_event(gate)
-        if cx.expanded is not None:                        # the context's previous batch is committed
-            bst.wait_event(cx.expanded)
-        _lib.check(L.tmh_init(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, None, bst_p))
-        _lib.check(L.tmh_plan(sim._eng, 0, secs, C.c_void_p(cx.plan.data_ptr()), bst_p))
-        _lib.check(L.tmh_walk_part(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs,
-                                   C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
-                                   cx.scratch.numel(), None, 0, _lib.WALK_DRAWS, bst_p))
-        if args.minutes_ahead:   # the minute table needs the draws, not the walk
-            _lib.check(L.tmh_expand_part(*expand_args(cx), _lib.EXPAND_MINUTES, bst_p))
-        cx.done.record(bst)
-        tl_mark("built", j, bst)
-
-    tl = {}   # --timeline: per-batch HIP timing events (build done, walk start / end, expansion start / end)
-
-    def tl_mark(key, j, stream):
-        if args.timeline:
-            e = torch.cuda.Event(enable_timing=True)
-            e.record(stream)
-            tl.setdefault(key, {})[j] = e
-
-    def g_walk(j):
-        cx = ctxs[j % len(ctxs)]
-        wst = wsts[j % W]
-        wst.wait_event(cx.done)
-        tl_mark("walk0", j, wst)
-        _lib.check(L.tmh_walk_part(sim._eng, C.c_void_p(cx.state.data_ptr()), cx.chain0, n, 0, secs,
-                                   C.c_void_p(cx.plan.data_ptr()), C.c_void_p(cx.scratch.data_ptr()),
-                                   cx.scratch.numel(), None, 0, _lib.WALK_SEGMENTS, C.c_void_p(wst.cuda_stream)))
-        cx.walked.record(wst)
-        tl_mark("walk1", j, wst)
-
-    def g_expand(j):
-        cx = ctxs[j % len(ctxs)]
-        es, ep = estream, eptr
-        es.wait_event(cx.walked)
-        args_ = expand_args(cx)
-        tl_mark("exp0", j, es)
-        _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_KERNEL | (_lib.EXPAND_NO_MINUTES if args.minutes_ahead else 0),
-                                     ep))
-        tl_mark("exp1", j, es)
-        if cx.expanded is None:
-            cx.expanded = torch.cuda.Event()
-        if args.commit_stream:   # fixup + commit beside the next expansion
-            cx.kernel_done.record(es)
-            cst.wait_event(cx.kernel_done)
-            _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_COMMIT, C.c_void_p(cst.cuda_stream)))
-            cx.expanded.record(cst)
-        else:
-            _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_COMMIT, ep))
-            cx.expanded.record(es)
-
-    def run_gated(k0, cnt):
-        """W walks in flight (W + 2 contexts): when the walk of batch k ends, the
-        expansion of k, the walk of k + W (on k's walk stream) and the construction
-        of k + W + 1 are released together."""
-        end = k0 + cnt
-        for j in range(k0, min(k0 + A, end)):
-            # the run's first walk is the pipeline's fill latency (its expansion waits for it with
-            # nothing else to do): chain order, whose windiest wavefront is shorter than the wind
-            # order's (four windy chains); the wind order for the rest, which run beside expansions
-            if args.walk_order and hasattr(L, "tmh_set_walk_order"):
-                _lib.check(L.tmh_set_walk_order(sim._eng, 0 if (j == k0 and W > 1) else 1))
-            g_build(j, None)
-        for j in range(k0, min(k0 + W, end)):
-            g_walk(j)
-        for k in range(k0, end):
-            gate = ctxs[k % len(ctxs)].walked
-            if k + A < end:
-                g_build(k + A, gate)
-            if k + W < end:
-                g_walk(k + W)
-            g_expand(k)
-
-    def run_batches(k0, cnt):
-        """Batches k0 .. k0 + cnt - 1.  One-window batches are software-pipelined:
-        construction + plan and the expansions run in order on one stream, the
-        segment walks of the next (depth - 1) batches on high-priority streams beside
-        them, so the one-wave-per-SIMD walks overlap the expansion instead of running
-        in lockstep with it (separate per-batch streams drift into lockstep: every
-        expansion then shares the chip with the others and with every walk)."""
-        if nwin > 1 or not args.stagger:
-            for k in range(k0, k0 + cnt):
-                one_step(k)
-            return
-        if args.schedule == "gated" and len(ctxs) >= max(A + 1, W + 2):
-            run_gated(k0, cnt)
-            return
-        D = len(ctxs)
-        ahead = D - 1
-        for k in range(k0, min(k0 + D, k0 + cnt)):
-            build(k)
-        for k in range(k0, min(k0 + ahead, k0 + cnt)):
-            start(k)
-        for k in range(k0, k0 + cnt):
-            if k + ahead < k0 + cnt:
-                start(k + ahead)
-            finish(k)
-            if k + D < k0 + cnt:
-                build(k + D)
+    run_batches, one_step = pipe.run, pipe.one_step
 
     def exchange():
         """stats mode: the one cross-GPU step, an RCCL all-reduce of the aggregate statistics"""
-        torch.cuda.synchronize()
-        for cx in ctxs:   # (streams a schedule never created have nothing to wait for)
-            for st_ in (cx._stream, cx._wstream):
-                if st_ is not None:
-                    st_.synchronize()
-        hist = sum(cx.hist for cx in ctxs)
-        acc = torch.stack([cx.acc for cx in ctxs])
-        tot = dict(energy_pv=acc[:, 0].sum(), energy_meter=acc[:, 1].sum(), energy_residual=acc[:, 2].sum(),
-                   peak_residual=acc[:, 3].max(), hist=hist)
-        return all_reduce_stats(tot)
+        pipe.sync()
+        return all_reduce_stats(pipe.totals())
 
     run_batches(0, args.warmup)
     if args.mode == "stats":
         exchange()                                         # loads torch's reduction kernels outside the timing
-        for cx in ctxs:
-            cx.hist.zero_()
-            cx.acc[:3].zero_()
-            cx.acc[3].fill_(-float("inf"))
+        pipe.reset_stats()
     torch.cuda.synchronize()
     for kk in (_lib.K_EXPAND, _lib.K_SEGMENTS, _lib.K_CANDIDATES, _lib.K_STEP):
         _lib.profile_read(sim._eng, kk)                    # drop the warmup launches
@@ -756,10 +429,7 @@ def main():
     alone_ms *= 1 if nwin == 1 else nwin
     for kk in (_lib.K_SEGMENTS, _lib.K_CANDIDATES, _lib.K_STEP):
         _lib.profile_read(sim._eng, kk)
-    bad = 0
-    for cx in ctxs:
-        sim.state = cx.state
-        bad += int((sim.status() != 0).sum())
+    bad = pipe.faulted()
     for name in phases:                                    # per batch (all windows)
         if phases[name] is not None:
             phases[name] *= nwin
@@ -829,11 +499,11 @@ def main():
                                + ")",
                    "chains_node": n_node, "chains_per_gpu": n, "seconds": secs,
                    "parallelism": f"chains sharded over {world} GPU(s), {scaling} scaling",
-                   "batches_in_flight": len(ctxs), "staggered": bool(args.stagger and nwin == 1),
+                   "batches_in_flight": len(pipe.ctxs), "staggered": bool(args.stagger and nwin == 1),
                    "construction_on": args.build_on, "walk_priority": args.walk_priority,
-                   "schedule": args.schedule if (args.stagger and nwin == 1 and len(ctxs) >= 3) else None,
+                   "schedule": args.schedule if pipe.gated() else None,
                    "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"), "walks_in_flight": W, "walk_order": bool(args.walk_order), "walk_cus": args.walk_cus or "all", "other_cus": args.other_cus if args.walk_cus else "all",
-                   "walk_chains_per_row": args.walk_cpr, "walk_lanes": args.walk_lanes or "auto", "build_ahead": A,
+                   "walk_chains_per_row": args.walk_cpr, "walk_lanes": args.walk_lanes or "auto", "build_ahead": pipe.A,
                    "minutes_ahead": bool(args.minutes_ahead), "commit_stream": bool(args.commit_stream),
                    "compacted_windows": bool(args.compact and args.mode == "stats" and nwin > 1)},
         "roofline": roof,
@@ -843,6 +513,7 @@ def main():
         "effective_trace_gbs": (TB * n * secs / (elapsed / args.steps) / 1e9) if args.mode == "trace" else None,
         "faulted_chains": bad,
     }
+    tl = pipe.tl
     if args.timeline and "exp0" in tl:
         ks = sorted(k for k in tl["exp0"] if k >= args.warmup and k in tl["exp1"] and k + 1 in tl.get("exp0", {}))
         gaps = [tl["exp1"][k].elapsed_time(tl["exp0"][k + 1]) for k in ks]
@@ -854,7 +525,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args, kw)
     if rank == 0 and world == 1 and args.secondary != "none":
-        del ctxs   # the children need the memory
+        del pipe, run_batches, one_step   # the children need the memory
         torch.cuda.empty_cache()
         line["secondary"] = secondary_lines(args)
     if rank == 0:

@@ -50,10 +50,12 @@ extern "C" {
 #define TMH_CHAIN_ASSERT_BINARY 2   /* cloud_cover_binary.py:90-98 (assert not recurse) */
 #define TMH_CHAIN_SIGMA_OVERFLOW 3  /* sigma arrays exceed TMH_SIGMA_CAP (no reference analogue) */
 #define TMH_CHAIN_U_EXHAUSTED 4     /* injected uniform stream ran out */
-#define TMH_CHAIN_SEGMENT_OVERFLOW 5 /* > n_steps/128 + 256 + 2,048 cloud segments in one window; or more
-                                         than n_steps/128 + 256 while the batch's demand exceeds the
-                                         window's shared overflow pool (n/16 + 8 chunks of 256): then every
-                                         such chain faults at its first record past the row (deterministic;
+#define TMH_CHAIN_SEGMENT_OVERFLOW 5 /* more than cap + 2,048 cloud segments in one window, where the row
+                                         cap = (n_steps/135 + 16) rounded up to 16 (656 a day: ~1.7x the
+                                         mean 386 calls, exceeded by ~0.3 % of the chain-days); or more
+                                         than cap while the batch's demand exceeds the window's shared
+                                         overflow pool (n/16 + 8 chunks of 256): then every such chain
+                                         faults at its first record past the row (deterministic;
                                          time-parallel path) */
 #define TMH_CHAIN_GUARD_OVERFLOW 6   /* fp32 guard-band records of the batch exceeded their room (never observed; time-parallel path) */
 
@@ -204,7 +206,7 @@ int tmh_live_chains(struct tmh_engine* eng, const void* state, uint32_t n_chains
 int tmh_state_move(struct tmh_engine* eng, const void* src, uint32_t n_src, void* dst, uint32_t n_dst,
                    const uint32_t* map, const uint32_t* count, uint32_t cap, int scatter, void* stream);
 /* Tests only: segment records kept per chain (a multiple of 16; 0 = the default
- * n_steps/128 + 256, rounded up to 16) and the overflow pool's chunks (0 = n_chains/16 + 8), for
+ * (n_steps/135 + 16) rounded up to 16) and the overflow pool's chunks (0 = n_chains/16 + 8), for
  * every later tmh_scratch_bytes / launch in this process.  Exercises the
  * overflow path, which the default sizes reach only on the windiest days. */
 int tmh_test_set_segment_capacity(uint32_t cap, uint32_t pool_chunks);
@@ -290,8 +292,8 @@ int tmh_expand(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_
                const void* plan, void* scratch, size_t scratch_bytes, void* stream);
 
 /* The walk in parts and across windows (time-parallel path).
- * parts: TMH_WALK_DRAWS = boundary draws, markov hourly cover and candidate cloud
- * lengths (many small workgroups); TMH_WALK_SEGMENTS = the P1 segment walk (one
+ * parts: TMH_WALK_DRAWS = boundary draws, markov hourly cover, candidate cloud
+ * lengths and the window's minute draws (many small workgroups); TMH_WALK_SEGMENTS = the P1 segment walk (one
  * wave per SIMD, long-lived).  Small grids issued beside a running expansion
  * wait for CU slots, so a pipelining caller puts the draws on the expansion's
  * stream and only the segment walk on a second, high-priority stream.
@@ -310,17 +312,15 @@ int tmh_walk_part(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t
                   const void* prev_scratch, uint32_t prev_n_steps, int parts, void* stream);
 
 /* tmh_expand in its two halves, for callers that overlap independent batches
- * (bench.py): TMH_EXPAND_KERNEL = the window's minute draws and the P2
- * expansion (traces / statistics); TMH_EXPAND_COMMIT = the fp32 guard-band
- * recomputation (fixup) and the state / statistics commit.  The commit half is
- * latency-bound (a few waves); on a second stream, after an event recorded
- * behind the kernel half, it runs beside the next batch's expansion.  Order:
- * KERNEL then COMMIT on the same buffers; the traces and statistics are final
- * after COMMIT.  tmh_expand == KERNEL | COMMIT.  TMH_EXPAND_MINUTES alone = the
- * window's minute draws only (they need the window-start state -- after tmh_init
- * or the previous window's COMMIT -- and the walk's draws, not the segment walk),
- * so a caller can build them ahead on another stream; a later TMH_EXPAND_KERNEL |
- * TMH_EXPAND_NO_MINUTES on the same buffers then runs the expansion alone. */
+ * (bench.py): TMH_EXPAND_KERNEL = the P2 expansion (traces / statistics);
+ * TMH_EXPAND_COMMIT = the fp32 guard-band recomputation (fixup) and the state /
+ * statistics commit.  The commit half is latency-bound (a few waves); on a second
+ * stream, after an event recorded behind the kernel half, it runs beside the next
+ * batch's expansion.  Order: KERNEL then COMMIT on the same buffers; the traces and
+ * statistics are final after COMMIT.  tmh_expand == KERNEL | COMMIT.  The window's
+ * minute draws are part of TMH_WALK_DRAWS (one launch with the candidate lengths,
+ * built with the construction, off the expansion's stream); TMH_EXPAND_MINUTES and
+ * TMH_EXPAND_NO_MINUTES (round 3's split of them) are accepted and do nothing. */
 #define TMH_EXPAND_KERNEL 1
 #define TMH_EXPAND_COMMIT 2
 #define TMH_EXPAND_MINUTES 4
@@ -340,9 +340,24 @@ enum { TMH_K_EXPAND = 0, TMH_K_SEGMENTS = 1, TMH_K_CANDIDATES = 2, TMH_K_STEP = 
 int tmh_profile_enable(struct tmh_engine* eng, int on);
 int tmh_profile_read(struct tmh_engine* eng, int kernel, double* total_ms, int* launches);
 
+/* The expansion variant the engine's last tmh_step / tmh_expand(_part) launched
+ * (tests and measurement: which kernel instantiation produced a line or a trace):
+ * TMH_OUT_ANY (any trace fields and/or statistics), TMH_OUT_TRACE3 (exactly pv,
+ * meter, residual, no statistics: the trace-mode hot path), TMH_OUT_STATS
+ * (statistics only), plus TMH_OUT_SITES with per-chain sites and TMH_OUT_FP64 in
+ * fp64; -1 before the first expansion (and on the sequential path, whose one
+ * kernel serves every output). */
+#define TMH_OUT_ANY 0
+#define TMH_OUT_TRACE3 1
+#define TMH_OUT_STATS 2
+#define TMH_OUT_SITES 16
+#define TMH_OUT_FP64 32
+int tmh_engine_last_expand(const struct tmh_engine* eng);
+
 /* Device math probes for parity tests: out[i] = f(a, x[i]) with
  * f = 0 ndtri, 1 gammaincinv, 2 stdtrit, 3 al_ppf, 4 ndtri (fp32 path),
- * 8 ndtri of the fp64 per-second noise (unpolished). */
+ * 8 ndtri of the fp64 per-second noise (unpolished), 9 / 10 the fp32 PV chain's
+ * v_med3_f32 clamps med3(x, 0, a) / med3(x, -inf, a). */
 int tmh_probe(int fn, double a, const double* x, double* out, uint32_t n, void* stream);
 
 #ifdef __cplusplus

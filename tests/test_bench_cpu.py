@@ -142,3 +142,27 @@ def test_secondary_lines_report_a_failed_child(monkeypatch):
 def test_hw_queues_flag_defaults_to_sixteen(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py"])
     assert bench.parse().hw_queues == 16
+
+
+def test_pipeline_defaults_match_bench_schedule():
+    """bench.py and the GPU tests of the timed schedule (tests/test_gpu_trace3.py) take the
+    schedule from tmhpvsim_amd.pipeline.pipeline_defaults: C2 runs the gated schedule with
+    five contexts, two walks in flight and construction four batches ahead; C3 two stats
+    contexts; C4 / C5 day windows (C5 compacted)."""
+    import sys
+    from tmhpvsim_amd.pipeline import pipeline_defaults
+    c2 = pipeline_defaults("c2")
+    assert (c2.mode, c2.pipeline, c2.walks, c2.build_ahead, c2.window, c2.schedule) == ("trace", 5, 2, 4, 86400, "gated")
+    assert not c2.minutes_ahead and not c2.commit_stream and c2.walk_order
+    c3 = pipeline_defaults("c3")
+    assert (c3.mode, c3.pipeline, c3.walks) == ("stats", 2, 1)
+    c4, c5 = pipeline_defaults("c4"), pipeline_defaults("c5")
+    assert c4.window == c5.window == 86400 and c5.compact and not c4.compact
+    import bench
+    old = sys.argv
+    try:
+        sys.argv = ["bench.py"]
+        a = bench.parse()
+    finally:
+        sys.argv = old
+    assert a.cfg == c2

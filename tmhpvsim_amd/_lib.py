@@ -66,10 +66,11 @@ EXPORTS = ["tmh_abi_version", "tmh_last_error", "tmh_state_bytes", "tmh_state_of
            "tmh_set_shape_tables", "tmh_set_sites", "tmh_walk", "tmh_expand",
            "tmh_walk_part", "tmh_expand_part", "tmh_set_clock", "tmh_test_set_segment_capacity",
            "tmh_set_walk_chains_per_row", "tmh_set_walk_lanes", "tmh_set_chain_ids", "tmh_live_chains", "tmh_state_move",
-           "tmh_stream_create_cus", "tmh_stream_destroy", "tmh_set_walk_order"]
+           "tmh_stream_create_cus", "tmh_stream_destroy", "tmh_set_walk_order", "tmh_engine_last_expand"]
 K_EXPAND, K_SEGMENTS, K_CANDIDATES, K_STEP = 0, 1, 2, 3
 WALK_DRAWS, WALK_SEGMENTS = 1, 2
 EXPAND_KERNEL, EXPAND_COMMIT, EXPAND_MINUTES, EXPAND_NO_MINUTES = 1, 2, 4, 8
+OUT_ANY, OUT_TRACE3, OUT_STATS, OUT_SITES, OUT_FP64 = 0, 1, 2, 16, 32   # tmh_engine_last_expand
 
 _lib = None
 
@@ -121,6 +122,9 @@ def load():
         L.tmh_state_move.argtypes = [p, p, u32, p, u32, p, p, u32, C.c_int, p]
     L.tmh_workspace_bytes.argtypes = [u32, u32]
     L.tmh_engine_path.argtypes = [p]
+    if hasattr(L, "tmh_engine_last_expand"):
+        L.tmh_engine_last_expand.argtypes = [p]
+        L.tmh_engine_last_expand.restype = C.c_int
     L.tmh_engine_create.argtypes = [C.POINTER(Params), C.POINTER(Clock), C.c_int, C.POINTER(p)]
     L.tmh_engine_destroy.argtypes = [p]
     if hasattr(L, "tmh_set_clock"):

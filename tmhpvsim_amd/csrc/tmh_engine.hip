@@ -11,7 +11,8 @@
 //    processes are CloudCoverBinary's cloud/clear segment sequence and, in
 //    markov mode, the hour-to-hour cloud cover.
 //      draws: event_draws_kernel (day/hour boundary draws), markov_cc_kernel
-//         (markov mode), candidates_kernel (the next calls' try-0 lengths).
+//         (markov mode), draws_tail_kernel (the next calls' try-0 lengths and the
+//         window's minute draws).
 //      P1 segments_kernel: four chains per wavefront, one per 16-lane row, walk
 //         from segment end to segment end (next_cloud with the sigma scan spread
 //         over the row, DPP argmin and shift) and record each segment as
@@ -44,6 +45,8 @@
 #include "tmhpvsim.h"
 
 using namespace tmh;
+static_assert(OUT_ANY == TMH_OUT_ANY && OUT_TRACE3 == TMH_OUT_TRACE3 && OUT_STATS == TMH_OUT_STATS,
+              "expansion variants: tmh_model.h and include/tmhpvsim.h agree");
 
 namespace {
 
@@ -60,9 +63,9 @@ struct BlockDesc {                 // as of the step before the block start; -1 
 
 // Segment records: a chain's first `cap` records sit in its row of `rec`; records
 // past that go to 256-record chunks of a shared overflow pool, allocated by the
-// walk (atomic counter) and listed per chain in `ovf` (OVF_SLOTS chunks).  cap is
-// sized to ~2.3x the mean calls per window (~387 a day), so the pool
-// serves the windy tail.  TMH_CHAIN_SEGMENT_OVERFLOW is deterministic: a chain
+// walk (atomic counter) and listed per chain in `ovf` (OVF_SLOTS chunks).  cap =
+// (n_steps/135 + 16) rounded up to 16 (seg_cap: 656 a day, ~1.7x the mean 386 calls per
+// window; ~0.3 % of the chain-days spill past it), so the pool serves the windy tail.  TMH_CHAIN_SEGMENT_OVERFLOW is deterministic: a chain
 // past cap + 256 OVF_SLOTS records faults at that record (a property of the chain
 // alone); and when the batch's demand exceeds the pool (some claim failed: the
 // total demand, not the claim order, decides that), overflow_settle_kernel faults
@@ -92,6 +95,7 @@ struct SegView {                   // P1 -> P2 scratch
     uint32_t kcap;
     void* mtab;                    // [nmin][2][n] R: the _next_min draws (cloudy, clear noise) of every minute boundary
     uint32_t nmin;
+    double* mend;                  // [4][n] fp64 draws of the window end's minute boundaries q1, q0 (cloudy, clear; fp32 engines)
     struct FixRec* fix;            // [fixcap] fp32 guard-band seconds for fixup_kernel
     uint32_t fixcap;
     uint32_t* nfix;                // records appended (> fixcap: some were lost, see commit_kernel)
@@ -626,9 +630,10 @@ __device__ __forceinline__ void minute_draws(const DrawParams& dp, uint64_t chai
 }
 
 // the cloud cover in force at the minute boundary at window step jm (the last
-// two hourly draws at or before it, or the window-start pair), interpolated
-__device__ __forceinline__ double minute_cc(const StateView& st, const SegView& sg, uint32_t n, uint32_t c,
-                                            int64_t W0, int64_t jm, const int2* __restrict__ events, int ne,
+// two hourly draws at or before it, or the window-start pair: the state's, or the
+// previous window's walk's end pair when the window is chained to it), interpolated
+__device__ __forceinline__ double minute_cc(const StateView& st, const PrevView& prev, const SegView& sg, uint32_t n,
+                                            uint32_t c, int64_t W0, int64_t jm, const int2* __restrict__ events, int ne,
                                             const double* __restrict__ tab64)
 {
     const int64_t step = W0 + jm;
@@ -640,45 +645,90 @@ __device__ __forceinline__ double minute_cc(const StateView& st, const SegView& 
     }
     const int h0 = lo - 1, h1 = lo - 2;
     const double* evd = sg.evd;
+    const double sb = prev.status ? prev.end_p1[c] : st.sb[S_CC][c];
+    const double sa = prev.status ? prev.end_p1[(size_t)n + c] : st.sa[S_CC][c];
     double pb, pa;
     if (h0 < 0) {
-        pb = st.sb[S_CC][c];
-        pa = st.sa[S_CC][c];
+        pb = sb;
+        pa = sa;
     } else {
         pa = evd[(size_t)h0 * 4 * n + c];
-        pb = h1 < 0 ? st.sa[S_CC][c] : evd[(size_t)h1 * 4 * n + c];
+        pb = h1 < 0 ? sa : evd[(size_t)h1 * 4 * n + c];
     }
     return interp(pb, pa, tab64[(size_t)jm * ROW + G_HOURF]);
 }
 
-// The _next_min draws of every (candidate minute boundary, chain) of the window,
-// one work-item each, before the expansion: minute m sits at window step
-// fm + 60 m.  The expansion and the block-start reconstruction read them instead
-// of drawing in their loops.  R = float: the fp32 kernels' copies (float table).
+// The window's per-chain draws that need the boundary-event draws but not the segment
+// walk: one launch after event_draws_kernel (+ markov_cc_kernel, walk_order_kernel).
+//  * rows y < kcap: the try-0 candidate lengths pow(alpha + delta u, expo) of each
+//    chain's next kcap next_cloud calls (cloud_cover_binary.py:35-40; keyed by (chain,
+//    call number) only, so drawn here at full occupancy instead of one wave-redundant
+//    Philox + pow per call in the walk), stored by walk row;
+//  * rows kcap + m: the _next_min draws (clearskyindexmodel.py:86-95,109-111) of the
+//    window's minute boundary m (window step fm + 60 m) of every chain, which the
+//    expansion's per-second loop, its block-start reconstruction and the commit read
+//    instead of drawing.  R = float: the fp32 kernels' copies, plus the fp64 draws of
+//    the window's last two minute boundaries (the state's noise samplers at the window
+//    end, which commit_kernel stores) in `mend`;
+//  * row 0 also resets the walk's pool / queue counters and the expansion's guard-band
+//    records and statistics accumulators.
+// Chained to the previous window's walk (prev), the window-start status and cloud-cover
+// pair come from that walk, so these draws may run before that window's expansion and
+// commit (tmh_walk_part).  Built with the construction (TMH_WALK_DRAWS), the minute
+// table is off the expansion's stream.
 template <typename R>
-__global__ __launch_bounds__(256) void minute_table_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
-                                                           int64_t W0, uint32_t nsteps, int64_t fm,
-                                                           const double* __restrict__ tab64,
-                                                           const int2* __restrict__ events,
-                                                           const uint32_t* __restrict__ n_events, SegView sg)
+__global__ __launch_bounds__(256) void draws_tail_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
+                                                         int64_t W0, uint32_t nsteps, int64_t fm,
+                                                         const double* __restrict__ tab64,
+                                                         const int2* __restrict__ events,
+                                                         const uint32_t* __restrict__ n_events,
+                                                         const BlockDesc* __restrict__ desc_end, SegView sg,
+                                                         PrevView prev)
 {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t m = blockIdx.y;
-    const int64_t jm = fm + 60 * (int64_t)m;
-    if (m == 0 && c < n) {   // the expansion's guard-band bookkeeping (this kernel runs just before it)
-        if (c == 0) *sg.nfix = 0;
-        sg.corr[c] = 0.0;
-        sg.corr[(size_t)n + c] = 0.0;
-        for (int k = 0; k < 3; ++k) sg.acc_fx[(size_t)k * n + c] = 0;
-        sg.acc_mx[c] = max_key(-INFINITY);
+    const uint32_t y = blockIdx.y;
+    if (y == 0) {
+        if (c == 0) {   // the walk that follows hands out overflow chunks and queued chains
+            *sg.pool_n = 0;
+            *sg.walk_q = 0;
+            *sg.pool_short = 0;
+            *sg.nfix = 0;
+        }
+        if (c < n) {    // the expansion's guard-band corrections and fixed-point statistics
+            sg.corr[c] = 0.0;
+            sg.corr[(size_t)n + c] = 0.0;
+            for (int k = 0; k < 3; ++k) sg.acc_fx[(size_t)k * n + c] = 0;
+            sg.acc_mx[c] = max_key(-INFINITY);
+        }
     }
-    if (c >= n || jm >= (int64_t)nsteps) return;
+    if (c >= n) return;
+    const uint64_t chain = chain0 + gid(dp.ids, c);
+    if (y < sg.kcap) {
+        if ((prev.status ? prev.status[c] : st.status[c]) != 0) return;
+        const U4 b = keyed_block(dp.seed, chain, (uint64_t)(st.ncalls[c] + y), TAG_CLOUD, 0);
+        // stored by walk row: the chains of a walk wavefront read adjacent words
+        sg.cand[(size_t)y * n + (sg.rank ? sg.rank[c] : c)] = pow_d(dp.alpha + dp.delta * u52(b.x, b.y), dp.expo);
+        return;
+    }
+    const uint32_t m = y - sg.kcap;
+    const int64_t jm = fm + 60 * (int64_t)m;
+    if (jm >= (int64_t)nsteps) return;
     const int ne = (int)min(*n_events, ev_cap_dev(nsteps));
+    const double cc = minute_cc(st, prev, sg, n, c, W0, jm, events, ne, tab64);
     double cloudy, clear;
-    minute_draws<R>(dp, chain0 + gid(dp.ids, c), W0 + jm, minute_cc(st, sg, n, c, W0, jm, events, ne, tab64), cloudy, clear);
+    minute_draws<R>(dp, chain, W0 + jm, cc, cloudy, clear);
     R* t = reinterpret_cast<R*>(sg.mtab);
     t[(size_t)(2 * m) * n + c] = (R)cloudy;
     t[(size_t)(2 * m + 1) * n + c] = (R)clear;
+    if constexpr (sizeof(R) == 4) {   // the window end's last two minute boundaries, in fp64
+        const BlockDesc de = *desc_end;
+        const int q = (int32_t)m == de.q0 ? 1 : ((int32_t)m == de.q1 ? 0 : -1);
+        if (q >= 0) {
+            minute_draws<double>(dp, chain, W0 + jm, cc, cloudy, clear);
+            sg.mend[(size_t)(2 * q) * n + c] = cloudy;
+            sg.mend[(size_t)(2 * q + 1) * n + c] = clear;
+        }
+    }
 }
 
 // cc / clear_day / noise pairs described by `d`, from the draw tables (start = window start)
@@ -1087,25 +1137,6 @@ __device__ __forceinline__ void fractions_at(const WinClock& w, int32_t j, const
     }
 }
 
-// try-0 candidate lengths of the next kcap next_cloud calls of every chain:
-// keyed by (chain, call number) only, so they are drawn before the walk, at
-// full occupancy, instead of one wave-redundant Philox + pow per call inside it
-__global__ __launch_bounds__(256) void candidates_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
-                                                         SegView sg, PrevView prev)
-{
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t k = blockIdx.y;
-    if (c == 0 && k == 0) {   // the walk that follows hands out overflow chunks and queued chains
-        *sg.pool_n = 0;
-        *sg.walk_q = 0;
-        *sg.pool_short = 0;
-    }
-    if (c >= n || (prev.status ? prev.status[c] : st.status[c]) != 0) return;
-    const U4 b = keyed_block(dp.seed, chain0 + gid(dp.ids, c), (uint64_t)(st.ncalls[c] + k), TAG_CLOUD, 0);
-    // stored by walk row: the chains of a walk wavefront read adjacent words
-    sg.cand[(size_t)k * n + (sg.rank ? sg.rank[c] : c)] = pow_d(dp.alpha + dp.delta * u52(b.x, b.y), dp.expo);
-}
-
 // Walk rows ordered by the chain's wind over the window, windiest first.  A chain's
 // next_cloud calls per window grow with its wind speed (the cloud lengths are x / ws;
 // correlation 0.84 between calls and the window-start wind pair's sum over 4,096 oracle
@@ -1114,7 +1145,7 @@ __global__ __launch_bounds__(256) void candidates_kernel(DrawParams dp, StateVie
 // (17 % at 16 chains per wavefront), and the busiest wavefronts are dispatched first.
 // Faulted chains last.  Bitonic sort of (key, chain) per tile of ORDER_TILE rows in LDS.
 // The walk's results do not depend on the order (each group walks its own chain).  The
-// try-0 candidate table is stored by walk row (candidates_kernel writes row rank[c]), so
+// try-0 candidate table is stored by walk row (draws_tail_kernel writes row rank[c]), so
 // a wavefront's candidate loads stay on shared cache lines as in chain order (read by
 // chain, the scattered rows made the 16-chain C3 walk 3.7x slower).
 constexpr uint32_t ORDER_TILE = 4096;
@@ -1334,7 +1365,7 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
     };
     uint32_t ncall0 = 0, ncall = 0;
     // call ncall0 + k's try-0 length: the table, or past it (the windiest chains) drawn here,
-    // one per lane of the group per refill, as candidates_kernel would have
+    // one per lane of the group per refill, as draws_tail_kernel would have
     auto cand_at = [&](uint32_t k) {
         if (k < sg.kcap) return sg.cand[(size_t)k * n + r];   // stored by walk row
         const U4 b = keyed_block(dp.seed, chain0 + gid(dp.ids, c), (uint64_t)(ncall0 + k), TAG_CLOUD, 0);
@@ -1866,7 +1897,7 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
         } else {
             second_body<R>(kp, pkv, row, flp, fs, covered, noise_z<R>(un), meter_w<R>(um), csi, pv, meter, res, held);
         }
-        held = held && ok;
+        held = held && ok && live;   // lanes past the last chain run on uninitialised samplers: never held
         if constexpr (sizeof(R) == 4) {
             if (held) {   // jb is wave-uniform: the word and the bit are scalars
                 uint32_t* hw = reinterpret_cast<uint32_t*>(&held_lds[threadIdx.x]) + (jb >> 5);
@@ -1931,7 +1962,7 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
     if constexpr (sizeof(R) == 4) {
         const uint4 hm = held_lds[threadIdx.x];
         const bool held_any = (hm.x | hm.y | hm.z | hm.w) != 0;
-        if (held_any) {   // (chain, block, seconds) for fixup_kernel (outside the loop: no registers held across it)
+        if (live && held_any) {   // (chain, block, seconds) for fixup_kernel (outside the loop: no registers held across it)
             const uint32_t k = atomicAdd(sg.nfix, 1u);
             if (k < sg.fixcap) sg.fix[k] = FixRec{c, b, jr, 0u, hm};
         }
@@ -2028,7 +2059,9 @@ __global__ __launch_bounds__(256) void state_move_kernel(StateView src, StateVie
 // residual are overwritten; the statistics get the exact differences of the
 // sums (fp32 values in fp64 differ exactly, so the corrections add up in any
 // order), the final residual's maximum and histogram count (the expansion left
-// these seconds out of both).  Grid-stride over (record, second of the block).
+// these seconds out of both).  One work-item per (record, second of its block):
+// the kernel's duration is one second's recomputation (a latency-bound fp64 chain),
+// not a record's mask of them in a row.  Grid-stride over the records.
 template <bool SITES>
 __global__ __launch_bounds__(256) void fixup_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
                                                     int64_t W0, uint32_t nsteps, int64_t utc0,
@@ -2041,15 +2074,16 @@ __global__ __launch_bounds__(256) void fixup_kernel(KParams kp, DrawParams dp, S
 {
     const uint32_t nrec = min(*sg.nfix, sg.fixcap);
     const int ne = (int)min(*n_events, ev_cap_dev(nsteps));
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < 4 * nrec; t += gridDim.x * blockDim.x) {
-      const FixRec fr = sg.fix[t >> 2];   // four work-items per record, one per 32-second mask word
-      const uint32_t w = t & 3;
-      uint32_t mw = w == 0 ? fr.mask.x : (w == 1 ? fr.mask.y : (w == 2 ? fr.mask.z : fr.mask.w));
-      const uint32_t c = fr.c;
-      const BlockDesc db = desc[fr.b];
-      while (mw) {   // usually one second
-        const uint32_t i = 32 * w + (uint32_t)__builtin_ctz(mw);
-        mw &= mw - 1;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < (uint64_t)BLOCK_STEPS * nrec;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t i = (uint32_t)(t % BLOCK_STEPS);   // second of the record's block
+        const FixRec& fr = sg.fix[t / BLOCK_STEPS];
+        const uint32_t w = i >> 5;
+        const uint32_t mw = w == 0 ? fr.mask.x : (w == 1 ? fr.mask.y : (w == 2 ? fr.mask.z : fr.mask.w));
+        if (!((mw >> (i & 31)) & 1u)) continue;
+        const uint32_t c = fr.c;
+        if (c >= n || fr.b >= sg.nblk) continue;   // (never appended: the expansion records live chains only)
+        const BlockDesc db = desc[fr.b];
         const uint32_t j = fr.b * BLOCK_STEPS + i;
         float pv32, meter, pv;
         if (!redo_second<SITES>(kp, dp, st, sg, n, c, chain0, W0, utc0, j, db, fr.jr, events, ne, tab64, tab32, sun,
@@ -2069,40 +2103,36 @@ __global__ __launch_bounds__(256) void fixup_kernel(KParams kp, DrawParams dp, S
             const int bin = x < 0.0 ? 0 : (x >= (double)(sv.n_bins - 1) ? (int)sv.n_bins - 1 : (int)x);
             atomicAdd((unsigned long long*)&sv.hist[bin], 1ull);
         }
-      }
     }
 }
 
-// The window's per-chain statistics (fixed-point block sums + fixup_kernel's exact
-// corrections) into the caller's accumulators; every input is order-free, so the
-// result is deterministic.
-__global__ __launch_bounds__(256) void stats_commit_kernel(uint32_t n, SegView sg, StatsView sv,
-                                                           const uint32_t* __restrict__ ids, uint32_t acc_n)
-{
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n) return;
-    const double p = (double)sg.acc_fx[c] * sg.fx_inv + sg.corr[c];
-    const double m = (double)sg.acc_fx[(size_t)n + c] * sg.fx_inv;
-    const double r = (double)sg.acc_fx[2 * (size_t)n + c] * sg.fx_inv + sg.corr[(size_t)n + c];
-    const double mx = max_unkey(sg.acc_mx[c]);
-    const uint32_t g = gid(ids, c);
-    const size_t an = acc_n ? acc_n : n;   // acc rows: the full batch
-    sv.acc[g] += p;
-    sv.acc[an + g] += m;
-    sv.acc[2 * an + g] += r;
-    sv.acc[3 * an + g] = fmax(sv.acc[3 * an + g], mx);
-}
-
+// The window's end, one work-item per chain, after the expansion (and the fixup):
+//  * statistics (sv.acc): the window's fixed-point block sums + the fixup's exact
+//    corrections into the caller's fp64 accumulators (every input is order-free, so
+//    the result is deterministic);
+//  * state: the window-end sampler pairs (the last hour / clear-day events from the
+//    draw tables, the last two minute draws: fp32 engines take the fast copies from the
+//    minute table and the fp64 ones from `mend`), the walk's wind pair and status.
 template <typename R>
 __global__ __launch_bounds__(256) void commit_kernel(StateView st, uint32_t n, SegView sg, StatsView sv, MinuteCtx mc0,
                                                      const uint32_t* __restrict__ n_events,
                                                      const BlockDesc* __restrict__ desc_end, int markov,
-                                                     uint32_t acc_n)
+                                                     const uint32_t* __restrict__ ids, uint32_t acc_n)
 {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n) return;   // the statistics: stats_commit_kernel, launched before
-    (void)sv;
-    (void)acc_n;
+    if (c >= n) return;
+    if (sv.acc) {
+        const double p = (double)sg.acc_fx[c] * sg.fx_inv + sg.corr[c];
+        const double m = (double)sg.acc_fx[(size_t)n + c] * sg.fx_inv;
+        const double r = (double)sg.acc_fx[2 * (size_t)n + c] * sg.fx_inv + sg.corr[(size_t)n + c];
+        const double mx = max_unkey(sg.acc_mx[c]);
+        const uint32_t g = gid(ids, c);
+        const size_t an = acc_n ? acc_n : n;   // acc rows: the full batch
+        sv.acc[g] += p;
+        sv.acc[an + g] += m;
+        sv.acc[2 * an + g] += r;
+        sv.acc[3 * an + g] = fmax(sv.acc[3 * an + g], mx);
+    }
     if (st.status[c] != 0) return;
     // records lost (never observed: room for ~100x the measured rate): the batch's
     // chains are marked, as it is not known whose seconds were not recomputed
@@ -2117,19 +2147,30 @@ __global__ __launch_bounds__(256) void commit_kernel(StateView st, uint32_t n, S
     MinuteCtx mc = mc0;
     mc.chain += gid(mc.dp.ids, c);
     mc.ne = (int)min(*n_events, sg.evcap);
-    if constexpr (sizeof(R) == 4) {   // the fast noise copies from the fp32 table, the fp64 pairs drawn again
+    const BlockDesc de = *desc_end;
+    if constexpr (sizeof(R) == 4) {   // the fast noise copies from the fp32 table, the fp64 pairs from mend
         Samp sf = sp;
         load_fast_noise(st, c, sf);
-        samplers_at<float>(*desc_end, sg, n, c, sf, mc, st);
+        samplers_at<float>(de, sg, n, c, sf, mc, st);
         st.fn[0][c] = make_float2((float)sf.b[S_CLOUDY_NOISE], (float)sf.a[S_CLOUDY_NOISE]);
         st.fn[1][c] = make_float2((float)sf.b[S_CLEAR_NOISE], (float)sf.a[S_CLEAR_NOISE]);
-        exact_noise_at(*desc_end, mc.dp, st, sg, n, c, mc0.chain, mc.W0, mc.fm, mc.events, mc.tab64, sp);
+        if (de.q0 >= 0) {   // as exact_noise_at: q1's draws (or the pair's after value), then q0's
+            if (de.q1 >= 0) {
+                sp.b[S_CLOUDY_NOISE] = sg.mend[c];
+                sp.b[S_CLEAR_NOISE] = sg.mend[(size_t)n + c];
+            } else {
+                sp.b[S_CLOUDY_NOISE] = sp.a[S_CLOUDY_NOISE];
+                sp.b[S_CLEAR_NOISE] = sp.a[S_CLEAR_NOISE];
+            }
+            sp.a[S_CLOUDY_NOISE] = sg.mend[2 * (size_t)n + c];
+            sp.a[S_CLEAR_NOISE] = sg.mend[3 * (size_t)n + c];
+        }
         for (int k : {S_CC, S_CLEAR_DAY}) {
             sp.b[k] = sf.b[k];
             sp.a[k] = sf.a[k];
         }
     } else {
-        samplers_at<R>(*desc_end, sg, n, c, sp, mc, st);
+        samplers_at<R>(de, sg, n, c, sp, mc, st);
     }
 #pragma unroll
     for (int k = 0; k < 5; ++k) {   // cc, clear_day, cloudy_hour (unchanged), noises
@@ -2163,6 +2204,7 @@ __global__ void probe_kernel(int fn, double a, const double* x, double* out, uin
         case 6: v = dpp_f64<0x138>(a, x[i]); break;            // wave_shr:1, lane 0 <- a
         case 7: v = readlane_f64(x[i], 63); break;
         case 9: v = (double)__builtin_amdgcn_fmed3f((float)x[i], 0.0f, (float)a); break;   // pv_power_f's final clamp
+        case 10: v = (double)__builtin_amdgcn_fmed3f((float)x[i], -INFINITY, (float)a); break;   // its min(csi, csimax)
         default: v = NAN;
     }
     out[i] = v;
@@ -2339,6 +2381,8 @@ size_t scratch_layout(uint32_t n, uint32_t n_steps, void* base, SegView* v, size
         v->mtab = (void*)(b + o);
     }
     o += align_up((size_t)n * nmin * 2 * rbytes);
+    if (v) v->mend = (double*)(b + o);
+    o += align_up((size_t)n * 4 * 8);
     const uint32_t fc = fix_cap(n, n_steps);
     if (v) {
         v->fixcap = fc;
@@ -2370,6 +2414,7 @@ struct tmh_engine {
     uint32_t walk_cpr = 1;  // chains per walk row (tmh_set_walk_chains_per_row)
     uint32_t walk_lanes = 0;  // lanes per chain in the walk (tmh_set_walk_lanes; 0: by batch size)
     bool walk_order = true;   // walk rows windiest chain first (tmh_set_walk_order)
+    int last_expand = -1;     // TMH_OUT_* of the last expansion launched (tmh_engine_last_expand)
     // kernel timing (tmh_profile_*): event pairs per kernel, read and recycled
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[TMH_K_COUNT];
@@ -2594,6 +2639,8 @@ int tmh_engine_destroy(struct tmh_engine* eng)
 }
 
 int tmh_engine_path(const struct tmh_engine* eng) { return eng ? eng->path : TMH_E_INVAL; }
+
+int tmh_engine_last_expand(const struct tmh_engine* eng) { return eng ? eng->last_expand : TMH_E_INVAL; }
 
 int tmh_set_shape_tables(struct tmh_engine* eng, const double* shapes, const int32_t* is_t, uint32_t n_chains)
 {
@@ -2872,8 +2919,18 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
         else
             sg.order = sg.rank = nullptr;
         hipEvent_t t_cand = eng->mark(s);
-        hipLaunchKernelGGL(candidates_kernel, dim3(cb, sg.kcap), dim3(256), 0, s, eng->dp, v, chain0, n_chains, sg,
-                           prev);
+        {   // candidates + the window's minute draws (+ counter resets), one launch
+            const int64_t fmh = first_minute_host(utc0, step0);
+            const uint32_t nm = fmh < (int64_t)n_steps ? (uint32_t)((n_steps - 1 - fmh) / 60 + 1) : 0;
+            const dim3 grid(cb, sg.kcap + nm);
+            const BlockDesc* de = pv.desc + nblk_of(n_steps);
+            if (f64)
+                hipLaunchKernelGGL(draws_tail_kernel<double>, grid, dim3(256), 0, s, eng->dp, v, chain0, n_chains, step0,
+                                   n_steps, fmh, pv.tab64, pv.events, pv.n_events, de, sg, prev);
+            else
+                hipLaunchKernelGGL(draws_tail_kernel<float>, grid, dim3(256), 0, s, eng->dp, v, chain0, n_chains, step0,
+                                   n_steps, fmh, pv.tab64, pv.events, pv.n_events, de, sg, prev);
+        }
         eng->close(TMH_K_CANDIDATES, t_cand, s);
         if (int rc = hip_check(hipGetLastError(), "draws kernels launch")) return rc;
     }
@@ -2897,21 +2954,6 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     hipLaunchKernelGGL(overflow_settle_kernel, dim3(cb), dim3(256), 0, s, n_chains, sg);
     eng->close(TMH_K_SEGMENTS, t_seg, s);
     if (int rc = hip_check(hipGetLastError(), "segments kernel launch")) return rc;
-    }
-    if ((phases & PH_MINUTES) || ((phases & PH_EXPAND) && !(phases & PH_NO_MINUTES))) {
-    {   // the window's minute draws, one work-item each (read by the expansion and the commit)
-        const int64_t fmh = first_minute_host(utc0, step0);
-        const uint32_t nm = fmh < (int64_t)n_steps ? (uint32_t)((n_steps - 1 - fmh) / 60 + 1) : 0;
-        // row 0 of the grid also resets the expansion's bookkeeping (guard-band records,
-        // corrections, the fixed-point statistics): launched even without a minute boundary
-        const uint32_t gy = std::max(nm, 1u);
-        if (f64)
-            hipLaunchKernelGGL(minute_table_kernel<double>, dim3(cb, gy), dim3(256), 0, s, eng->dp, v, chain0,
-                               n_chains, step0, n_steps, fmh, pv.tab64, pv.events, pv.n_events, sg);
-        else
-            hipLaunchKernelGGL(minute_table_kernel<float>, dim3(cb, gy), dim3(256), 0, s, eng->dp, v, chain0,
-                               n_chains, step0, n_steps, fmh, pv.tab64, pv.events, pv.n_events, sg);
-    }
     }
     if (phases & PH_EXPAND) {
     hipEvent_t t_exp = eng->mark(s);
@@ -2943,15 +2985,16 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
         else LAUNCH(float, OUT_ANY, false);
     }
 #undef LAUNCH
+    eng->last_expand = (eng->kp.sites ? (TMH_OUT_ANY | TMH_OUT_SITES) : out) | (f64 ? TMH_OUT_FP64 : 0);
     eng->close(TMH_K_EXPAND, t_exp, s);
     if (int rc = hip_check(hipGetLastError(), "expand_kernel launch")) return rc;
     }
     if (!(phases & PH_COMMIT)) return TMH_OK;
     if (!f64 && eng->kp.with_pv) {   // the fp32 guard-band seconds, in fp64
-        // grid-stride over the records: ~1.3e-3 of the (chain, block)s, so about one 256-thread
-        // workgroup per 2^17 of them (C3: 1 M chains x 675 blocks -> 4,096 workgroups; was 64,
-        // 8.3 ms per batch on a quarter of the CUs)
-        const uint32_t gx = (uint32_t)std::min<uint64_t>(4096, std::max<uint64_t>(64, (uint64_t)n_chains * sg.nblk >> 17));
+        // one work-item per (record, second): records are ~1.3e-3 of the (chain, block)s, so
+        // ~n nblk / 3,000 workgroups of 256 cover them in one pass (C2: ~900); grid-stride past
+        // 16,384 (C3: 1 M chains x 675 blocks)
+        const uint32_t gx = (uint32_t)std::min<uint64_t>(16384, std::max<uint64_t>(64, (uint64_t)n_chains * sg.nblk / 3000));
         if (eng->kp.sites)
             hipLaunchKernelGGL(fixup_kernel<true>, dim3(gx), dim3(256), 0, s, eng->kp, eng->dp, v, chain0, n_chains, step0,
                                n_steps, utc0, pv.tab64, pv.tab32, pv.sun, pv.events, pv.n_events, pv.desc, sg, tv, sv);
@@ -2961,15 +3004,13 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
         if (int rc = hip_check(hipGetLastError(), "fixup_kernel launch")) return rc;
     }
     const MinuteCtx mc{eng->dp, chain0, step0, first_minute_host(utc0, step0), pv.events, 0, pv.tab64};
-    if (sv.acc)
-        hipLaunchKernelGGL(stats_commit_kernel, dim3(cb), dim3(256), 0, s, n_chains, sg, sv, eng->dp.ids,
-                           eng->kp.ids ? eng->kp.ids_n : 0u);
+    const uint32_t acc_n = eng->kp.ids ? eng->kp.ids_n : 0u;
     if (f64)
         hipLaunchKernelGGL(commit_kernel<double>, dim3(cb), dim3(256), 0, s, v, n_chains, sg, sv, mc, pv.n_events,
-                           pv.desc + nblk_of(n_steps), eng->dp.markov, eng->kp.ids ? eng->kp.ids_n : 0u);
+                           pv.desc + nblk_of(n_steps), eng->dp.markov, eng->dp.ids, acc_n);
     else
         hipLaunchKernelGGL(commit_kernel<float>, dim3(cb), dim3(256), 0, s, v, n_chains, sg, sv, mc, pv.n_events,
-                           pv.desc + nblk_of(n_steps), eng->dp.markov, eng->kp.ids ? eng->kp.ids_n : 0u);
+                           pv.desc + nblk_of(n_steps), eng->dp.markov, eng->dp.ids, acc_n);
     eng->close(TMH_K_STEP, t_step, s);
     return hip_check(hipGetLastError(), "commit_kernel launch");
 }

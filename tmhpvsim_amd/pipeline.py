@@ -1,0 +1,448 @@
+"""Batches of chains in flight on one GPU: the schedules bench.py times.
+
+A batch = one BatchedSim engine's n chains constructed fresh (tmh_init, new global
+ids every batch) and advanced over `secs` seconds (tmh_plan + tmh_walk_part +
+tmh_expand_part, or tmh_step per window).  Several batches are in flight at once,
+each in its own context (state, plan, scratch, outputs), so the latency-bound
+segment walks of the next batches run beside this batch's expansion
+(DESIGN.md "The C2 pipeline").  bench.py times `BatchPipeline.run`; the GPU tests
+(tests/test_gpu_trace3.py) run the same object and compare every batch's trace
+with a separate tmh_run of the same chains, so the timed schedule is the tested
+one.
+
+Reference: the batch replaces n chains of `pvsim`'s per-second loop
+(/root/reference/tmhpvsim/pvsim.py:72-84: PVModel.next, get_meter_value,
+meter - pv), one ClearskyindexModel per chain (clearskyindexmodel.py:57-160).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+from . import _lib
+
+
+@dataclass
+class PipelineConfig:
+    """How batches overlap (bench.py's flags; `pipeline_defaults` gives each workload's)."""
+    mode: str = "trace"          # "trace": pv, meter, residual traces; "stats": on-GPU statistics
+    window: int = 86400          # steps per tmh_step window (a batch of secs > window runs windows in order)
+    pipeline: int = 5            # contexts (batches in flight)
+    walks: int = 2               # gated schedule: segment walks in flight
+    build_ahead: int = 4         # gated: construction of batch k + A released when walk k ends
+    stagger: bool = True         # one-window batches software-pipelined (else one tmh_step each, in turn)
+    schedule: str = "gated"      # "gated" or round 1's "stagger"
+    build_on: str = "walk"       # stagger schedule: construction on the walk or the expansion stream
+    walk_priority: str = "normal"
+    expand_priority: str = "normal"
+    build_priority: str = "normal"
+    minutes_ahead: bool = False  # gated: minute table with the construction instead of before the expansion
+    commit_stream: bool = False  # gated: fixup + commit on a stream of their own
+    walk_order: bool = True      # walk rows windiest chain first (the run's first walk in chain order)
+    walk_cus: int = 0            # gated: segment walks on CU-mask bits 0 .. K-1 (0 = all CUs)
+    other_cus: str = "all"       # with walk_cus: the other streams on all CUs or the rest
+    compact: bool = False        # multi-window stats batches: later windows on the live chains only
+    timeline: bool = False       # gated: HIP events around every build, walk and expansion
+    hist_bins: int = 4096
+    hist_lo: float = -300.0
+    hist_hi: float = 9000.0
+
+
+def pipeline_defaults(workload, precision="fp32", seconds=None, window=None, walks=None, build_ahead=None,
+                      pipeline=None, compact=None, mode=None, **overrides):
+    """The measured-best schedule of each BASELINE.json workload (DESIGN.md "The C2
+    pipeline", "C3, C4, C5"): bench.py's defaults, shared with the tests that check
+    the timed schedule."""
+    c5, c4 = workload == "c5", workload == "c4"
+    secs = seconds or {"c2": 86400, "c3": 86400, "c4": 365 * 86400, "c5": 604800}[workload]
+    mode = mode or ("trace" if workload == "c2" else "stats")
+    # C2: two walks in flight (r02, same-box A/B: 1.71-1.72 ms per batch against 1.81 with one)
+    walks = walks if walks is not None else (2 if workload == "c2" else 1)
+    # construction released walks + 2 batches ahead (round 3, 16 queues, same box, 3 reps:
+    # 1.41-1.44 ms per C2 batch at 4, 5 or 6 ahead against 1.48-1.55 at 3, 1.86-1.90 at 2)
+    build_ahead = build_ahead or max(1, walks) + (2 if walks > 1 else 1)
+    # c3: two 1 M-chain batches in flight (2 x ~27 GB of state + scratch): +3 % over one (r02)
+    pipeline = pipeline or (2 if workload == "c3" else build_ahead + 1)
+    cfg = PipelineConfig(
+        mode=mode,
+        window=min(window or (86400 if (c5 or c4) else secs), secs),
+        pipeline=pipeline, walks=walks, build_ahead=build_ahead,
+        # C2 (same-box A/B, r01): construction on the walk stream at normal priority
+        # 1.94e11 chain-s/s vs 1.82e11 on the expansion stream with high-priority walks
+        build_on="walk" if workload == "c2" else "expand",
+        walk_priority="normal" if workload == "c2" else "high",
+        compact=bool(c5 if compact is None else compact),
+    )
+    for k, v in overrides.items():
+        if v is not None:
+            setattr(cfg, k, v)
+    return cfg
+
+
+class BatchPipeline:
+    """`cfg.pipeline` contexts of `n` chains each over `secs` seconds on `sim`'s engine.
+    chain0_of(k): global id of the first chain of batch k (fresh chains every batch)."""
+
+    def __init__(self, sim, n, secs, cfg: PipelineConfig, chain0_of, device):
+        import torch
+        self.torch = torch
+        self.L = L = _lib.load()
+        self.sim, self.n, self.secs, self.cfg, self.chain0_of, self.dev = sim, n, secs, cfg, chain0_of, device
+        self.win = win = min(cfg.window, secs)
+        self.nwin = nwin = (secs + win - 1) // win
+        prio_lo, prio_hi = torch.cuda.Stream.priority_range()
+        self._prio = lambda s: prio_hi if s == "high" else prio_lo
+        pipe = self
+
+        class Ctx:   # one batch in flight: its own state, plan, scratch, outputs and HIP streams
+            # The context's own streams are created on first use: the gated schedule runs on
+            # shared streams, and every extra stream shares one of HIP's few hardware queues
+            # with a busy one (a queue runs its packets in order, across streams).
+            @property
+            def stream(self):
+                if self._stream is None:
+                    self._stream = torch.cuda.Stream(device)
+                return self._stream
+
+            @property
+            def sptr(self):
+                return C.c_void_p(self.stream.cuda_stream)
+
+            @property
+            def wstream(self):   # the walk runs on a stream of its own
+                if self._wstream is None:
+                    self._wstream = torch.cuda.Stream(device, priority=pipe._prio(cfg.walk_priority))
+                return self._wstream
+
+            @property
+            def wptr(self):
+                return C.c_void_p(self.wstream.cuda_stream)
+
+            def __init__(self):
+                self._stream = self._wstream = None
+                self.chain0 = None
+                self.walked = torch.cuda.Event()
+                self.done = torch.cuda.Event()
+                self.kernel_done = torch.cuda.Event()
+                self.expanded = None   # recorded after this context's last expansion
+                self.state = torch.zeros(L.tmh_state_bytes(n), dtype=torch.uint8, device=device)
+                self.plan = torch.empty(L.tmh_plan_bytes(win), dtype=torch.uint8, device=device)
+                self.scratch = torch.empty(L.tmh_engine_scratch_bytes(sim._eng, n, win), dtype=torch.uint8,
+                                           device=device)
+                if cfg.compact and cfg.mode == "stats" and nwin > 1:   # compacted windows: a working state
+                    self.work = torch.empty_like(self.state)
+                    self.ids = torch.empty(n, dtype=torch.int32, device=device)
+                    self.nlive = torch.zeros(1, dtype=torch.int32, device=device)
+                if nwin > 1:   # second plan + scratch: window w+1's walk beside window w's expansion
+                    self.plan2 = torch.empty_like(self.plan)
+                    self.scratch2 = torch.empty_like(self.scratch)
+                    self.wev = [torch.cuda.Event(), torch.cuda.Event()]
+                    self.eev = [torch.cuda.Event(), torch.cuda.Event()]
+                self.trace = {f: torch.empty(win, n, dtype=sim.real, device=device) for f in ("pv", "meter", "residual")} \
+                    if cfg.mode == "trace" else {}
+                self.tr = _lib.Trace(None, None, *(self.trace[f].data_ptr() if f in self.trace else None
+                                                   for f in ("pv", "meter", "residual")), n)
+                self.st = None
+                if cfg.mode == "stats":
+                    self.hist = torch.zeros(cfg.hist_bins, dtype=torch.int64, device=device)
+                    self.acc = torch.zeros(4, n, dtype=torch.float64, device=device)
+                    self.acc[3].fill_(-float("inf"))
+                    self.st = _lib.Stats(self.hist.data_ptr(), cfg.hist_bins, 0, cfg.hist_lo, cfg.hist_hi,
+                                         self.acc.data_ptr())
+
+        self.ctxs = [Ctx() for _ in range(max(1, cfg.pipeline))]
+        # one stream for every batch's expansion: expansions run back to back, in order
+        # (they fill the chip on their own), while the walks of the next batches run on
+        # their own streams beside them
+        self.estream = torch.cuda.Stream(device, priority=self._prio(cfg.expand_priority))
+        W = self.W = max(1, cfg.walks)
+        self.wsts = [torch.cuda.Stream(device, priority=self._prio(cfg.walk_priority)) for _ in range(W)]
+        self.bst = torch.cuda.Stream(device, priority=self._prio(cfg.build_priority))
+        self.cst = torch.cuda.Stream(device)
+        if cfg.walk_cus:   # the walks on a share of every XCD's CUs (CU-masked streams)
+            ncu = torch.cuda.get_device_properties(device).multi_processor_count
+            self.wsts = [_lib.cu_stream(0, cfg.walk_cus, device) for _ in range(W)]
+            if cfg.other_cus == "rest":
+                self.bst, self.cst = (_lib.cu_stream(cfg.walk_cus, ncu - cfg.walk_cus, device) for _ in range(2))
+                self.estream = _lib.cu_stream(cfg.walk_cus, ncu - cfg.walk_cus, device)
+        self.eptr = C.c_void_p(self.estream.cuda_stream)
+        self.bst_p = C.c_void_p(self.bst.cuda_stream)
+        self.A = cfg.build_ahead
+        self.tl = {}   # timeline: per-batch HIP timing events (build done, walk start / end, expansion start / end)
+
+    # ------------------------------------------------------------------ helpers
+    def ctx_of(self, k):
+        return self.ctxs[k % len(self.ctxs)]
+
+    def _p(self, t):
+        return C.c_void_p(t.data_ptr())
+
+    def tl_mark(self, key, j, stream):
+        if self.cfg.timeline:
+            e = self.torch.cuda.Event(enable_timing=True)
+            e.record(stream)
+            self.tl.setdefault(key, {})[j] = e
+
+    def expand_args(self, cx):
+        return (self.sim._eng, self._p(cx.state), cx.chain0, self.n, 0, self.secs, None, C.byref(cx.tr),
+                C.byref(cx.st) if cx.st is not None else None, self._p(cx.plan), self._p(cx.scratch),
+                cx.scratch.numel())
+
+    # ------------------------------------------------------------------ one batch at a time
+    def one_step(self, k):
+        """A whole batch on its context's streams (multi-window batches, or no overlap)."""
+        L, sim, n, secs, win, cfg = self.L, self.sim, self.n, self.secs, self.win, self.cfg
+        cx = self.ctx_of(k)
+        chain0 = cx.chain0 = self.chain0_of(k)                 # fresh global chains every batch
+        _lib.check(L.tmh_init(sim._eng, self._p(cx.state), chain0, n, None, cx.sptr))
+        if self.nwin == 1 or sim.path != "time_parallel":
+            for s0 in range(0, secs, win):   # windows: a trace window is overwritten by the next
+                w = min(win, secs - s0)
+                _lib.check(L.tmh_plan(sim._eng, s0, w, self._p(cx.plan), cx.sptr))
+                _lib.check(L.tmh_step(sim._eng, self._p(cx.state), chain0, n, s0, w, None,
+                                      C.byref(cx.tr), C.byref(cx.st) if cx.st is not None else None,
+                                      self._p(cx.plan), self._p(cx.scratch), cx.scratch.numel(), cx.sptr))
+            return
+        if cfg.compact and cfg.mode == "stats":   # windows in order, the live chains of each only
+            sp = self._p(cx.state)
+            for s0 in range(0, secs, win):
+                w = min(win, secs - s0)
+                nl, cur = n, cx.state
+                if s0 > 0:
+                    _lib.check(L.tmh_live_chains(sim._eng, sp, n, None, self._p(cx.ids), self._p(cx.nlive), cx.sptr))
+                    cx.stream.synchronize()                # n_live was written on the batch's stream
+                    nl = int(cx.nlive.item())
+                    if nl < n:
+                        cur = cx.work
+                        if nl:
+                            _lib.check(L.tmh_state_move(sim._eng, sp, n, self._p(cx.work), nl, self._p(cx.ids),
+                                                        self._p(cx.nlive), nl, 0, cx.sptr))
+                            _lib.check(L.tmh_set_chain_ids(sim._eng, self._p(cx.ids), n))
+                if nl:
+                    _lib.check(L.tmh_plan(sim._eng, s0, w, self._p(cx.plan), cx.sptr))
+                    _lib.check(L.tmh_step(sim._eng, self._p(cur), chain0, nl, s0, w, None, C.byref(cx.tr),
+                                          C.byref(cx.st), self._p(cx.plan), self._p(cx.scratch),
+                                          cx.scratch.numel(), cx.sptr))
+                if nl and cur is cx.work:
+                    _lib.check(L.tmh_state_move(sim._eng, self._p(cx.work), nl, sp, n, self._p(cx.ids),
+                                                self._p(cx.nlive), nl, 1, cx.sptr))
+                _lib.check(L.tmh_set_chain_ids(sim._eng, None, 0))
+            return
+        # multi-window: the segment walk of window w+1 beside the expansion of window w;
+        # plans and draws on the expansion's stream (as BatchedSim.run)
+        bufs = [(cx.plan, cx.scratch), (cx.plan2, cx.scratch2)]
+        wins = [(s0, min(win, secs - s0)) for s0 in range(0, secs, win)]
+        sp = self._p(cx.state)
+
+        def views(w):
+            return tuple(self._p(t) for t in bufs[w & 1])
+
+        def prev_of(w):
+            return (views(w - 1)[1], wins[w - 1][1]) if w > 0 else (None, 0)
+
+        def draws(w):
+            pl, sc = views(w)
+            _lib.check(L.tmh_plan(sim._eng, wins[w][0], wins[w][1], pl, cx.sptr))
+            _lib.check(L.tmh_walk_part(sim._eng, sp, chain0, n, wins[w][0], wins[w][1], pl, sc, cx.scratch.numel(),
+                                       *prev_of(w), _lib.WALK_DRAWS, cx.sptr))
+            cx.wev[w & 1].record(cx.stream)
+
+        def segments(w):
+            pl, sc = views(w)
+            cx.wstream.wait_event(cx.wev[w & 1])
+            _lib.check(L.tmh_walk_part(sim._eng, sp, chain0, n, wins[w][0], wins[w][1], pl, sc, cx.scratch.numel(),
+                                       *prev_of(w), _lib.WALK_SEGMENTS, cx.wptr))
+            cx.eev[w & 1].record(cx.wstream)
+
+        draws(0)
+        segments(0)
+        for w in range(len(wins)):
+            cx.stream.wait_event(cx.eev[w & 1])
+            if w + 1 < len(wins):
+                draws(w + 1)
+                segments(w + 1)
+            pl, sc = views(w)
+            _lib.check(L.tmh_expand(sim._eng, sp, chain0, n, wins[w][0], wins[w][1], None,
+                                    C.byref(cx.tr), C.byref(cx.st) if cx.st is not None else None, pl, sc,
+                                    cx.scratch.numel(), cx.sptr))
+
+    # ------------------------------------------------------------------ round 1's staggered schedule
+    def _build(self, k):      # construction of batch k's chains, its plan and draws
+        L, sim, cx = self.L, self.sim, self.ctx_of(k)
+        cx.chain0 = self.chain0_of(k)
+        if self.cfg.build_on == "walk":   # on the batch's walk stream, after the expansion
+            bs, bp = cx.wstream, cx.wptr   # that last used this context: beside the running expansion
+            if cx.expanded is not None:
+                bs.wait_event(cx.expanded)
+        else:                          # in order on the expansion stream
+            bs, bp = self.estream, self.eptr
+        _lib.check(L.tmh_init(sim._eng, self._p(cx.state), cx.chain0, self.n, None, bp))
+        _lib.check(L.tmh_plan(sim._eng, 0, self.secs, self._p(cx.plan), bp))
+        _lib.check(L.tmh_walk_part(sim._eng, self._p(cx.state), cx.chain0, self.n, 0, self.secs, self._p(cx.plan),
+                                   self._p(cx.scratch), cx.scratch.numel(), None, 0, _lib.WALK_DRAWS, bp))
+        cx.done.record(bs)
+
+    def _start(self, k):      # the segment walk of batch k, on its context's walk stream
+        L, sim, cx = self.L, self.sim, self.ctx_of(k)
+        cx.wstream.wait_event(cx.done)
+        _lib.check(L.tmh_walk_part(sim._eng, self._p(cx.state), cx.chain0, self.n, 0, self.secs, self._p(cx.plan),
+                                   self._p(cx.scratch), cx.scratch.numel(), None, 0, _lib.WALK_SEGMENTS, cx.wptr))
+        cx.walked.record(cx.wstream)
+
+    def _finish(self, k):     # the expansion on the expansion stream, then its commit on the
+        L, cx = self.L, self.ctx_of(k)   # batch's walk stream, beside the next batch's expansion
+        self.estream.wait_event(cx.walked)
+        args_ = self.expand_args(cx)
+        _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_KERNEL, self.eptr))
+        cx.kernel_done.record(self.estream)
+        cx.wstream.wait_event(cx.kernel_done)
+        _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_COMMIT, cx.wptr))
+        if cx.expanded is None:
+            cx.expanded = self.torch.cuda.Event()
+        cx.expanded.record(cx.wstream)
+
+    # ------------------------------------------------------------------ the gated schedule (C2)
+    # One walk stream per walk in flight and one construction stream for all batches.
+    # When the walk of batch k ends, three streams are released together: the
+    # expansion of k, the walk of k + W and the construction of k + A.  Their
+    # workgroups are then dispatched interleaved, so the walk (one long-lived wave
+    # per SIMD) and the construction kernels are resident beside the expansion
+    # instead of queueing behind its 10,800 workgroups (a kernel launched while an
+    # expansion fills the CUs waits for its tail: the walks then ran three at a time,
+    # between expansions, rocprofv3 kernel trace r02).
+    def g_build(self, j, gate):
+        L, sim, cfg = self.L, self.sim, self.cfg
+        cx = self.ctx_of(j)
+        cx.chain0 = self.chain0_of(j)
+        bst, bp = self.bst, self.bst_p
+        if gate is not None:
+            bst.wait_event(gate)
+        if cx.expanded is not None:                        # the context's previous batch is committed
+            bst.wait_event(cx.expanded)
+        _lib.check(L.tmh_init(sim._eng, self._p(cx.state), cx.chain0, self.n, None, bp))
+        _lib.check(L.tmh_plan(sim._eng, 0, self.secs, self._p(cx.plan), bp))
+        _lib.check(L.tmh_walk_part(sim._eng, self._p(cx.state), cx.chain0, self.n, 0, self.secs, self._p(cx.plan),
+                                   self._p(cx.scratch), cx.scratch.numel(), None, 0, _lib.WALK_DRAWS, bp))
+        if cfg.minutes_ahead:   # the minute table needs the draws, not the walk
+            _lib.check(L.tmh_expand_part(*self.expand_args(cx), _lib.EXPAND_MINUTES, bp))
+        cx.done.record(bst)
+        self.tl_mark("built", j, bst)
+
+    def g_walk(self, j):
+        L, sim = self.L, self.sim
+        cx = self.ctx_of(j)
+        wst = self.wsts[j % self.W]
+        wst.wait_event(cx.done)
+        self.tl_mark("walk0", j, wst)
+        _lib.check(L.tmh_walk_part(sim._eng, self._p(cx.state), cx.chain0, self.n, 0, self.secs, self._p(cx.plan),
+                                   self._p(cx.scratch), cx.scratch.numel(), None, 0, _lib.WALK_SEGMENTS,
+                                   C.c_void_p(wst.cuda_stream)))
+        cx.walked.record(wst)
+        self.tl_mark("walk1", j, wst)
+
+    def g_expand(self, j):
+        L, cfg = self.L, self.cfg
+        cx = self.ctx_of(j)
+        es, ep = self.estream, self.eptr
+        es.wait_event(cx.walked)
+        args_ = self.expand_args(cx)
+        self.tl_mark("exp0", j, es)
+        _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_KERNEL | (_lib.EXPAND_NO_MINUTES if cfg.minutes_ahead else 0),
+                                     ep))
+        self.tl_mark("exp1", j, es)
+        if cx.expanded is None:
+            cx.expanded = self.torch.cuda.Event()
+        if cfg.commit_stream:   # fixup + commit beside the next expansion
+            cx.kernel_done.record(es)
+            self.cst.wait_event(cx.kernel_done)
+            _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_COMMIT, C.c_void_p(self.cst.cuda_stream)))
+            cx.expanded.record(self.cst)
+        else:
+            _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_COMMIT, ep))
+            cx.expanded.record(es)
+
+    def run_gated(self, k0, cnt):
+        """W walks in flight: when the walk of batch k ends, the expansion of k, the walk
+        of k + W (on k's walk stream) and the construction of k + A are released together."""
+        L, sim, cfg, W, A = self.L, self.sim, self.cfg, self.W, self.A
+        end = k0 + cnt
+        for j in range(k0, min(k0 + A, end)):
+            # the run's first walk is the pipeline's fill latency (its expansion waits for it with
+            # nothing else to do): chain order, whose windiest wavefront is shorter than the wind
+            # order's (four windy chains); the wind order for the rest, which run beside expansions
+            if cfg.walk_order:
+                _lib.check(L.tmh_set_walk_order(sim._eng, 0 if (j == k0 and W > 1) else 1))
+            self.g_build(j, None)
+        for j in range(k0, min(k0 + W, end)):
+            self.g_walk(j)
+        for k in range(k0, end):
+            gate = self.ctx_of(k).walked
+            if k + A < end:
+                self.g_build(k + A, gate)
+            if k + W < end:
+                self.g_walk(k + W)
+            self.g_expand(k)
+
+    def gated(self):
+        """Whether `run` takes the gated schedule (one-window, staggered batches)."""
+        cfg = self.cfg
+        return (self.nwin == 1 and cfg.stagger and cfg.schedule == "gated"
+                and len(self.ctxs) >= max(self.A + 1, self.W + 2))
+
+    def run(self, k0, cnt):
+        """Batches k0 .. k0 + cnt - 1.  One-window batches are software-pipelined:
+        construction + plan and the expansions run in order, the segment walks of the
+        next batches on their own streams beside them, so the one-wave-per-SIMD walks
+        overlap the expansion instead of running in lockstep with it.  The caller
+        synchronises (the outputs of batch k sit in context k % pipeline)."""
+        cfg = self.cfg
+        if self.nwin > 1 or not cfg.stagger:
+            for k in range(k0, k0 + cnt):
+                self.one_step(k)
+            return
+        if self.gated():
+            self.run_gated(k0, cnt)
+            return
+        D = len(self.ctxs)
+        ahead = D - 1
+        for k in range(k0, min(k0 + D, k0 + cnt)):
+            self._build(k)
+        for k in range(k0, min(k0 + ahead, k0 + cnt)):
+            self._start(k)
+        for k in range(k0, k0 + cnt):
+            if k + ahead < k0 + cnt:
+                self._start(k + ahead)
+            self._finish(k)
+            if k + D < k0 + cnt:
+                self._build(k + D)
+
+    # ------------------------------------------------------------------ statistics
+    def sync(self):
+        torch = self.torch
+        torch.cuda.synchronize()
+        for cx in self.ctxs:   # (streams a schedule never created have nothing to wait for)
+            for st_ in (cx._stream, cx._wstream):
+                if st_ is not None:
+                    st_.synchronize()
+
+    def totals(self):
+        """stats mode: the node-local totals over every context (histogram, energies, peak)."""
+        torch = self.torch
+        hist = sum(cx.hist for cx in self.ctxs)
+        acc = torch.stack([cx.acc for cx in self.ctxs])
+        return dict(energy_pv=acc[:, 0].sum(), energy_meter=acc[:, 1].sum(), energy_residual=acc[:, 2].sum(),
+                    peak_residual=acc[:, 3].max(), hist=hist)
+
+    def reset_stats(self):
+        for cx in self.ctxs:
+            cx.hist.zero_()
+            cx.acc[:3].zero_()
+            cx.acc[3].fill_(-float("inf"))
+
+    def faulted(self):
+        """chains with a nonzero status over the contexts' last batches"""
+        bad = 0
+        for cx in self.ctxs:
+            self.sim.state = cx.state
+            bad += int((self.sim.status() != 0).sum())
+        return bad
