@@ -198,12 +198,19 @@ def parse():
     ap.add_argument("--compact", type=int, default=None,
                     help="multi-window stats workloads: run each window after the first on the chains still "
                          "live (faulted chains, e.g. C5's markov AssertionError, drop out); default 1 for c5")
+    ap.add_argument("--proxy-world", type=int, default=1,
+                    help="one-GPU proxy of an N-GPU strong-scaled run (c3 / c4 / c5): time rank 0's shard of "
+                         "N GPUs (chains / N) alone on this GPU; `value` is then that rank's rate and "
+                         "`projected_node_value` N times it. Not a scaling measurement: the RCCL exchange and "
+                         "the other ranks are absent")
     ap.add_argument("--pipeline", type=int, default=None,
                     help="batches in flight on separate HIP streams (1 = no overlap): the segment walks of the "
                          "next batches (latency-bound, one wave per SIMD) run beside this batch's expansion")
     a = ap.parse_args()
     if a.gpus < 1:
         ap.error("--gpus must be >= 1")
+    if a.proxy_world > 1 and (a.gpus > 1 or a.workload not in STRONG):
+        ap.error("--proxy-world: a one-GPU proxy of a strong-scaled workload (c3 / c4 / c5)")
     from tmhpvsim_amd.pipeline import pipeline_defaults
     c5, c4 = a.workload == "c5", a.workload == "c4"
     a.chains = a.chains or DEFAULT_CHAINS[a.workload]
@@ -238,6 +245,13 @@ SECONDARY = {   # --secondary: the other BASELINE.json configs, each in a child 
     "c3": ["--workload", "c3", "--steps", "4", "--warmup", "1"],
     "c4": ["--workload", "c4", "--steps", "2", "--warmup", "1"],
     "c5": ["--workload", "c5", "--steps", "2", "--warmup", "1"],
+    # one-GPU proxies of the strong-scaled configurations at N = 8 (and C4 at 2, 4): rank 0's
+    # shard timed alone; `projected_efficiency` = N x its rate / the N = 1 rate above
+    "c3_proxy8": ["--workload", "c3", "--proxy-world", "8", "--steps", "6", "--warmup", "2"],
+    "c4_proxy2": ["--workload", "c4", "--proxy-world", "2", "--steps", "4", "--warmup", "1"],
+    "c4_proxy4": ["--workload", "c4", "--proxy-world", "4", "--steps", "4", "--warmup", "1"],
+    "c4_proxy8": ["--workload", "c4", "--proxy-world", "8", "--steps", "4", "--warmup", "1"],
+    "c5_proxy8": ["--workload", "c5", "--proxy-world", "8", "--steps", "4", "--warmup", "1"],
 }
 
 
@@ -263,8 +277,15 @@ def secondary_lines(args):
                                                                "kernel_ms")},
                          "roofline_alone": roof.get("alone"), "faulted_chains": d.get("faulted_chains"),
                          "chain_seconds_live": d.get("chain_seconds_live")}
+            if d.get("proxy_world"):
+                out[name].update(proxy_world=d["proxy_world"], projected_node_value=d["projected_node_value"],
+                                 proxy_note=d["proxy_note"])
         except Exception as e:   # noqa: BLE001 - report, never lose the headline line
             out[name] = {"error": f"{type(e).__name__}: {e}"[:300]}
+    for name, d in out.items():   # strong-scaling readiness on one GPU: N x rank rate / the N = 1 rate
+        base = out.get(name.split("_proxy")[0], {})
+        if d.get("proxy_world") and base.get("value"):
+            d["projected_efficiency"] = d["proxy_world"] * d["value"] / base["value"]
     return out
 
 
@@ -365,7 +386,8 @@ def main():
     from tmhpvsim_amd.dist import all_reduce_stats
 
     L = _lib.load()
-    shard0, n, n_node, scaling = rank_chains(args.workload, args.chains, rank, world)
+    proxy = args.proxy_world if world == 1 else 1
+    shard0, n, n_node, scaling = rank_chains(args.workload, args.chains, rank, world * proxy)
     secs, win = args.seconds, args.window
 
     def batch_chain0(k):   # global id of this rank's first chain in batch k: fresh chains every batch
@@ -441,7 +463,7 @@ def main():
         b = torch.tensor([bad], device=dev, dtype=torch.int64)
         dist.all_reduce(b, op=dist.ReduceOp.SUM)
         bad = int(b[0])
-    chain_seconds = n_node * secs * args.steps                 # every rank's chains (C2: n per rank)
+    chain_seconds = (n if proxy > 1 else n_node) * secs * args.steps   # every rank's chains (C2: n per rank)
     # stats mode: the chain-seconds actually simulated = the histogram's count (a chain
     # that faults, e.g. the reference's AssertionError in markov mode, freezes and
     # records nothing more; edge bins absorb out-of-range residuals)
@@ -513,6 +535,12 @@ def main():
         "effective_trace_gbs": (TB * n * secs / (elapsed / args.steps) / 1e9) if args.mode == "trace" else None,
         "faulted_chains": bad,
     }
+    if proxy > 1:
+        line["proxy_world"] = proxy
+        line["projected_node_value"] = value * proxy
+        line["proxy_note"] = (f"one-GPU proxy: rank 0's shard of {proxy} GPUs ({n} of {n_node} chains) timed alone on one "
+                              "GPU; value = that rank's rate, projected_node_value = value x N (equal shards, no "
+                              "exchange cost); not a scaling measurement")
     tl = pipe.tl
     if args.timeline and "exp0" in tl:
         ks = sorted(k for k in tl["exp0"] if k >= args.warmup and k in tl["exp1"] and k + 1 in tl.get("exp0", {}))

@@ -124,7 +124,12 @@ def test_secondary_lines_default_to_the_full_report_only(monkeypatch, argv, want
     monkeypatch.setattr(sys, "argv", ["bench.py"] + argv)
     a = bench.parse()
     assert a.secondary == want
-    assert set(bench.SECONDARY) == {"c2_fp64", "c3", "c4", "c5"}
+    assert {"c2_fp64", "c3", "c4", "c5"} <= set(bench.SECONDARY)
+    proxies = {k for k in bench.SECONDARY if "_proxy" in k}      # one-GPU proxies of the strong-scaled configs
+    assert proxies == {"c3_proxy8", "c4_proxy2", "c4_proxy4", "c4_proxy8", "c5_proxy8"}
+    for k in proxies:
+        argv = bench.SECONDARY[k]
+        assert argv[argv.index("--proxy-world") + 1] == k.split("proxy")[1]
 
 
 def test_secondary_lines_report_a_failed_child(monkeypatch):

@@ -26,15 +26,51 @@ def test_reference_clearskyindexmodel_test():
     assert m.time.time == t0 + datetime.timedelta(seconds=25 * 3600)
 
 
-def test_reference_pvmodel_test():
-    """tests/test_pvmodel.py:6-10: one day at 1 s, generation >= 0."""
+# README.rst:95-100: the reference's pvsim CSV around noon of 2019-09-06 (one chain)
+README_NOON = np.array([165.172689783798, 157.28289673499341, 169.98499896607225, 161.48141720257405,
+                        169.63913912237203, 173.56040563731491])
+
+
+@pytest.fixture(scope="module")
+def noon_distribution():
+    """4,096 keyed chains (fp64) constructed at 2019-09-06 00:00 Europe/Berlin, as PVModel(t0) is
+    in tests/test_pvmodel.py:6-10, run to 12:10: the stand-in PV system's distribution over chains
+    of the README's six seconds (12:00:00-05) and of the 12:00-12:10 mean."""
+    from tmhpvsim_amd.engine import BatchedSim
+    sim = BatchedSim(4096, "2019-09-06 00:00:00", tz="Europe/Berlin", params=ModelParams(seed=0x9EAD), precision="fp64",
+                     device="cuda:0", horizon=12 * 3600 + 600)
+    pv = sim.run(12 * 3600 + 600, trace=("pv",))["pv"]
+    ok = torch.as_tensor(sim.status() == 0, device="cuda:0")
+    pv = pv[:, ok]
+    return pv[12 * 3600:12 * 3600 + 6].cpu().numpy(), pv[12 * 3600:].mean(0).cpu().numpy()
+
+
+def test_readme_noon_pv_plausibility(noon_distribution):
+    """Plausibility anchor, no parity claim (pvlib's SAM module / CEC inverter and the Linke
+    table are stand-ins here): each of the README's six noon values lies inside the
+    central 98 % of the 4,096 chains' PV at the same second, and near the upper part of it (the
+    README's chain was under a mostly clear sky: 157-174 W against the stand-in system's
+    clear-sky ceiling).  The measured percentiles are recorded in DESIGN.md."""
+    six, _ = noon_distribution
+    q = np.array([(six[s] <= README_NOON[s]).mean() for s in range(6)])   # ECDF of each README value
+    print("README noon values at chain-distribution quantiles", np.round(q, 3),
+          "; chain p50/p90/p99/max at 12:00:00:", np.round(np.percentile(six[0], [50, 90, 99, 100]), 1))
+    assert ((q > 0.01) & (q < 0.99)).all(), q
+
+
+def test_reference_pvmodel_test(noon_distribution):
+    """tests/test_pvmodel.py:6-10: one day at 1 s, generation >= 0; the chain's noon mean within
+    the 4,096-chain distribution of the same quantity (the band the fixture measures, in place
+    of a fixed window)."""
     from tmhpvsim_amd import PVModel
+    _, noon_means = noon_distribution
+    lo, hi = np.percentile(noon_means, [0.05, 99.95])
     t0 = datetime.datetime(2019, 9, 6)
     m = PVModel(t0, seed=5)
     pv = np.array([m.next(t0 + datetime.timedelta(seconds=s)) for s in range(86400)])
     assert (pv >= 0).all() and pv.max() > 0
     noon = pv[12 * 3600:12 * 3600 + 600]
-    assert 10.0 < noon.mean() < 250.0            # README.rst:95-100: ~157-174 W around noon
+    assert lo <= noon.mean() <= hi, (noon.mean(), lo, hi)
 
 
 def test_pvmodel_default_time_streams_a_day():

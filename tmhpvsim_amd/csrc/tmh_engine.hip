@@ -1264,6 +1264,25 @@ constexpr int WALK_CAND = 32;   // try-0 candidates per LDS refill of a chain (o
 // between chunks.  Smaller G: fewer lanes (and issue slots) per chain-call,
 // more chunks per lane.  Output per chain: segment records (first uncovered
 // step, next call step) and the window-end binary state.
+#ifdef TMH_WALK_PROF
+// Diagnostic build only (-DTMH_WALK_PROF, scripts/walk_prof.py): per-lane cycles of the
+// walk loop's sections (s_memtime stamps) over the iterations the lane took part in, its
+// iteration count and total, read back with tmh_debug_walk_prof.  The lanes of a wave's
+// busiest group see every iteration.  Not compiled into the product library.
+constexpr int WPROF_N = 6, WPROF_WAVES = 1 << 18;   // (threads)
+__device__ unsigned long long g_walk_prof[WPROF_WAVES][WPROF_N + 2];
+#define WPROF(i)                                                    \
+    do {                                                            \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();           \
+        wp[i] += t_ - wpt;                                          \
+        wpt = t_;                                                   \
+    } while (0)
+#else
+#define WPROF(i) \
+    do {         \
+    } while (0)
+#endif
+
 template <bool QUEUE, int G>
 __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
                                                           int64_t W0, uint32_t nsteps, tmh_clock ck,
@@ -1471,6 +1490,10 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
     };
     const uint32_t groups = gridDim.x * blockDim.x / G;
     if (live) start_chain();
+#ifdef TMH_WALK_PROF
+    uint64_t wp[WPROF_N] = {0, 0, 0, 0, 0, 0}, wpt = __builtin_amdgcn_s_memtime(), wit = 0;
+    const uint64_t wt0 = wpt;
+#endif
     for (;;) {
         if constexpr (QUEUE) {
             while (live && !(active && e < W1)) {   // group-uniform: the group's chain is done, take the next one
@@ -1489,7 +1512,11 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
         // Every chunk an array of the wave reaches (and, for the shift, the one past it:
         // (last + 1) / G <= L / G) is processed; a reset (L <= 11) stays in the NFIX chunks.
         const int Lmax = wave_max_grp<G>(run ? L : 0);
+        WPROF(0);
         if (!run) continue;
+#ifdef TMH_WALK_PROF
+        ++wit;
+#endif
         while (next_ev <= e) {   // _next_day / _next_hour at steps <= e
             if (ev_fl & FL_DAY) {
                 wsb = wsa;
@@ -1514,6 +1541,7 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
             kb += WALK_CAND;
         }
         const double x0 = cbuf[rel - kb];
+        WPROF(1);
         // ---- next_cloud: tries (cloud_cover_binary.py:82-98)
         int tries = 0, last = -1;
         double ncl = 0.0, bdl = 0.0;
@@ -1565,6 +1593,7 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
             if (tries == 40) break;
         }
         ++ncall;
+        WPROF(2);
         if (last < 0) {   // assert not recurse (:91)
             status = TMH_CHAIN_ASSERT_BINARY;
             fault = (int32_t)(e - W0);
@@ -1605,6 +1634,7 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
                 vl[ch] = first ? nclr : f * nsc;
             }
         }
+        WPROF(3);
         L = last + 2;
         cl = ncl;
         clr = nclr;
@@ -1633,7 +1663,18 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
         }
         put_rec(nrec, (int)(s_start + ceil_thr(cl) - 1), (int)e);
         ++nrec;
+        WPROF(4);
     }
+#ifdef TMH_WALK_PROF
+    {
+        const uint32_t wave = blockIdx.x * blockDim.x + threadIdx.x;
+        if (wave < (uint32_t)WPROF_WAVES) {
+            for (int i = 0; i < WPROF_N; ++i) g_walk_prof[wave][i] = wp[i];
+            g_walk_prof[wave][WPROF_N] = wit;
+            g_walk_prof[wave][WPROF_N + 1] = __builtin_amdgcn_s_memtime() - wt0;
+        }
+    }
+#endif
     if constexpr (!QUEUE)   // one chain per group
         if (live) finish_chain();
 }
@@ -1693,25 +1734,21 @@ constexpr int exp_waves()
 {
     return SITES ? 2 : (sizeof(R) == 8 ? 4 : (OUT == OUT_TRACE3 ? 7 : 6));
 }
-template <typename R, int OUT, bool SITES>
-__global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0,
-                                                     uint32_t n, int64_t W0, uint32_t nsteps, int64_t utc0,
-                                                     const double* __restrict__ tab64,
-                                                     const float* __restrict__ tab32,
-                                                     const double* __restrict__ sun,
-                                                     const int2* __restrict__ events,
-                                                     const uint32_t* __restrict__ n_events,
-                                                     const BlockDesc* __restrict__ desc, SegView sg, TraceView tr,
-                                                     StatsView sv)
+// One (128-second block b, chain block cblk) tile of the expansion: one work-item per
+// chain of the block (the expansion's unit of work, below).  The LDS staging areas are
+// the kernel's (one column per thread, so consecutive tiles need no barrier between them).
+template <typename R, int OUT, bool SITES, int WGT>
+__device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KParams& kp, const DrawParams& dp,
+                                            const StateView& st, uint64_t chain0, uint32_t n, int64_t W0,
+                                            uint32_t nsteps, int64_t utc0, const double* __restrict__ tab64,
+                                            const float* __restrict__ tab32, const double* __restrict__ sun,
+                                            const int2* __restrict__ events, const uint32_t* __restrict__ n_events,
+                                            const BlockDesc* __restrict__ desc, const SegView& sg,
+                                            const TraceView& tr, const StatsView& sv, uint32_t* lds_hist,
+                                            uint32_t (*cov_lds)[WGT], R (*min_lds)[WGT], uint4* held_lds)
 {
-    extern __shared__ uint32_t lds_hist[];
-    const uint32_t c = blockIdx.y * blockDim.x + threadIdx.x;   // grid: x = time block, y = chain block
-    const uint32_t b = blockIdx.x;
+    const uint32_t c = cblk * blockDim.x + threadIdx.x;
     const bool live = c < n;
-    if (sv.hist) {
-        for (uint32_t i = threadIdx.x; i < (sv.n_bins + 1) / 2; i += blockDim.x) lds_hist[i] = 0;   // 16-bit bin pairs
-        __syncthreads();
-    }
     const uint32_t j0 = b * BLOCK_STEPS, j1 = min(j0 + (uint32_t)BLOCK_STEPS, nsteps);
     const uint64_t chain = chain0 + gid(kp.ids, c);
     const int64_t fm = first_minute(utc0, W0);
@@ -1758,9 +1795,6 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
     // waits behind the trace stores (gfx9's vmcnt counts loads and stores alike;
     // per-second record loads cost 42 % of the waves' cycles in such waits, PMC
     // SQ_WAIT_ANY).  Word-major: lane-consecutive dwords, no bank conflicts.
-    constexpr int WGT = exp_wg<R, OUT, SITES>();   // threads per workgroup
-    __shared__ uint32_t cov_lds[4][WGT];
-    __shared__ R min_lds[4][WGT];   // minute boundaries mA, mA + 1 of the block: cloudy, clear noise
     const int32_t s0i = (int32_t)(W0 + j0), s1i = (int32_t)(W0 + j1);
     const int32_t mA = (int32_t)j0 <= (int32_t)fm ? 0 : ((int32_t)j0 - (int32_t)fm + 59) / 60;
     {
@@ -1805,7 +1839,6 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
     uint32_t cov_w = 0;
     const double* evd = sg.evd + c;
     // the guard-band seconds of the lane's block, a bit each, in LDS: no register carried through the loop
-    __shared__ uint4 held_lds[WGT];
     held_lds[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
     // Trace stores: one buffer resource per output for the block's rows (built here,
     // not per store) and one running per-lane byte offset; lanes past the last chain
@@ -1974,9 +2007,71 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
         atomicAdd(fx + 2 * (size_t)n + c, (unsigned long long)llrint(acc.r * sg.fx_scale));
         __hip_atomic_fetch_max(sg.acc_mx + c, max_key(acc.mx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+}
+
+
+// Statistics without per-chain sites (C3, C4) run persistent workgroups: grid = the CUs'
+// resident workgroups, each looping over (chain block, time block) tiles (tile t =
+// blockIdx.x + k gridDim.x, time block fastest).  Each workgroup keeps one LDS histogram
+// of 16-bit bin pairs over all its tiles and flushes it to the device histogram once at
+// its end (plus, after a tile, any bin that reached 2^15: a tile adds at most 128 x 256 =
+// 2^15 to a bin, so no bin overflows 16 bits) -- instead of flushing up to 4,096
+// device-scope 64-bit atomics after every tile (round 3: 2.38 B of HBM writes per
+// chain-second, almost all of them these flushes).  The other outputs keep one tile per
+// workgroup (grid x = time block, y = chain block).
+template <typename R, int OUT, bool SITES>
+constexpr bool exp_persistent()
+{
+    return OUT == OUT_STATS && !SITES;
+}
+template <typename R, int OUT, bool SITES>
+__global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0,
+                                                     uint32_t n, int64_t W0, uint32_t nsteps, int64_t utc0,
+                                                     const double* __restrict__ tab64,
+                                                     const float* __restrict__ tab32,
+                                                     const double* __restrict__ sun,
+                                                     const int2* __restrict__ events,
+                                                     const uint32_t* __restrict__ n_events,
+                                                     const BlockDesc* __restrict__ desc, SegView sg, TraceView tr,
+                                                     StatsView sv)
+{
+    extern __shared__ uint32_t lds_hist[];
+    constexpr int WGT = exp_wg<R, OUT, SITES>();   // threads per workgroup
+    __shared__ uint32_t cov_lds[4][WGT];
+    __shared__ R min_lds[4][WGT];   // minute boundaries mA, mA + 1 of the block: cloudy, clear noise
+    __shared__ uint4 held_lds[WGT];
+    const uint32_t nw = (sv.n_bins + 1) / 2;   // 16-bit bin pairs
+    if (sv.hist) {
+        for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) lds_hist[i] = 0;
+        __syncthreads();
+    }
+    auto tile = [&](uint32_t b, uint32_t cblk) __attribute__((always_inline)) {
+        expand_tile<R, OUT, SITES, WGT>(b, cblk, kp, dp, st, chain0, n, W0, nsteps, utc0, tab64, tab32, sun, events,
+                                        n_events, desc, sg, tr, sv, lds_hist, cov_lds, min_lds, held_lds);
+    };
+    if constexpr (exp_persistent<R, OUT, SITES>()) {
+        const uint32_t ntile = sg.nblk * ((n + WGT - 1) / WGT);
+        for (uint32_t t = blockIdx.x; t < ntile; t += gridDim.x) {
+            tile(t % sg.nblk, t / sg.nblk);
+            if (sv.hist) {   // bins at 2^15 or more go to the device histogram before the next tile
+                __syncthreads();
+                for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) {
+                    const uint32_t w = lds_hist[i], lo = w & 0x8000u ? w & 0xFFFFu : 0u, hi = w & 0x80000000u ? w >> 16 : 0u;
+                    if (lo | hi) {
+                        lds_hist[i] = w - (lo | (hi << 16));
+                        if (lo) atomicAdd((unsigned long long*)&sv.hist[2 * i], (unsigned long long)lo);
+                        if (hi) atomicAdd((unsigned long long*)&sv.hist[2 * i + 1], (unsigned long long)hi);
+                    }
+                }
+                __syncthreads();
+            }
+        }
+    } else {
+        tile(blockIdx.x, blockIdx.y);   // grid: x = time block, y = chain block
+    }
     if (sv.hist) {
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < (sv.n_bins + 1) / 2; i += blockDim.x) {
+        for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) {
             const uint32_t w = lds_hist[i], lo = w & 0xFFFFu, hi = w >> 16;
             if (lo) atomicAdd((unsigned long long*)&sv.hist[2 * i], (unsigned long long)lo);
             if (hi) atomicAdd((unsigned long long*)&sv.hist[2 * i + 1], (unsigned long long)hi);   // hi = 0 past n_bins
@@ -2961,17 +3056,28 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     const int out = (no_stats && tv.pv && tv.meter && tv.residual && !tv.csi && !tv.covered) ? OUT_TRACE3
                     : (!tv.pv && !tv.meter && !tv.residual && !tv.csi && !tv.covered) ? OUT_STATS
                                                                                       : OUT_ANY;
-    auto exp_grid = [&](uint32_t wg) {
+    const size_t lds_exp = stats && stats->hist ? (size_t)((stats->n_bins + 1) / 2) * 4 : 0;   // 16-bit bin pairs
+    // one workgroup per tile, or (persistent statistics kernels) the resident workgroups of
+    // the device, at most one per tile
+    auto exp_grid = [&](uint32_t wg, bool persist, const void* kfn) {
         const uint32_t ecb = (n_chains + wg - 1) / wg;
-        return dim3(sg.nblk, ecb);
+        if (!persist) return dim3(sg.nblk, ecb);
+        const uint64_t ntile = (uint64_t)sg.nblk * ecb;
+        int per_cu = 0, ncu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, (int)wg, lds_exp) != hipSuccess || per_cu < 1)
+            per_cu = 1;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, eng->device) != hipSuccess || ncu < 1)
+            ncu = 256;
+        return dim3((uint32_t)std::min<uint64_t>(ntile, (uint64_t)per_cu * ncu));
     };
     if (out == OUT_TRACE3 && tv.ld * (f64 ? 8u : 4u) * BLOCK_STEPS >= (1ull << 31))   // one block's rows: one buffer range
         return fail(TMH_E_INVAL, "trace ld %llu too large (a 128-step block of rows must stay under 2 GiB)",
                     (unsigned long long)tv.ld);
-    const size_t lds_exp = stats && stats->hist ? (size_t)((stats->n_bins + 1) / 2) * 4 : 0;   // 16-bit bin pairs
 #define LAUNCH(R, O, S)                                                                                            \
-    hipLaunchKernelGGL((expand_kernel<R, O, S>), exp_grid(exp_wg<R, O, S>()), dim3(exp_wg<R, O, S>()), lds_exp, s, eng->kp, eng->dp, v, chain0, n_chains,      \
-                       step0, n_steps, utc0, pv.tab64, pv.tab32, pv.sun, pv.events, pv.n_events, pv.desc, sg, tv, sv)
+    hipLaunchKernelGGL((expand_kernel<R, O, S>),                                                                   \
+                       exp_grid(exp_wg<R, O, S>(), exp_persistent<R, O, S>(), (const void*)&expand_kernel<R, O, S>), \
+                       dim3(exp_wg<R, O, S>()), lds_exp, s, eng->kp, eng->dp, v, chain0, n_chains, step0, n_steps,   \
+                       utc0, pv.tab64, pv.tab32, pv.sun, pv.events, pv.n_events, pv.desc, sg, tv, sv)
     if (eng->kp.sites) {   // per-chain sites: one instantiation per precision, any output
         if (f64) LAUNCH(double, OUT_ANY, true);
         else LAUNCH(float, OUT_ANY, true);
@@ -3083,6 +3189,16 @@ int tmh_run(struct tmh_engine* eng, void* state, uint64_t chain0, uint32_t n_cha
     return tmh_step(eng, state, chain0, n_chains, step0, n_steps, inj, trace, stats, workspace,
                     (char*)workspace + pb, workspace_bytes - pb, stream);
 }
+
+#ifdef TMH_WALK_PROF
+// diagnostic build only: the walk's per-wave section cycles (see g_walk_prof)
+int tmh_debug_walk_prof(unsigned long long* host, uint32_t waves)
+{
+    if (waves > (uint32_t)WPROF_WAVES) waves = WPROF_WAVES;
+    return hip_check(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_walk_prof), (size_t)waves * (WPROF_N + 2) * 8, 0,
+                                         hipMemcpyDeviceToHost), "walk prof");
+}
+#endif
 
 int tmh_probe(int fn, double a, const double* x, double* out, uint32_t n, void* stream)
 {
