@@ -272,67 +272,29 @@ class BatchedSim:
         _lib.check(self.L.tmh_set_clock(self._eng, C.byref(self.clock.as_struct())))
 
     def _run_pipelined(self, n_steps, win, trace, res, st):
-        """Windows of the time-parallel path, pipelined: the segment walk of window
-        w+1 (tmh_walk_part SEGMENTS, on a high-priority stream) runs beside the
-        expansion of window w (on the current stream, which also builds each
-        window's plan and draws); two plan + scratch buffers.  Same bits as one
-        tmh_run per window (tests/test_gpu_parity.py)."""
+        """Windows of the time-parallel path, pipelined (run_windows): each window's plan,
+        draws and segment walk on a walk stream that runs up to two windows ahead of the
+        expansions on the current stream.  Same bits as one tmh_run per window
+        (tests/test_gpu_parity.py)."""
         torch = _torch()
-        L = self.L
         main = torch.cuda.current_stream(self.device)
         if getattr(self, "_wstream", None) is None:
             self._wstream = torch.cuda.Stream(self.device, priority=torch.cuda.Stream.priority_range()[1])
-        walk = self._wstream
-        mptr, wptr = C.c_void_p(main.cuda_stream), C.c_void_p(walk.cuda_stream)
-        pb = L.tmh_plan_bytes(win)
-        bufs = [self.workspace(win), self.workspace(win)]
-        drawn = [torch.cuda.Event(), torch.cuda.Event()]
-        walked = [torch.cuda.Event(), torch.cuda.Event()]
         wins = []
         done = 0
         while done < n_steps:
             k = min(win, n_steps - done)
             wins.append((self.step + done, k, done))
             done += k
+        bufs = [self.workspace(win) for _ in range(min(WINDOW_BUFFERS, len(wins)))]
 
-        def views(w):
-            b = bufs[w & 1]
-            return C.c_void_p(b.data_ptr()), C.c_void_p(b.data_ptr() + pb), b.numel() - pb
+        def trace_of(w):
+            off, k = wins[w][2], wins[w][1]
+            return _lib.Trace(*(res[f][off:off + k].data_ptr() if f in trace else None
+                                for f in ("csi", "covered", "pv", "meter", "residual")), self.n)
 
-        def prev_of(w):
-            return (views(w - 1)[1], wins[w - 1][1]) if w > 0 else (None, 0)
-
-        def draws(w):      # plan + boundary draws + candidates of window w, on the main stream
-            s0, k, _ = wins[w]
-            plan, scr, nb = views(w)
-            _lib.check(L.tmh_plan(self._eng, s0, k, plan, mptr))
-            ps, pk = prev_of(w)
-            _lib.check(L.tmh_walk_part(self._eng, _ptr(self.state), self.chain0, self.n, s0, k, plan, scr, nb, ps, pk,
-                                       _lib.WALK_DRAWS, mptr))
-            drawn[w & 1].record(main)
-
-        def segments(w):   # the segment walk of window w, on the walk stream
-            s0, k, _ = wins[w]
-            plan, scr, nb = views(w)
-            walk.wait_event(drawn[w & 1])
-            ps, pk = prev_of(w)
-            _lib.check(L.tmh_walk_part(self._eng, _ptr(self.state), self.chain0, self.n, s0, k, plan, scr, nb, ps, pk,
-                                       _lib.WALK_SEGMENTS, wptr))
-            walked[w & 1].record(walk)
-
-        draws(0)
-        segments(0)
-        for w in range(len(wins)):
-            main.wait_event(walked[w & 1])
-            if w + 1 < len(wins):
-                draws(w + 1)       # buffer (w+1) & 1 was last read by expand(w-1), earlier on this stream
-                segments(w + 1)    # beside expand(w)
-            s0, k, off = wins[w]
-            plan, scr, nb = views(w)
-            tr = _lib.Trace(*(res[f][off:off + k].data_ptr() if f in trace else None
-                              for f in ("csi", "covered", "pv", "meter", "residual")), self.n)
-            _lib.check(L.tmh_expand(self._eng, _ptr(self.state), self.chain0, self.n, s0, k, None, C.byref(tr),
-                                    C.byref(st) if st is not None else None, plan, scr, nb, mptr))
+        run_windows(self.L, self._eng, self.state, self.chain0, self.n, [(a, k) for a, k, _ in wins], bufs, main,
+                    self._wstream, trace_of, st)
         self._keep = bufs   # allocated on the main stream, whose last work is the last expansion
 
     def plan(self, step0, n_steps):
@@ -360,6 +322,64 @@ class BatchedSim:
         if self.hist is not None:
             tot["hist"] = self.hist.clone()
         return tot
+
+
+WINDOW_BUFFERS = 3   # plan + scratch sets of the multi-window pipeline (run_windows)
+
+
+def run_windows(L, eng, state, chain0, n, wins, bufs, main, walk, trace_of, st):
+    """Consecutive windows [(step0, n_steps)] of the same chains, software-pipelined over
+    len(bufs) workspace buffers (plan + scratch each, window w in buffer w % K):
+
+      walk stream: plan(w), draws(w) chained to window w-1's walk (tmh_walk_part with
+                   prev_scratch), segment walk(w) -- up to K-1 windows ahead;
+      main stream: expansion + commit of window w once its walk is done.
+
+    The walk of a window needs only the previous window's walk (its end status,
+    cloud-cover and wind pairs, call counts, sigma arrays), never its expansion, so the
+    walks run back to back while the expansions follow; buffer w % K is reused once the
+    expansion of window w - K is done.  With small batches (the walk latency-bound) the
+    per-window tail (fixup, commit, plan, draws) is off the walk's path.  trace_of(w):
+    the window's tmh_trace; st: tmh_stats or None.  Same bits as one tmh_run per window."""
+    import ctypes as C
+    torch = _torch()
+    K = len(bufs)
+    mptr, wptr = C.c_void_p(main.cuda_stream), C.c_void_p(walk.cuda_stream)
+    nb = bufs[0].numel()
+    pbytes = [L.tmh_plan_bytes(int(max(k for _, k in wins)))] * K
+    walked = [torch.cuda.Event() for _ in range(K)]
+    expanded = [torch.cuda.Event() for _ in range(K)]
+
+    def views(w):
+        b = bufs[w % K]
+        return C.c_void_p(b.data_ptr()), C.c_void_p(b.data_ptr() + pbytes[w % K]), nb - pbytes[w % K]
+
+    def prev_of(w):
+        return (views(w - 1)[1], wins[w - 1][1]) if w > 0 else (None, 0)
+
+    def issue_walk(w):   # plan, draws and segment walk of window w, on the walk stream
+        s0, k = wins[w]
+        plan, scr, sb = views(w)
+        if w >= K:
+            walk.wait_event(expanded[w % K])   # the expansion of window w - K has read this buffer
+        _lib.check(L.tmh_plan(eng, s0, k, plan, wptr))
+        ps, pk = prev_of(w)
+        _lib.check(L.tmh_walk_part(eng, _ptr(state), chain0, n, s0, k, plan, scr, sb, ps, pk,
+                                   _lib.WALK_DRAWS | _lib.WALK_SEGMENTS, wptr))
+        walked[w % K].record(walk)
+
+    for w in range(min(K - 1, len(wins))):
+        issue_walk(w)
+    for w in range(len(wins)):
+        if w + K - 1 < len(wins):
+            issue_walk(w + K - 1)
+        s0, k = wins[w]
+        plan, scr, sb = views(w)
+        main.wait_event(walked[w % K])
+        tr = trace_of(w)
+        _lib.check(L.tmh_expand(eng, _ptr(state), chain0, n, s0, k, None, C.byref(tr) if tr is not None else None,
+                                C.byref(st) if st is not None else None, plan, scr, sb, mptr))
+        expanded[w % K].record(main)
 
 
 def torch_uint8():

@@ -20,6 +20,7 @@ import ctypes as C
 from dataclasses import dataclass
 
 from . import _lib
+from .engine import WINDOW_BUFFERS, run_windows
 
 
 @dataclass
@@ -133,11 +134,12 @@ class BatchPipeline:
                     self.work = torch.empty_like(self.state)
                     self.ids = torch.empty(n, dtype=torch.int32, device=device)
                     self.nlive = torch.zeros(1, dtype=torch.int32, device=device)
-                if nwin > 1:   # second plan + scratch: window w+1's walk beside window w's expansion
-                    self.plan2 = torch.empty_like(self.plan)
-                    self.scratch2 = torch.empty_like(self.scratch)
-                    self.wev = [torch.cuda.Event(), torch.cuda.Event()]
-                    self.eev = [torch.cuda.Event(), torch.cuda.Event()]
+                if nwin > 1 and not (cfg.compact and cfg.mode == "stats"):
+                    # plan + scratch sets of the multi-window pipeline (engine.run_windows): the
+                    # walks of the next windows run ahead of this window's expansion
+                    wb = L.tmh_plan_bytes(win) + L.tmh_engine_scratch_bytes(sim._eng, n, win)
+                    self.wbufs = [torch.empty(wb, dtype=torch.uint8, device=device)
+                                  for _ in range(min(WINDOW_BUFFERS, nwin))]
                 self.trace = {f: torch.empty(win, n, dtype=sim.real, device=device) for f in ("pv", "meter", "residual")} \
                     if cfg.mode == "trace" else {}
                 self.tr = _lib.Trace(None, None, *(self.trace[f].data_ptr() if f in self.trace else None
@@ -228,43 +230,10 @@ class BatchPipeline:
                                                 self._p(cx.nlive), nl, 1, cx.sptr))
                 _lib.check(L.tmh_set_chain_ids(sim._eng, None, 0))
             return
-        # multi-window: the segment walk of window w+1 beside the expansion of window w;
-        # plans and draws on the expansion's stream (as BatchedSim.run)
-        bufs = [(cx.plan, cx.scratch), (cx.plan2, cx.scratch2)]
+        # multi-window: each window's plan, draws and walk on the context's walk stream,
+        # up to two windows ahead of the expansions on its stream (engine.run_windows)
         wins = [(s0, min(win, secs - s0)) for s0 in range(0, secs, win)]
-        sp = self._p(cx.state)
-
-        def views(w):
-            return tuple(self._p(t) for t in bufs[w & 1])
-
-        def prev_of(w):
-            return (views(w - 1)[1], wins[w - 1][1]) if w > 0 else (None, 0)
-
-        def draws(w):
-            pl, sc = views(w)
-            _lib.check(L.tmh_plan(sim._eng, wins[w][0], wins[w][1], pl, cx.sptr))
-            _lib.check(L.tmh_walk_part(sim._eng, sp, chain0, n, wins[w][0], wins[w][1], pl, sc, cx.scratch.numel(),
-                                       *prev_of(w), _lib.WALK_DRAWS, cx.sptr))
-            cx.wev[w & 1].record(cx.stream)
-
-        def segments(w):
-            pl, sc = views(w)
-            cx.wstream.wait_event(cx.wev[w & 1])
-            _lib.check(L.tmh_walk_part(sim._eng, sp, chain0, n, wins[w][0], wins[w][1], pl, sc, cx.scratch.numel(),
-                                       *prev_of(w), _lib.WALK_SEGMENTS, cx.wptr))
-            cx.eev[w & 1].record(cx.wstream)
-
-        draws(0)
-        segments(0)
-        for w in range(len(wins)):
-            cx.stream.wait_event(cx.eev[w & 1])
-            if w + 1 < len(wins):
-                draws(w + 1)
-                segments(w + 1)
-            pl, sc = views(w)
-            _lib.check(L.tmh_expand(sim._eng, sp, chain0, n, wins[w][0], wins[w][1], None,
-                                    C.byref(cx.tr), C.byref(cx.st) if cx.st is not None else None, pl, sc,
-                                    cx.scratch.numel(), cx.sptr))
+        run_windows(L, sim._eng, cx.state, chain0, n, wins, cx.wbufs, cx.stream, cx.wstream, lambda w: cx.tr, cx.st)
 
     # ------------------------------------------------------------------ round 1's staggered schedule
     def _build(self, k):      # construction of batch k's chains, its plan and draws
