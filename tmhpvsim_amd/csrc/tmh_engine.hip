@@ -1200,14 +1200,18 @@ __device__ __forceinline__ double mov_dpp_f64(double v)
 }
 
 // min over the G lanes of each group: quad_perm [1,0,3,2], [2,3,0,1], then
-// row_half_mirror (G >= 8: the other quad of the half row), row_mirror (G = 16)
+// row_half_mirror (G >= 8: the other quad of the half row), row_mirror (G = 16).
+// The scan's distances are never NaN (+inf or |tot - 3600| of a finite total), so a
+// compare and a select are the minimum; fmin would first canonicalise both operands
+// (two more fp64 ops per step on the walk's latency chain).
 template <int G>
 __device__ __forceinline__ double grp_min_f64(double v)
 {
-    v = fmin(v, mov_dpp_f64<0xB1>(v));
-    v = fmin(v, mov_dpp_f64<0x4E>(v));
-    if constexpr (G >= 8) v = fmin(v, mov_dpp_f64<0x141>(v));
-    if constexpr (G >= 16) v = fmin(v, mov_dpp_f64<0x140>(v));
+    auto mn = [](double a, double b) { return b < a ? b : a; };
+    v = mn(v, mov_dpp_f64<0xB1>(v));
+    v = mn(v, mov_dpp_f64<0x4E>(v));
+    if constexpr (G >= 8) v = mn(v, mov_dpp_f64<0x141>(v));
+    if constexpr (G >= 16) v = mn(v, mov_dpp_f64<0x140>(v));
     return v;
 }
 
