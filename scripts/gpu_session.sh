@@ -20,6 +20,9 @@ step smoke 300 python __graft_entry__.py smoke
 step pytest 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider -rf --durations=25 --timeout 400 \
     --timeout-method thread ${K:+-k "$K"}
 step bench 480 python bench.py --steps 20 --warmup 5
+case "$D" in *counters*)
+  (cd /tmp && timeout -k 10 120 rocprofv3 --list-avail > "$OLDPWD/gpurun_out/counters_$TAG.txt" 2>&1; echo "counters rc=$?") ;;
+esac
 case "$D" in *walkprof*)
   step walkprof 240 env TMHPVSIM_LIB=$PWD/tmhpvsim_amd/libtmh_wprof.so python scripts/walk_prof.py --chains 4096 2048 ;;
 esac
