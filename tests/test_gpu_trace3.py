@@ -227,3 +227,33 @@ def test_c4_shape_pipeline_equals_batches():
         torch.cuda.synchronize()
         assert torch.equal(cx.hist, s.hist), ci
         assert _same(cx.acc, s.chain_acc), ci
+
+
+def test_c5_shape_compacted_group_equals_batches():
+    """bench.py's C5 schedule (pipeline_defaults("c5"): markov cc with per-site tables and
+    sites, day windows compacted to the live chains) with three batches advanced window by
+    window together (BatchPipeline.compact_batches: one host read of the live counts per
+    window for the group, per-context chain ids set around each context's launches) ==
+    BatchedSim.run(compact=True) of each batch alone: statistics and histogram bit for bit."""
+    from tmhpvsim_amd.engine import BatchedSim
+    from tmhpvsim_amd.params import CC_MARKOV, site_grid, site_shape_tables
+    from tmhpvsim_amd.pipeline import BatchPipeline, pipeline_defaults
+    n, secs, start = 512, 3 * 86400, "2019-09-05 00:00:00"
+    mp = ModelParams(cc_mode=CC_MARKOV)
+    kw = dict(shape_tables=site_shape_tables(n), sites=site_grid(32, 16))
+    cfg = pipeline_defaults("c5", seconds=secs)
+    assert cfg.compact and cfg.window == 86400
+    sim = BatchedSim(n, start, tz=TZ, params=mp, device="cuda:0", horizon=secs, **kw)
+    pipe = BatchPipeline(sim, n, secs, cfg, lambda k: 7_000_000 + k * n, torch.device("cuda:0"))
+    pipe.run(0, len(pipe.ctxs))
+    pipe.sync()
+    faulted = 0
+    for ci, cx in enumerate(pipe.ctxs):
+        s = BatchedSim(n, start, tz=TZ, params=mp, device="cuda:0", horizon=secs, chain0=7_000_000 + ci * n, **kw)
+        s.enable_stats()
+        s.run(secs, trace=(), window=86400, compact=True)
+        torch.cuda.synchronize()
+        faulted += int((s.status() != 0).sum())
+        assert torch.equal(cx.hist, s.hist), ci
+        assert _same(cx.acc, s.chain_acc), ci
+    assert faulted > n // 4, "the test needs chains that fault (markov AssertionError)"

@@ -206,34 +206,56 @@ class BatchPipeline:
                                       self._p(cx.plan), self._p(cx.scratch), cx.scratch.numel(), cx.sptr))
             return
         if cfg.compact and cfg.mode == "stats":   # windows in order, the live chains of each only
-            sp = self._p(cx.state)
-            for s0 in range(0, secs, win):
-                w = min(win, secs - s0)
-                nl, cur = n, cx.state
-                if s0 > 0:
-                    _lib.check(L.tmh_live_chains(sim._eng, sp, n, None, self._p(cx.ids), self._p(cx.nlive), cx.sptr))
-                    cx.stream.synchronize()                # n_live was written on the batch's stream
-                    nl = int(cx.nlive.item())
+            self.compact_batches([k], init=False)
+            return
+        # multi-window: each window's plan, draws and walk on the context's walk stream,
+        # up to two windows ahead of the expansions on its stream (engine.run_windows)
+        wins = [(s0, min(win, secs - s0)) for s0 in range(0, secs, win)]
+        run_windows(L, sim._eng, cx.state, chain0, n, wins, cx.wbufs, cx.stream, cx.wstream, lambda w: cx.tr, cx.st)
+
+    def compact_batches(self, ks, init=True):
+        """Compacted multi-window statistics batches (C5), one per context, advanced window
+        by window together: every window after the first runs on the chains still live
+        (tmh_live_chains -> one host read of the counts per window for the whole group ->
+        tmh_state_move gather, tmh_set_chain_ids, tmh_plan + tmh_step, scatter).  The
+        chain ids are engine state read at each launch, so the contexts' launches are
+        issued one context at a time while their streams run concurrently."""
+        L, sim, n, secs, win = self.L, self.sim, self.n, self.secs, self.win
+        cxs = [self.ctx_of(k) for k in ks]
+        assert len({id(c) for c in cxs}) == len(cxs), "one batch per context"
+        if init:
+            for k, cx in zip(ks, cxs):
+                cx.chain0 = self.chain0_of(k)
+                _lib.check(L.tmh_init(sim._eng, self._p(cx.state), cx.chain0, n, None, cx.sptr))
+        for s0 in range(0, secs, win):
+            w = min(win, secs - s0)
+            nls = [n] * len(cxs)
+            if s0 > 0:
+                for cx in cxs:
+                    _lib.check(L.tmh_live_chains(sim._eng, self._p(cx.state), n, None, self._p(cx.ids),
+                                                 self._p(cx.nlive), cx.sptr))
+                for i, cx in enumerate(cxs):
+                    cx.stream.synchronize()            # n_live was written on the batch's stream
+                    nls[i] = int(cx.nlive.item())
+            for nl, cx in zip(nls, cxs):
+                sp, cur = self._p(cx.state), cx.state
+                try:
                     if nl < n:
                         cur = cx.work
                         if nl:
                             _lib.check(L.tmh_state_move(sim._eng, sp, n, self._p(cx.work), nl, self._p(cx.ids),
                                                         self._p(cx.nlive), nl, 0, cx.sptr))
                             _lib.check(L.tmh_set_chain_ids(sim._eng, self._p(cx.ids), n))
-                if nl:
-                    _lib.check(L.tmh_plan(sim._eng, s0, w, self._p(cx.plan), cx.sptr))
-                    _lib.check(L.tmh_step(sim._eng, self._p(cur), chain0, nl, s0, w, None, C.byref(cx.tr),
-                                          C.byref(cx.st), self._p(cx.plan), self._p(cx.scratch),
-                                          cx.scratch.numel(), cx.sptr))
-                if nl and cur is cx.work:
-                    _lib.check(L.tmh_state_move(sim._eng, self._p(cx.work), nl, sp, n, self._p(cx.ids),
-                                                self._p(cx.nlive), nl, 1, cx.sptr))
-                _lib.check(L.tmh_set_chain_ids(sim._eng, None, 0))
-            return
-        # multi-window: each window's plan, draws and walk on the context's walk stream,
-        # up to two windows ahead of the expansions on its stream (engine.run_windows)
-        wins = [(s0, min(win, secs - s0)) for s0 in range(0, secs, win)]
-        run_windows(L, sim._eng, cx.state, chain0, n, wins, cx.wbufs, cx.stream, cx.wstream, lambda w: cx.tr, cx.st)
+                    if nl:
+                        _lib.check(L.tmh_plan(sim._eng, s0, w, self._p(cx.plan), cx.sptr))
+                        _lib.check(L.tmh_step(sim._eng, self._p(cur), cx.chain0, nl, s0, w, None, C.byref(cx.tr),
+                                              C.byref(cx.st), self._p(cx.plan), self._p(cx.scratch),
+                                              cx.scratch.numel(), cx.sptr))
+                    if nl and cur is cx.work:
+                        _lib.check(L.tmh_state_move(sim._eng, self._p(cx.work), nl, sp, n, self._p(cx.ids),
+                                                    self._p(cx.nlive), nl, 1, cx.sptr))
+                finally:
+                    _lib.check(L.tmh_set_chain_ids(sim._eng, None, 0))
 
     # ------------------------------------------------------------------ round 1's staggered schedule
     def _build(self, k):      # construction of batch k's chains, its plan and draws
@@ -365,6 +387,11 @@ class BatchPipeline:
         overlap the expansion instead of running in lockstep with it.  The caller
         synchronises (the outputs of batch k sit in context k % pipeline)."""
         cfg = self.cfg
+        if self.nwin > 1 and cfg.compact and cfg.mode == "stats" and self.sim.path == "time_parallel":
+            P = len(self.ctxs)   # compacted windows: one group of batches (one per context) at a time
+            for g in range(k0, k0 + cnt, P):
+                self.compact_batches(list(range(g, min(g + P, k0 + cnt))))
+            return
         if self.nwin > 1 or not cfg.stagger:
             for k in range(k0, k0 + cnt):
                 self.one_step(k)
