@@ -1546,18 +1546,17 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
         }
         const double x0 = cbuf[rel - kb];
         WPROF(1);
-        // ---- next_cloud: tries (cloud_cover_binary.py:82-98)
+        // ---- next_cloud: tries (cloud_cover_binary.py:82-98).  Try 0 (its length from the
+        // candidate table) is straight-line code; the retries (8 % of the calls: tries 1..39,
+        // reset_sigma before try 20, the AssertionError after try 39) loop only for the groups
+        // whose try 0 found no possible entry.
         int tries = 0, last = -1;
-        double ncl = 0.0, bdl = 0.0;
-        for (;;) {
-            double x;
-            if (tries == 0 && x0 >= 0.0) x = x0;
-            else x = pow_d(dp.alpha + dp.delta * keyed_u(dp.seed, chain0 + gid(dp.ids, c), ncall, TAG_CLOUD, (uint32_t)(tries >> 1),
-                                                        tries & 1),
-                           dp.expo);
+        double ncl = 0.0, bdl = 0.0, bd = INFINITY;
+        int bk = INT_MAX;
+        auto attempt = [&](double x) __attribute__((always_inline)) {   // one try: scan + group minimum
             ncl = x / ws;
-            double bd = INFINITY;
-            int bk = INT_MAX;
+            bd = INFINITY;
+            bk = INT_MAX;
             auto scan = [&](int k, double sc, double sl) {   // :83-88, branch-free
                 const double nsc = ncl + sc;
                 const double nsl = f * nsc;
@@ -1579,23 +1578,32 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
                 const int k = k0 + p;
                 if (k < L) scan(k, gsc[k], gsl[k]);
             }
-            const double dmin = grp_min_f64<G>(bd);
-            if (dmin < INFINITY) {
-                last = grp_min_i32<G>(bd == dmin ? bk : INT_MAX);
-                break;
-            }
-            ++tries;
-            if (tries == 20) {   // reset_sigma (cloud_cover_binary.py:76-78); 300 (k+1) is exact
-                const int nl = (int)(h * 12);
+            return grp_min_f64<G>(bd);
+        };
+        auto draw = [&](int t) {   // try t's cloud length, keyed by (chain, call number, try)
+            return pow_d(dp.alpha + dp.delta * keyed_u(dp.seed, chain0 + gid(dp.ids, c), ncall, TAG_CLOUD,
+                                                       (uint32_t)(t >> 1), t & 1),
+                         dp.expo);
+        };
+        double dmin = attempt(x0 >= 0.0 ? x0 : draw(0));
+        if (!(dmin < INFINITY)) {   // group-uniform
+            for (;;) {
+                ++tries;
+                if (tries == 20) {   // reset_sigma (cloud_cover_binary.py:76-78); 300 (k+1) is exact
+                    const int nl = (int)(h * 12);
 #pragma unroll
-                for (int ch = 0; ch * G < 12; ++ch) {
-                    vc[ch] = 300.0 * (ch * G + p + 1);
-                    vl[ch] = f * vc[ch];
+                    for (int ch = 0; ch * G < 12; ++ch) {
+                        vc[ch] = 300.0 * (ch * G + p + 1);
+                        vl[ch] = f * vc[ch];
+                    }
+                    L = nl;
                 }
-                L = nl;
+                if (tries == 40) break;
+                dmin = attempt(draw(tries));
+                if (dmin < INFINITY) break;
             }
-            if (tries == 40) break;
         }
+        if (dmin < INFINITY) last = grp_min_i32<G>(bd == dmin ? bk : INT_MAX);
         ++ncall;
         WPROF(2);
         if (last < 0) {   // assert not recurse (:91)
