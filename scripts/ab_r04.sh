@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round-4 A/B runs on one box (each a bench line; one rep unless REPS is set):
+#   c5 with the current library vs the 3-waves-per-SIMD C5 expansion (libtmh_c5w3.so);
+#   the C4 one-GPU proxies at N = 8 with day windows vs 7-day windows.
+set -u
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TAG="${1:-ab}"
+run() {   # run NAME LIB ARGS...
+  local name=$1 lib=$2; shift 2
+  local l=$PWD/tmhpvsim_amd/libtmhpvsim.so; [ "$lib" = cur ] || l=$PWD/tmhpvsim_amd/libtmh_$lib.so
+  TMHPVSIM_LIB=$l timeout -k 10 300 python bench.py --no-cpu-baseline --secondary none "$@" \
+      > gpurun_out/ab_${TAG}_$name.json 2> gpurun_out/ab_${TAG}_$name.err || { echo "$name failed rc=$?"; tail -3 gpurun_out/ab_${TAG}_$name.err; exit 1; }
+  python3 -c "
+import json; d=json.loads(open('gpurun_out/ab_${TAG}_$name.json').read().strip().splitlines()[-1]); r=d['roofline']
+print('$name', 'value %.4g ms/step %.2f kernel %.3f alone %s' % (d['value'], d['ms_per_step'], r.get('kernel_ms') or 0, (r.get('alone') or {}).get('kernel_ms')), d.get('projected_node_value'))"
+}
+for rep in $(seq 1 ${REPS:-1}); do
+  run c5_cur cur --workload c5 --steps 2 --warmup 1
+  run c5_w3 c5w3 --workload c5 --steps 2 --warmup 1
+  run c4p8_d1 cur --workload c4 --proxy-world 8 --steps 4 --warmup 1
+  run c4p8_d7 cur --workload c4 --proxy-world 8 --steps 4 --warmup 1 --window 604800
+done
