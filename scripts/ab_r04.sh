@@ -19,6 +19,8 @@ print('$name', 'value %.4g ms/step %.2f kernel %.3f alone %s' % (d['value'], d['
 for rep in $(seq 1 ${REPS:-1}); do
   run c5_cur cur --workload c5 --steps 2 --warmup 1
   run c5_w3 c5w3 --workload c5 --steps 2 --warmup 1
+  run c5_loop c5loop --workload c5 --steps 2 --warmup 1
+  run c5_loopw3 c5loopw3 --workload c5 --steps 2 --warmup 1
   run c4p8_d1 cur --workload c4 --proxy-world 8 --steps 4 --warmup 1
   run c4p8_d7 cur --workload c4 --proxy-world 8 --steps 4 --warmup 1 --window 604800
 done
