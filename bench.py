@@ -217,7 +217,10 @@ def parse():
     a.seconds = a.seconds or {"c2": 86400, "c3": 86400, "c4": 365 * 86400, "c5": 604800}[a.workload]
     # the schedule (contexts, walks in flight, construction ahead, streams): the measured-best
     # defaults of each workload, shared with the tests that run the timed schedule
-    a.cfg = pipeline_defaults(a.workload, a.precision, seconds=a.seconds, window=a.window, walks=a.walks,
+    # the chains of one batch on one GPU: C2 per GPU; C3 / C4 / C5 the node total / N (the proxy's N)
+    a.chains = a.chains or DEFAULT_CHAINS[a.workload]
+    per_gpu = a.chains if a.workload not in STRONG else -(-a.chains // (a.gpus * max(1, a.proxy_world)))
+    a.cfg = pipeline_defaults(a.workload, a.precision, chains=per_gpu, seconds=a.seconds, window=a.window, walks=a.walks,
                               build_ahead=a.build_ahead, pipeline=a.pipeline, compact=a.compact, mode=a.mode,
                               stagger=a.stagger, schedule=a.schedule, build_on=a.build_on,
                               walk_priority=a.walk_priority, expand_priority=a.expand_priority,

@@ -280,6 +280,7 @@ class BatchedSim:
         main = torch.cuda.current_stream(self.device)
         if getattr(self, "_wstream", None) is None:
             self._wstream = torch.cuda.Stream(self.device, priority=torch.cuda.Stream.priority_range()[1])
+            self._pstream = torch.cuda.Stream(self.device)
         wins = []
         done = 0
         while done < n_steps:
@@ -294,7 +295,7 @@ class BatchedSim:
                                 for f in ("csi", "covered", "pv", "meter", "residual")), self.n)
 
         run_windows(self.L, self._eng, self.state, self.chain0, self.n, [(a, k) for a, k, _ in wins], bufs, main,
-                    self._wstream, trace_of, st)
+                    self._wstream, trace_of, st, plan_stream=self._pstream)
         self._keep = bufs   # allocated on the main stream, whose last work is the last expansion
 
     def plan(self, step0, n_steps):
@@ -327,11 +328,13 @@ class BatchedSim:
 WINDOW_BUFFERS = 3   # plan + scratch sets of the multi-window pipeline (run_windows)
 
 
-def run_windows(L, eng, state, chain0, n, wins, bufs, main, walk, trace_of, st):
+def run_windows(L, eng, state, chain0, n, wins, bufs, main, walk, trace_of, st, plan_stream=None):
     """Consecutive windows [(step0, n_steps)] of the same chains, software-pipelined over
     len(bufs) workspace buffers (plan + scratch each, window w in buffer w % K):
 
-      walk stream: plan(w), draws(w) chained to window w-1's walk (tmh_walk_part with
+      plan stream: plan(w) (chain-independent: clock and geometry rows) as soon as buffer
+                   w % K is free;
+      walk stream: draws(w) chained to window w-1's walk (tmh_walk_part with
                    prev_scratch), segment walk(w) -- up to K-1 windows ahead;
       main stream: expansion + commit of window w once its walk is done.
 
@@ -344,11 +347,13 @@ def run_windows(L, eng, state, chain0, n, wins, bufs, main, walk, trace_of, st):
     import ctypes as C
     torch = _torch()
     K = len(bufs)
-    mptr, wptr = C.c_void_p(main.cuda_stream), C.c_void_p(walk.cuda_stream)
+    pst = plan_stream or walk
+    mptr, wptr, pptr = C.c_void_p(main.cuda_stream), C.c_void_p(walk.cuda_stream), C.c_void_p(pst.cuda_stream)
     nb = bufs[0].numel()
     pbytes = [L.tmh_plan_bytes(int(max(k for _, k in wins)))] * K
     walked = [torch.cuda.Event() for _ in range(K)]
     expanded = [torch.cuda.Event() for _ in range(K)]
+    planned = [torch.cuda.Event() for _ in range(K)]
 
     def views(w):
         b = bufs[w % K]
@@ -361,8 +366,13 @@ def run_windows(L, eng, state, chain0, n, wins, bufs, main, walk, trace_of, st):
         s0, k = wins[w]
         plan, scr, sb = views(w)
         if w >= K:
-            walk.wait_event(expanded[w % K])   # the expansion of window w - K has read this buffer
-        _lib.check(L.tmh_plan(eng, s0, k, plan, wptr))
+            pst.wait_event(expanded[w % K])    # the expansion of window w - K has read this buffer
+            if pst is not walk:
+                walk.wait_event(expanded[w % K])
+        _lib.check(L.tmh_plan(eng, s0, k, plan, pptr))
+        if pst is not walk:
+            planned[w % K].record(pst)
+            walk.wait_event(planned[w % K])
         ps, pk = prev_of(w)
         _lib.check(L.tmh_walk_part(eng, _ptr(state), chain0, n, s0, k, plan, scr, sb, ps, pk,
                                    _lib.WALK_DRAWS | _lib.WALK_SEGMENTS, wptr))

@@ -50,10 +50,14 @@ class PipelineConfig:
 
 
 def pipeline_defaults(workload, precision="fp32", seconds=None, window=None, walks=None, build_ahead=None,
-                      pipeline=None, compact=None, mode=None, **overrides):
+                      pipeline=None, compact=None, mode=None, chains=None, **overrides):
     """The measured-best schedule of each BASELINE.json workload (DESIGN.md "The C2
     pipeline", "C3, C4, C5"): bench.py's defaults, shared with the tests that check
-    the timed schedule."""
+    the timed schedule.  chains: the chains of one batch on this GPU (a rank's shard of
+    a strong-scaled workload); C4 / C5 shards smaller than the one-GPU batch keep more
+    batches in flight (their day windows are walk-latency-bound at small batches, so the
+    GPU has room for several: as many contexts as keep ~3 one-GPU batches' chains in
+    flight, at most 8)."""
     c5, c4 = workload == "c5", workload == "c4"
     secs = seconds or {"c2": 86400, "c3": 86400, "c4": 365 * 86400, "c5": 604800}[workload]
     mode = mode or ("trace" if workload == "c2" else "stats")
@@ -63,7 +67,11 @@ def pipeline_defaults(workload, precision="fp32", seconds=None, window=None, wal
     # 1.41-1.44 ms per C2 batch at 4, 5 or 6 ahead against 1.48-1.55 at 3, 1.86-1.90 at 2)
     build_ahead = build_ahead or max(1, walks) + (2 if walks > 1 else 1)
     # c3: two 1 M-chain batches in flight (2 x ~27 GB of state + scratch): +3 % over one (r02)
-    pipeline = pipeline or (2 if workload == "c3" else build_ahead + 1)
+    if not pipeline:
+        pipeline = 2 if workload == "c3" else build_ahead + 1
+        if (c4 or c5) and chains:
+            full = 16384 if c4 else 65536
+            pipeline = max(pipeline, min(8, -(-3 * full // int(chains))))
     cfg = PipelineConfig(
         mode=mode,
         window=min(window or (86400 if (c5 or c4) else secs), secs),
@@ -211,7 +219,10 @@ class BatchPipeline:
         # multi-window: each window's plan, draws and walk on the context's walk stream,
         # up to two windows ahead of the expansions on its stream (engine.run_windows)
         wins = [(s0, min(win, secs - s0)) for s0 in range(0, secs, win)]
-        run_windows(L, sim._eng, cx.state, chain0, n, wins, cx.wbufs, cx.stream, cx.wstream, lambda w: cx.tr, cx.st)
+        if getattr(cx, "pstream", None) is None:
+            cx.pstream = self.torch.cuda.Stream(self.dev)
+        run_windows(L, sim._eng, cx.state, chain0, n, wins, cx.wbufs, cx.stream, cx.wstream, lambda w: cx.tr, cx.st,
+                    plan_stream=cx.pstream)
 
     def compact_batches(self, ks, init=True):
         """Compacted multi-window statistics batches (C5), one per context, advanced window
