@@ -246,15 +246,17 @@ def parse():
 SECONDARY = {   # --secondary: the other BASELINE.json configs, each in a child process of its own
     "c2_fp64": ["--precision", "fp64", "--steps", "10", "--warmup", "3"],
     "c3": ["--workload", "c3", "--steps", "4", "--warmup", "1"],
-    "c4": ["--workload", "c4", "--steps", "2", "--warmup", "1"],
-    "c5": ["--workload", "c5", "--steps", "2", "--warmup", "1"],
+    # C4 / C5 at N = 1 keep 3 batches in flight: whole rounds of them (6 / 3 timed batches)
+    "c4": ["--workload", "c4", "--steps", "6", "--warmup", "1"],
+    "c5": ["--workload", "c5", "--steps", "3", "--warmup", "1"],
     # one-GPU proxies of the strong-scaled configurations at N = 8 (and C4 at 2, 4): rank 0's
-    # shard timed alone; `projected_efficiency` = N x its rate / the N = 1 rate above
+    # shard timed alone (8 batches in flight for C4 / C5 shards, pipeline_defaults);
+    # `projected_efficiency` = N x its rate / the N = 1 rate above
     "c3_proxy8": ["--workload", "c3", "--proxy-world", "8", "--steps", "6", "--warmup", "2"],
-    "c4_proxy2": ["--workload", "c4", "--proxy-world", "2", "--steps", "4", "--warmup", "1"],
-    "c4_proxy4": ["--workload", "c4", "--proxy-world", "4", "--steps", "4", "--warmup", "1"],
-    "c4_proxy8": ["--workload", "c4", "--proxy-world", "8", "--steps", "4", "--warmup", "1"],
-    "c5_proxy8": ["--workload", "c5", "--proxy-world", "8", "--steps", "4", "--warmup", "1"],
+    "c4_proxy2": ["--workload", "c4", "--proxy-world", "2", "--steps", "6", "--warmup", "1"],
+    "c4_proxy4": ["--workload", "c4", "--proxy-world", "4", "--steps", "8", "--warmup", "1"],
+    "c4_proxy8": ["--workload", "c4", "--proxy-world", "8", "--steps", "8", "--warmup", "1"],
+    "c5_proxy8": ["--workload", "c5", "--proxy-world", "8", "--steps", "8", "--warmup", "1"],
 }
 
 
