@@ -81,7 +81,7 @@ struct SegView {                   // P1 -> P2 scratch
     uint32_t* pool_n;              // chunks handed out (zeroed by the draws phase)
     uint32_t* walk_q;              // the walk's chain queue: chains taken past the first `rows` (zeroed likewise)
     uint32_t* pool_short;          // some chain found the pool exhausted (zeroed likewise)
-    uint32_t* order;               // [n] walk row -> chain (windiest first, walk_order_kernel); NULL: row r is chain r
+    uint32_t* order;               // [n] walk row -> chain (windiest first, walk_order_kernel; the identity without walk order)
     uint32_t* rank;                // [n] chain -> walk row (the inverse; cand is stored by row)
     int32_t* ovf_first;            // [n] window-relative step of the chain's record `cap` (INT_MAX: none)
     uint32_t* count;               // [n]
@@ -509,10 +509,15 @@ __global__ __launch_bounds__(256) void desc_kernel(int64_t step0, uint32_t n, in
 // _next_day / _next_hour draws of every (event, chain): clearskyindexmodel.py:101-107
 __global__ __launch_bounds__(256) void event_draws_kernel(DrawParams dp, uint64_t chain0, uint32_t n, uint32_t nsteps,
                                                           const int2* __restrict__ events,
-                                                          const uint32_t* __restrict__ n_events, double* evd)
+                                                          const uint32_t* __restrict__ n_events, double* evd,
+                                                          uint32_t* identity_order, uint32_t* identity_rank)
 {
     const uint32_t c = blockIdx.y * blockDim.x + threadIdx.x;
     const uint32_t e = blockIdx.x;
+    if (identity_order && e == 0 && c < n) {   // walk rows in chain order (tmh_set_walk_order off)
+        identity_order[c] = c;
+        identity_rank[c] = c;
+    }
     if (c >= n || e >= min(*n_events, ev_cap_dev(nsteps))) return;
     const uint64_t chain = chain0 + gid(dp.ids, c), step = (uint64_t)events[e].x;
     const int fl = events[e].y;
@@ -3013,18 +3018,18 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     const int64_t utc0 = eng->gp.clock.utc0;
     hipEvent_t t_step = phases == PH_ALL ? eng->mark(s) : nullptr;
     if (phases & PH_DRAWS) {
+        // the walk rows' order, read by the candidate table's layout and by the walk: computed
+        // here (tmh_set_walk_order before a window's draws), so the walk uses the order its
+        // window's draws were made with whatever the engine's flag says when it runs
         hipLaunchKernelGGL(event_draws_kernel, dim3(sg.evcap, cb), dim3(256), 0, s, eng->dp, chain0, n_chains, n_steps,
-                           pv.events, pv.n_events, sg.evd);
+                           pv.events, pv.n_events, sg.evd, eng->walk_order ? nullptr : sg.order,
+                           eng->walk_order ? nullptr : sg.rank);
         if (eng->dp.markov)
             hipLaunchKernelGGL(markov_cc_kernel, dim3(cb), dim3(256), 0, s, eng->kp, v, chain0, n_chains, n_steps,
                                pv.events, pv.n_events, sg.evd, prev);
-        // the walk rows' order (read by the candidates table's layout and the walk): set
-        // tmh_set_walk_order before a window's draws
         if (eng->walk_order)
             hipLaunchKernelGGL(walk_order_kernel, dim3((n_chains + ORDER_TILE - 1) / ORDER_TILE), dim3(1024), 0, s, v,
                                n_chains, sg, prev);
-        else
-            sg.order = sg.rank = nullptr;
         hipEvent_t t_cand = eng->mark(s);
         {   // candidates + the window's minute draws (+ counter resets), one launch
             const int64_t fmh = first_minute_host(utc0, step0);
@@ -3052,7 +3057,6 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
 #define WALK(Q, GG)                                                                                           \
     hipLaunchKernelGGL((segments_kernel<Q, GG>), wg, wt, wlds, s, eng->dp, v, chain0, n_chains, step0, n_steps, \
                        eng->gp.clock, pv.events, pv.n_events, sg, prev)
-    if (!eng->walk_order) sg.order = sg.rank = nullptr;   // (the draws phase wrote order / rank)
     const bool q = rows < n_chains;   // groups take queued chains
     if (G == 4) { if (q) WALK(true, 4); else WALK(false, 4); }
     else if (G == 8) { if (q) WALK(true, 8); else WALK(false, 8); }

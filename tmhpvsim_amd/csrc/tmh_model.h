@@ -1188,9 +1188,9 @@ constexpr float KT_GUARD = 4e-6f, PDC_GUARD = 1e-4f;
 __device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float csi, bool discok, bool& risky)
 {
     // min(csi, csimax) as a median with -inf: no canonicalising max of the row's value first.
-    // (v_med3_f32 on a NaN csi returns min(-inf, csimax) = -inf, where fminf gave csimax; a
-    // NaN csi occurs only on lanes whose outputs are masked (faulted chains, lanes past the
-    // last chain): the csi of a live second is interp(...) * (1 + noise) of finite pairs.)
+    // On a NaN csi it returns csimax, as fminf did (tmh_probe fn 10, test_probe_math); a NaN
+    // csi occurs only on lanes whose outputs are masked anyway (faulted chains, lanes past the
+    // last chain).
     const float c = __builtin_amdgcn_fmed3f(csi, -INFINITY, g[G_CSIMAX]);
     const float ghi = c * g[G_GHICS];
     const float kt = fminf(fmaxf(ghi * g[G_I0H], 0.0f), 1.0f);
