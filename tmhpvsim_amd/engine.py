@@ -378,6 +378,13 @@ def run_windows(L, eng, state, chain0, n, wins, bufs, main, walk, trace_of, st, 
                                    _lib.WALK_DRAWS | _lib.WALK_SEGMENTS, wptr))
         walked[w % K].record(walk)
 
+    # everything already issued on the main stream (the chains' construction, a previous
+    # run's last commit) precedes this run's plans, draws and walks
+    begun = torch.cuda.Event()
+    begun.record(main)
+    walk.wait_event(begun)
+    if pst is not walk:
+        pst.wait_event(begun)
     for w in range(min(K - 1, len(wins))):
         issue_walk(w)
     for w in range(len(wins)):

@@ -272,12 +272,12 @@ class BatchPipeline:
     def _build(self, k):      # construction of batch k's chains, its plan and draws
         L, sim, cx = self.L, self.sim, self.ctx_of(k)
         cx.chain0 = self.chain0_of(k)
-        if self.cfg.build_on == "walk":   # on the batch's walk stream, after the expansion
-            bs, bp = cx.wstream, cx.wptr   # that last used this context: beside the running expansion
-            if cx.expanded is not None:
-                bs.wait_event(cx.expanded)
+        if self.cfg.build_on == "walk":   # on the batch's walk stream, beside the running expansion
+            bs, bp = cx.wstream, cx.wptr
         else:                          # in order on the expansion stream
             bs, bp = self.estream, self.eptr
+        if cx.expanded is not None:   # after the commit of the context's previous batch (it reads
+            bs.wait_event(cx.expanded)   # and writes the state and scratch this construction resets)
         _lib.check(L.tmh_init(sim._eng, self._p(cx.state), cx.chain0, self.n, None, bp))
         _lib.check(L.tmh_plan(sim._eng, 0, self.secs, self._p(cx.plan), bp))
         _lib.check(L.tmh_walk_part(sim._eng, self._p(cx.state), cx.chain0, self.n, 0, self.secs, self._p(cx.plan),
