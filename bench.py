@@ -529,7 +529,7 @@ def main():
                    "batches_in_flight": len(pipe.ctxs), "staggered": bool(args.stagger and nwin == 1),
                    "construction_on": args.build_on, "walk_priority": args.walk_priority,
                    "schedule": args.schedule if pipe.gated() else None,
-                   "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"), "walks_in_flight": W, "walk_order": bool(args.walk_order), "walk_cus": args.walk_cus or "all", "other_cus": args.other_cus if args.walk_cus else "all",
+                   "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"), "walks_in_flight": pipe.W, "walk_order": bool(args.walk_order), "walk_cus": args.walk_cus or "all", "other_cus": args.other_cus if args.walk_cus else "all",
                    "walk_chains_per_row": args.walk_cpr, "walk_lanes": args.walk_lanes or "auto", "build_ahead": pipe.A,
                    "minutes_ahead": bool(args.minutes_ahead), "commit_stream": bool(args.commit_stream),
                    "compacted_windows": bool(args.compact and args.mode == "stats" and nwin > 1)},
