@@ -163,12 +163,13 @@ def parse():
                          "that take the next chain when theirs is done")
     ap.add_argument("--walk-lanes", type=int, default=0,
                     help="lanes per chain in the segment walk (tmh_set_walk_lanes: 4, 8 or 16; 0 = by batch size: 16 up to 8,192 chains, else 4)")
-    ap.add_argument("--hw-queues", type=int, default=16,
+    ap.add_argument("--hw-queues", type=int, default=None,
                     help="GPU_MAX_HW_QUEUES for this process (set before HIP starts; 0 = leave the environment's). "
                          "HIP maps streams round-robin onto that many hardware queues and a queue runs its "
                          "packets in order across the streams sharing it: with HIP's default 4 the expansion "
                          "stream shares a queue with another pipeline stream and waits for its kernels (same "
-                         "box: 1.74-1.76 ms per C2 batch with 4 queues, 1.49-1.51 with 8, 1.47-1.51 with 16)")
+                         "box: 1.74-1.76 ms per C2 batch with 4 queues, 1.49-1.51 with 8, 1.47-1.51 with 16); "
+                         "default 16, 32 for c4 / c5 (three streams per batch in flight, up to 8 batches)")
     ap.add_argument("--secondary", default=None,
                     help="after the headline measurement (one GPU only), run the other configurations in child "
                          "processes and add their lines under 'secondary': all | none | a comma list of "
@@ -239,6 +240,8 @@ def parse():
         # the full report (the default C2 run with its CPU baseline) carries them; quick runs do not
         a.secondary = "all" if (a.workload == "c2" and a.precision == "fp32" and not a.no_cpu_baseline) else "none"
     a.cc = a.cc or ("markov" if c5 else "faithful")
+    if a.hw_queues is None:
+        a.hw_queues = 32 if (c4 or c5) else 16
     a.start = a.start or ("2019-01-01 00:00:00" if c4 else "2019-09-05 00:00:00")
     return a
 
@@ -251,7 +254,7 @@ SECONDARY = {   # --secondary: the other BASELINE.json configs, each in a child 
     "c5": ["--workload", "c5", "--steps", "3", "--warmup", "1"],
     # one-GPU proxies of the strong-scaled configurations at N = 8 (and C4 at 2, 4): rank 0's
     # shard timed alone (8 batches in flight for C4 / C5 shards, pipeline_defaults);
-    # `projected_efficiency` = N x its rate / the N = 1 rate above
+    # `projected_efficiency` = T_1 / (N T_N) = its (rank) rate / the N = 1 rate above
     "c3_proxy8": ["--workload", "c3", "--proxy-world", "8", "--steps", "6", "--warmup", "2"],
     "c4_proxy2": ["--workload", "c4", "--proxy-world", "2", "--steps", "6", "--warmup", "1"],
     "c4_proxy4": ["--workload", "c4", "--proxy-world", "4", "--steps", "8", "--warmup", "1"],
@@ -287,10 +290,10 @@ def secondary_lines(args):
                                  proxy_note=d["proxy_note"])
         except Exception as e:   # noqa: BLE001 - report, never lose the headline line
             out[name] = {"error": f"{type(e).__name__}: {e}"[:300]}
-    for name, d in out.items():   # strong-scaling readiness on one GPU: N x rank rate / the N = 1 rate
+    for name, d in out.items():   # strong-scaling readiness on one GPU: T_1 / (N T_N) = rank rate / N = 1 rate
         base = out.get(name.split("_proxy")[0], {})
         if d.get("proxy_world") and base.get("value"):
-            d["projected_efficiency"] = d["proxy_world"] * d["value"] / base["value"]
+            d["projected_efficiency"] = d["value"] / base["value"]
     return out
 
 

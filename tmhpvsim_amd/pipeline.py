@@ -161,22 +161,29 @@ class BatchPipeline:
                                          self.acc.data_ptr())
 
         self.ctxs = [Ctx() for _ in range(max(1, cfg.pipeline))]
-        # one stream for every batch's expansion: expansions run back to back, in order
-        # (they fill the chip on their own), while the walks of the next batches run on
-        # their own streams beside them
-        self.estream = torch.cuda.Stream(device, priority=self._prio(cfg.expand_priority))
+        # One-window batches (C2, C3): one stream for every batch's expansion (expansions run
+        # back to back, in order: they fill the chip on their own) and, on the gated schedule,
+        # walk / construction / commit streams shared by the batches.  Multi-window batches
+        # (C4, C5) run on their contexts' own streams (main, walk, plan): HIP maps streams
+        # round-robin onto GPU_MAX_HW_QUEUES hardware queues and a queue runs its packets in
+        # order across the streams sharing it, so streams nobody uses are not created (bench.py
+        # raises the queues to 32 for these workloads' 3 streams per context).
         W = self.W = max(1, cfg.walks)
-        self.wsts = [torch.cuda.Stream(device, priority=self._prio(cfg.walk_priority)) for _ in range(W)]
-        self.bst = torch.cuda.Stream(device, priority=self._prio(cfg.build_priority))
-        self.cst = torch.cuda.Stream(device)
-        if cfg.walk_cus:   # the walks on a share of every XCD's CUs (CU-masked streams)
-            ncu = torch.cuda.get_device_properties(device).multi_processor_count
-            self.wsts = [_lib.cu_stream(0, cfg.walk_cus, device) for _ in range(W)]
-            if cfg.other_cus == "rest":
-                self.bst, self.cst = (_lib.cu_stream(cfg.walk_cus, ncu - cfg.walk_cus, device) for _ in range(2))
-                self.estream = _lib.cu_stream(cfg.walk_cus, ncu - cfg.walk_cus, device)
-        self.eptr = C.c_void_p(self.estream.cuda_stream)
-        self.bst_p = C.c_void_p(self.bst.cuda_stream)
+        self.estream = self.bst = self.cst = None
+        self.wsts = []
+        if nwin == 1:
+            self.estream = torch.cuda.Stream(device, priority=self._prio(cfg.expand_priority))
+            self.wsts = [torch.cuda.Stream(device, priority=self._prio(cfg.walk_priority)) for _ in range(W)]
+            self.bst = torch.cuda.Stream(device, priority=self._prio(cfg.build_priority))
+            self.cst = torch.cuda.Stream(device)
+            if cfg.walk_cus:   # the walks on a share of every XCD's CUs (CU-masked streams)
+                ncu = torch.cuda.get_device_properties(device).multi_processor_count
+                self.wsts = [_lib.cu_stream(0, cfg.walk_cus, device) for _ in range(W)]
+                if cfg.other_cus == "rest":
+                    self.bst, self.cst = (_lib.cu_stream(cfg.walk_cus, ncu - cfg.walk_cus, device) for _ in range(2))
+                    self.estream = _lib.cu_stream(cfg.walk_cus, ncu - cfg.walk_cus, device)
+            self.eptr = C.c_void_p(self.estream.cuda_stream)
+            self.bst_p = C.c_void_p(self.bst.cuda_stream)
         self.A = cfg.build_ahead
         self.tl = {}   # timeline: per-batch HIP timing events (build done, walk start / end, expansion start / end)
 
@@ -219,7 +226,7 @@ class BatchPipeline:
         # multi-window: each window's plan, draws and walk on the context's walk stream,
         # up to two windows ahead of the expansions on its stream (engine.run_windows)
         wins = [(s0, min(win, secs - s0)) for s0 in range(0, secs, win)]
-        if getattr(cx, "pstream", None) is None:
+        if getattr(cx, "pstream", None) is None:   # the context's plan stream (plans are per batch)
             cx.pstream = self.torch.cuda.Stream(self.dev)
         run_windows(L, sim._eng, cx.state, chain0, n, wins, cx.wbufs, cx.stream, cx.wstream, lambda w: cx.tr, cx.st,
                     plan_stream=cx.pstream)
