@@ -49,6 +49,35 @@ TRACE_BYTES = 12               # meter + pv + residual, fp32 (24 in fp64)
 # VALU issue peak: 256 CUs x 4 SIMD-32 x 32 lanes per cycle x 2.4 GHz (a wave64
 # instruction issues over 2 cycles, MI355X_MICROARCH.md), in lane-ops/s
 VALU_PEAK_TLANE = 256 * 4 * 32 * 2.4e9 / 1e12
+# Issue cycles per wave64 VALU instruction by rocprofv3 class, from the dependent-free
+# ("distinct") loops of profiles/r03_isa_rate.txt: fp32 add / mul / fma 2.2, integer
+# add and bit ops 2.3-2.8, fp64 add / mul / fma, cvt, 64-bit integer mad 4.1-4.3,
+# fp32 transcendentals 8.4, fp64 reciprocal 16.  Instructions in no class (compares,
+# selects, min / max / med3, DPP moves: 4.1-4.2; plain moves 2.2) are weighed at 4.
+VALU_CYCLES = {"ADD_F32": 2, "MUL_F32": 2, "FMA_F32": 2, "INT32": 2.5, "TRANS_F32": 8,
+               "ADD_F64": 4, "MUL_F64": 4, "FMA_F64": 4, "INT64": 4, "CVT": 4, "TRANS_F64": 16}
+VALU_OTHER_CYCLES = 4
+SIMD_CYCLES_PER_S = 256 * 4 * 2.4e9   # SIMDs x nominal clock
+
+
+def valu_busy(rec, ms):
+    """Cycle-weighted VALU-busy fractions of one launch of `ms` milliseconds:
+    'weighted' = the per-class wave-instruction counts x their issue cycles over the
+    SIMDs' cycles; 'active' = SQ_ACTIVE_INST_VALU (quad-cycles each wave spends on
+    VALU instructions, summed over waves) x 4 over the same.  The instruction-count
+    'frac' beside them prices every instruction at the 2-cycle fp32 rate."""
+    out = {}
+    denom = SIMD_CYCLES_PER_S * ms / 1e3
+    mix = rec.get("valu_mix")
+    if mix:
+        known = sum(mix.get(k, 0.0) for k in VALU_CYCLES)
+        other = max(0.0, rec["valu_insts_per_launch"] - known)
+        cyc = sum(mix.get(k, 0.0) * w for k, w in VALU_CYCLES.items()) + other * VALU_OTHER_CYCLES
+        out.update(busy_frac_weighted=cyc / denom, valu_cycles_per_launch=cyc,
+                   valu_other_insts_per_launch=other)
+    if rec.get("active_inst_valu"):
+        out["busy_frac_active"] = 4 * rec["active_inst_valu"] / denom
+    return out
 
 # BASELINE.json configs[1..4]: C2 4,096 sites on one GPU (weak scaling: per GPU);
 # C3 1 M chains, C4 16,384 sites, C5 65,536 sites for the node (strong scaling)
@@ -240,6 +269,7 @@ def parse():
         # the full report (the default C2 run with its CPU baseline) carries them; quick runs do not
         a.secondary = "all" if (a.workload == "c2" and a.precision == "fp32" and not a.no_cpu_baseline) else "none"
     a.cc = a.cc or ("markov" if c5 else "faithful")
+    a.hw_queues_given = a.hw_queues is not None   # secondaries pick their own default otherwise
     if a.hw_queues is None:
         a.hw_queues = 32 if (c4 or c5) else 16
     a.start = a.start or ("2019-01-01 00:00:00" if c4 else "2019-09-05 00:00:00")
@@ -273,8 +303,9 @@ def secondary_lines(args):
     for name, extra in SECONDARY.items():
         if args.secondary != "all" and name not in args.secondary.split(","):
             continue
-        cmd = [sys.executable, os.path.abspath(__file__), "--no-cpu-baseline", "--secondary", "none",
-               "--hw-queues", str(args.hw_queues)] + extra
+        cmd = [sys.executable, os.path.abspath(__file__), "--no-cpu-baseline", "--secondary", "none"] + extra
+        if args.hw_queues_given:
+            cmd += ["--hw-queues", str(args.hw_queues)]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
             d = json.loads(r.stdout.strip().splitlines()[-1])
@@ -282,7 +313,8 @@ def secondary_lines(args):
             out[name] = {"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"],
                          "steps": d["steps"], "dtype": d["dtype"], "workload": d["config"]["workload"],
                          "roofline": {k: roof.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
-                                                               "kernel_ms")},
+                                                               "kernel_ms", "busy_frac_weighted",
+                                                               "busy_frac_active")},
                          "roofline_alone": roof.get("alone"), "faulted_chains": d.get("faulted_chains"),
                          "chain_seconds_live": d.get("chain_seconds_live")}
             if d.get("proxy_world"):
@@ -489,7 +521,8 @@ def main():
         a = rec["valu_insts_per_launch"] * 64 / (ms / 1e3) / 1e12
         return {"achieved": a, "peak": VALU_PEAK_TLANE, "unit": "T lane-ops/s", "frac": a / VALU_PEAK_TLANE,
                 "valu_per_chain_second": rec["valu_insts_per_launch"] * 64 / (n * launch_secs),
-                "salu_per_chain_second": rec["salu_insts_per_launch"] * 64 / (n * launch_secs)}
+                "salu_per_chain_second": rec["salu_insts_per_launch"] * 64 / (n * launch_secs),
+                **valu_busy(rec, ms)}
 
     if args.mode == "trace":
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -505,7 +538,10 @@ def main():
         va = valu(alone_ms / nwin) or {}   # the same launch with no other batch in flight
         roof = {"bound": "valu", "achieved": v.get("achieved"), "peak": VALU_PEAK_TLANE, "unit": "T lane-ops/s",
                 "frac": v.get("frac"), "traffic": rec["traffic_bytes_per_launch"] if rec else None,
-                "alone": {"kernel_ms": alone_ms / nwin, "achieved": va.get("achieved"), "frac": va.get("frac")},
+                "alone": {"kernel_ms": alone_ms / nwin, "achieved": va.get("achieved"), "frac": va.get("frac"),
+                          "busy_frac_weighted": va.get("busy_frac_weighted"),
+                          "busy_frac_active": va.get("busy_frac_active")},
+                "busy_frac_weighted": v.get("busy_frac_weighted"), "busy_frac_active": v.get("busy_frac_active"),
                 "kernel": "expand_kernel (P2, " + sim.path + ")", "kernel_ms": kms_launch,
                 "launches_per_batch": nwin, "chain_seconds_per_launch": n * launch_secs,
                 "valu_per_chain_second": v.get("valu_per_chain_second"),

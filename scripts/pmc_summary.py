@@ -70,6 +70,9 @@ def record(d, **key):
                      ("active_inst_valu", "SQ_ACTIVE_INST_VALU")):
         if cn in c:
             rec[name] = c[cn]
+    mix = {cn[len("SQ_INSTS_VALU_"):]: c[cn] for cn in sorted(c) if cn.startswith("SQ_INSTS_VALU_")}
+    if len(mix) > 1:   # per-type VALU wave-instructions (bench.py weighs them by issue cycles)
+        rec["valu_mix"] = mix
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         rec["fetch_bytes_corrected"] = c["FETCH_SIZE"] * 1024 * 2
         rec["write_bytes"] = c["WRITE_SIZE"] * 1024

@@ -140,13 +140,30 @@ def test_secondary_lines_report_a_failed_child(monkeypatch):
         stdout = "not json"
 
     monkeypatch.setattr(subprocess, "run", lambda *a, **k: R())
-    out = bench.secondary_lines(argparse.Namespace(secondary="c3", hw_queues=16))
+    out = bench.secondary_lines(argparse.Namespace(secondary="c3", hw_queues=16, hw_queues_given=False))
     assert list(out) == ["c3"] and "error" in out["c3"]
 
 
-def test_hw_queues_flag_defaults_to_sixteen(monkeypatch):
-    monkeypatch.setattr(sys, "argv", ["bench.py"])
-    assert bench.parse().hw_queues == 16
+def test_hw_queues_flag_defaults(monkeypatch):
+    """16 hardware queues for C2 / C3; 32 for C4 / C5 (three streams per batch in flight)."""
+    for argv, want in (([], 16), (["--workload", "c3"], 16), (["--workload", "c4"], 32),
+                       (["--workload", "c5"], 32), (["--workload", "c4", "--hw-queues", "8"], 8)):
+        monkeypatch.setattr(sys, "argv", ["bench.py"] + argv)
+        a = bench.parse()
+        assert a.hw_queues == want and a.hw_queues_given == ("--hw-queues" in argv)
+
+
+def test_valu_busy_weights_the_instruction_classes():
+    """The cycle-weighted VALU-busy fraction: class counts x issue cycles, the rest at 4,
+    over 1024 SIMDs x 2.4 GHz; SQ_ACTIVE_INST_VALU is in quad-cycles."""
+    rec = {"valu_insts_per_launch": 1000.0, "active_inst_valu": 600.0,
+           "valu_mix": {"FMA_F32": 500.0, "TRANS_F32": 100.0, "FMA_F64": 100.0}}
+    ms = 1e3 / bench.SIMD_CYCLES_PER_S   # one SIMD-cycle of the whole chip
+    b = bench.valu_busy(rec, ms)
+    assert b["valu_other_insts_per_launch"] == 300.0
+    assert abs(b["valu_cycles_per_launch"] - (500 * 2 + 100 * 8 + 100 * 4 + 300 * 4)) < 1e-9
+    assert abs(b["busy_frac_weighted"] - 3400.0) < 1e-6 and abs(b["busy_frac_active"] - 2400.0) < 1e-6
+    assert bench.valu_busy({"valu_insts_per_launch": 1.0}, 1.0) == {}
 
 
 def test_pipeline_defaults_match_bench_schedule():
