@@ -71,7 +71,7 @@ extern "C" {
 #define TMH_PATH_TIME_PARALLEL 2 /* segment pass + (chain x 128 s block) expansion */
 
 #define TMH_SIGMA_CAP 512  /* capacity of sigma_cloud / sigma_clear per chain (max seen: 132) */
-#define TMH_GEOM_FIELDS 20 /* doubles per step in the clock/geometry table */
+#define TMH_GEOM_FIELDS 22 /* doubles per step in the clock/geometry table */
 
 /* ---- SAPM module parameter order (tmh_params.module) ---- */
 enum {

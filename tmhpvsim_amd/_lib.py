@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("TMHPVSIM_LIB") or os.path.join(HERE, "libtmhpvsim.so"
 
 TMH_ABI_VERSION = 1
 TMH_SIGMA_CAP = 512
-TMH_GEOM_FIELDS = 20
+TMH_GEOM_FIELDS = 22
 TMH_STATE_NFIELDS = 24
 TMH_FP32, TMH_FP64 = 0, 1
 PATH_AUTO, PATH_SEQUENTIAL, PATH_TIME_PARALLEL = 0, 1, 2

@@ -1762,7 +1762,8 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
                                             const int2* __restrict__ events, const uint32_t* __restrict__ n_events,
                                             const BlockDesc* __restrict__ desc, const SegView& sg,
                                             const TraceView& tr, const StatsView& sv, uint32_t* lds_hist,
-                                            uint32_t (*cov_lds)[WGT], R (*min_lds)[WGT], uint4* held_lds)
+                                            uint32_t (*cov_lds)[WGT], R (*min_lds)[WGT], uint4* held_lds,
+                                            const PV64* pv_lds, const double* log_lds_tab)
 {
     const uint32_t c = cblk * blockDim.x + threadIdx.x;
     const bool live = c < n;
@@ -1945,7 +1946,19 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
             meter = meter_w<R>(um);
             res = meter - pv;
         } else {
-            second_body<R>(kp, pkv, row, flp, fs, covered, noise_z<R>(un), meter_w<R>(um), csi, pv, meter, res, held);
+            if constexpr (sizeof(R) == 8 && !SITES) {
+                // the PV constants re-read from LDS each second (ds_read, no VALU) through an
+                // address the compiler cannot see is loop-invariant: hoisted, they would sit
+                // in SGPRs across the loop, be spilled to VGPR lanes and cost two v_readlane
+                // each per use (a sixth of the loop's VALU)
+                uint32_t pa = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) PV64*)pv_lds;
+                asm volatile("" : "+v"(pa));
+                const __attribute__((address_space(3))) PV64* p = (const __attribute__((address_space(3))) PV64*)(uintptr_t)pa;
+                second_body<R>(kp, pkv, row, flp, fs, covered, noise_z<R>(un), meter_w<R>(um), csi, pv, meter, res, held,
+                               p, (LdsD*)log_lds_tab);
+            } else {
+                second_body<R>(kp, pkv, row, flp, fs, covered, noise_z<R>(un), meter_w<R>(um), csi, pv, meter, res, held);
+            }
         }
         held = held && ok && live;   // lanes past the last chain run on uninitialised samplers: never held
         if constexpr (sizeof(R) == 4) {
@@ -2027,19 +2040,20 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
 }
 
 
-// Statistics without per-chain sites (C3, C4) run persistent workgroups: grid = the CUs'
-// resident workgroups, each looping over (chain block, time block) tiles (tile t =
-// blockIdx.x + k gridDim.x, time block fastest).  Each workgroup keeps one LDS histogram
-// of 16-bit bin pairs over all its tiles and flushes it to the device histogram once at
-// its end (plus, after a tile, any bin that reached 2^15: a tile adds at most 128 x 256 =
-// 2^15 to a bin, so no bin overflows 16 bits) -- instead of flushing up to 4,096
-// device-scope 64-bit atomics after every tile (round 3: 2.38 B of HBM writes per
-// chain-second, almost all of them these flushes).  The other outputs keep one tile per
-// workgroup (grid x = time block, y = chain block).
+// Statistics without per-chain sites (C3, C4): a workgroup runs EXP_TILES consecutive
+// 128-s blocks of its chain block (grid x = ceil(blocks / EXP_TILES), y = chain block)
+// and keeps one LDS histogram of 16-bit bin pairs over them, flushed to the device
+// histogram once at its end (plus, after a block, any bin that reached 2^15: a block
+// adds at most 128 x 256 = 2^15 to a bin, so no bin overflows 16 bits) -- a quarter of
+// the device-scope 64-bit atomics of one flush per block (round 3: 2.38 B of HBM
+// writes per chain-second, almost all of them these flushes).  Round 4 measured a
+// persistent grid (the device's resident workgroups looping over all blocks) 8-40 %
+// slower on C3 / C4 than hardware dispatch of one workgroup per tile; a few blocks per
+// workgroup keep the hardware's dynamic balance.
 template <typename R, int OUT, bool SITES>
-constexpr bool exp_persistent()
+constexpr int exp_tiles()
 {
-    return OUT == OUT_STATS && !SITES;
+    return OUT == OUT_STATS && !SITES ? 4 : 1;
 }
 template <typename R, int OUT, bool SITES>
 __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0,
@@ -2057,6 +2071,14 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
     __shared__ uint32_t cov_lds[4][WGT];
     __shared__ R min_lds[4][WGT];   // minute boundaries mA, mA + 1 of the block: cloudy, clear noise
     __shared__ uint4 held_lds[WGT];
+    // fp64: the PV constants and log_lds's table (one copy per workgroup)
+    __shared__ PV64 pv_lds[1];   // (176 + 16 bytes in the fp32 kernels: unused)
+    __shared__ __attribute__((aligned(16))) double log_tab[sizeof(R) == 8 ? 2 * LOG_TAB : 2];
+    if constexpr (sizeof(R) == 8) {
+        if (threadIdx.x < PV64_N) reinterpret_cast<double*>(pv_lds)[threadIdx.x] = reinterpret_cast<const double*>(&kp.pv64)[threadIdx.x];
+        log_table_fill(log_tab, threadIdx.x);
+        __syncthreads();
+    }
     const uint32_t nw = (sv.n_bins + 1) / 2;   // 16-bit bin pairs
     if (sv.hist) {
         for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) lds_hist[i] = 0;
@@ -2064,12 +2086,13 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
     }
     auto tile = [&](uint32_t b, uint32_t cblk) __attribute__((always_inline)) {
         expand_tile<R, OUT, SITES, WGT>(b, cblk, kp, dp, st, chain0, n, W0, nsteps, utc0, tab64, tab32, sun, events,
-                                        n_events, desc, sg, tr, sv, lds_hist, cov_lds, min_lds, held_lds);
+                                        n_events, desc, sg, tr, sv, lds_hist, cov_lds, min_lds, held_lds, pv_lds, log_tab);
     };
-    if constexpr (exp_persistent<R, OUT, SITES>()) {
-        const uint32_t ntile = sg.nblk * ((n + WGT - 1) / WGT);
-        for (uint32_t t = blockIdx.x; t < ntile; t += gridDim.x) {
-            tile(t % sg.nblk, t / sg.nblk);
+    if constexpr (exp_tiles<R, OUT, SITES>() > 1) {
+        constexpr uint32_t KT = exp_tiles<R, OUT, SITES>();
+        const uint32_t b1 = min((blockIdx.x + 1) * KT, sg.nblk);
+        for (uint32_t b = blockIdx.x * KT; b < b1; ++b) {
+            tile(b, blockIdx.y);
             if (sv.hist) {   // bins at 2^15 or more go to the device histogram before the next tile
                 __syncthreads();
                 for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) {
@@ -2699,6 +2722,29 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
         f.pacoc = (float)(iv[0] > 0.0 ? iv[0] : 0.0);
         f.eps0 = (float)(k.sqrt6 * 0.001);
         f.eps1 = (float)(k.sqrt6 * (0.0015 * 8));
+        PV64& d = k.pv64;   // the same forms in fp64 (ln, not log2: pv_power_d's log is natural)
+        d.tk = k.tmod_k + m[TMH_MOD_TEMP_DT] * 1e-3;
+        d.temp_air = k.temp_air;
+        d.fd = m[TMH_MOD_FD];
+        d.nmbvmp = -m[TMH_MOD_MBVMP];
+        d.bvmpo1 = m[TMH_MOD_BVMPO] + m[TMH_MOD_MBVMP];
+        d.nkq = m[TMH_MOD_N] * 1.38066e-23 / 1.60218e-19;
+        d.impo_c0 = m[TMH_MOD_IMPO] * m[TMH_MOD_C0];
+        d.impo_c1 = m[TMH_MOD_IMPO] * m[TMH_MOD_C1];
+        d.aimp0 = 1.0 - 25.0 * m[TMH_MOD_AIMP];
+        d.aimp = m[TMH_MOD_AIMP];
+        d.vmpo = m[TMH_MOD_VMPO];
+        d.c2ns = m[TMH_MOD_C2] * m[TMH_MOD_NS];
+        d.c3ns = m[TMH_MOD_C3] * m[TMH_MOD_NS];
+        d.paco = iv[0];
+        d.pso = iv[3];
+        d.ab1 = a1 - b1;
+        d.ab0 = a0 - b0;
+        d.b1 = b1;
+        d.b0 = b0;
+        d.c1 = c1;
+        d.c0 = c0;
+        d.pnt = -fabs(iv[8]);
     }
     memcpy(e->gp.site, p->site, sizeof e->gp.site);
     memcpy(e->gp.linke, p->linke, sizeof e->gp.linke);
@@ -3073,25 +3119,16 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
                     : (!tv.pv && !tv.meter && !tv.residual && !tv.csi && !tv.covered) ? OUT_STATS
                                                                                       : OUT_ANY;
     const size_t lds_exp = stats && stats->hist ? (size_t)((stats->n_bins + 1) / 2) * 4 : 0;   // 16-bit bin pairs
-    // one workgroup per tile, or (persistent statistics kernels) the resident workgroups of
-    // the device, at most one per tile
-    auto exp_grid = [&](uint32_t wg, bool persist, const void* kfn) {
-        const uint32_t ecb = (n_chains + wg - 1) / wg;
-        if (!persist) return dim3(sg.nblk, ecb);
-        const uint64_t ntile = (uint64_t)sg.nblk * ecb;
-        int per_cu = 0, ncu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, (int)wg, lds_exp) != hipSuccess || per_cu < 1)
-            per_cu = 1;
-        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, eng->device) != hipSuccess || ncu < 1)
-            ncu = 256;
-        return dim3((uint32_t)std::min<uint64_t>(ntile, (uint64_t)per_cu * ncu));
+    // x = time blocks (EXP_TILES per workgroup), y = chain blocks
+    auto exp_grid = [&](uint32_t wg, uint32_t kt) {
+        return dim3((sg.nblk + kt - 1) / kt, (n_chains + wg - 1) / wg);
     };
     if (out == OUT_TRACE3 && tv.ld * (f64 ? 8u : 4u) * BLOCK_STEPS >= (1ull << 31))   // one block's rows: one buffer range
         return fail(TMH_E_INVAL, "trace ld %llu too large (a 128-step block of rows must stay under 2 GiB)",
                     (unsigned long long)tv.ld);
 #define LAUNCH(R, O, S)                                                                                            \
     hipLaunchKernelGGL((expand_kernel<R, O, S>),                                                                   \
-                       exp_grid(exp_wg<R, O, S>(), exp_persistent<R, O, S>(), (const void*)&expand_kernel<R, O, S>), \
+                       exp_grid(exp_wg<R, O, S>(), exp_tiles<R, O, S>()),                                      \
                        dim3(exp_wg<R, O, S>()), lds_exp, s, eng->kp, eng->dp, v, chain0, n_chains, step0, n_steps,   \
                        utc0, pv.tab64, pv.tab32, pv.sun, pv.events, pv.n_events, pv.desc, sg, tv, sv)
     if (eng->kp.sites) {   // per-chain sites: one instantiation per precision, any output

@@ -364,4 +364,45 @@ __device__ __noinline__ double al_ppf(double y, double kappa)
 // fp64 pow out of line (cloud lengths, cloud_cover_binary.py:40): keeps callers' registers low
 __device__ __noinline__ double pow_d(double x, double y) { return pow(x, y); }
 
+// ---- fp64 natural log from an LDS table (the PV chain's log(Ee), pv_power_d) ----
+// x = 2^e m, m in [1, 2); c_i = 1 + (i + 1/2) / 128 for the top 7 bits i of m's
+// mantissa, u = m / c_i - 1 (|u| <= 2^-8, as fma(m, 1 / c_i, -1)), and
+// log x = e ln 2 + log c_i + log1p(u) with log1p to u^7 / 7 (truncation < 2^-67).
+// Absolute error a few 1e-16 (the rounding of e ln 2, 1 / c_i and log c_i): the PV
+// chain needs 1e-12 relative.  13 VALU instead of ocml log's ~90.  Zero, negative,
+// NaN, infinite and subnormal x take ocml's log (and its -inf / NaN).
+typedef __attribute__((address_space(3))) const double LdsD;
+constexpr int LOG_TAB = 128;
+
+// the table: t[2 i] = 1 / c_i, t[2 i + 1] = log c_i (one thread per entry)
+__device__ __forceinline__ void log_table_fill(double* t, uint32_t i)
+{
+    if (i < (uint32_t)LOG_TAB) {
+        const double c = 1.0 + (i + 0.5) * (1.0 / LOG_TAB);
+        t[2 * i] = 1.0 / c;
+        t[2 * i + 1] = log(c);
+    }
+}
+
+// (out of line: inlined, its constants would be hoisted into registers across the caller's loop)
+__device__ __noinline__ double log_edge(double x) { return x > 0.0 ? log(x) : (x == 0.0 ? -INFINITY : NAN); }
+
+__device__ __forceinline__ double log_lds(double x, LdsD* t)
+{
+    if (__builtin_expect(!(x >= 0x1p-1022) || x == INFINITY, 0)) return log_edge(x);
+    const uint64_t bits = (uint64_t)__double_as_longlong(x);
+    const uint32_t hi = (uint32_t)(bits >> 32);
+    const int e = (int)(hi >> 20) - 1023;
+    const uint32_t i = (hi >> 13) & (uint32_t)(LOG_TAB - 1);
+    const double m = __longlong_as_double((long long)(((uint64_t)((hi & 0x000FFFFFu) | 0x3FF00000u) << 32) |
+                                                      (bits & 0xFFFFFFFFull)));
+    const double u = fma(m, t[2 * i], -1.0);
+    double h = fma(u, 1.0 / 7.0, -1.0 / 6.0);
+    h = fma(h, u, 1.0 / 5.0);
+    h = fma(h, u, -1.0 / 4.0);
+    h = fma(h, u, 1.0 / 3.0);
+    h = fma(h, u, -1.0 / 2.0);
+    return fma((double)e, 0.693147180559945309417, t[2 * i + 1]) + fma(u * u, h, u);
+}
+
 }  // namespace tmh

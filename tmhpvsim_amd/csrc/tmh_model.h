@@ -28,6 +28,17 @@ struct PVF {
     float eps0, eps1;   // sqrt(6) 0.001, sqrt(6) 0.0015 * 8: the noise scale is eps0 + eps1 cc
 };
 
+// fp64 constants of the PV chain, folded on the host like PVF (pv_power_d): the
+// products and sums differ from pvmodel.py's order of operations by an ulp or two,
+// 1e-16 relative against the fp64 bar of 1e-12.
+//   tcell = poa tk + temp_air; Bvmpo = bvmpo1 + nmbvmp Ee; delta = nkq (tcell + 273.15)
+//   imp = Ee (impo_c0 + impo_c1 Ee) (aimp0 + aimp tcell); A - B, B, C affine in vmp
+struct PV64 {
+    double tk, temp_air, fd, nmbvmp, bvmpo1, nkq, impo_c0, impo_c1, aimp0, aimp, vmpo, c2ns, c3ns;
+    double paco, pso, ab1, ab0, b1, b0, c1, c0, pnt;   // pnt = -|Pnt| (night tare)
+};
+constexpr int PV64_N = sizeof(PV64) / 8;
+
 struct KParams {
     int32_t cc_mode, rng_mode, with_pv, precision;
     uint64_t seed;
@@ -40,6 +51,7 @@ struct KParams {
     double temp_air, wind;                      // sapm_celltemp inputs (pvmodel.py:69-70)
     double tmod_k;                              // exp(a + b * wind): constant for the run (wind fixed at 0)
     PVF pvf;                                    // fp32 copies for the fp32 chain
+    PV64 pv64;                                  // the fp64 chain's folded constants
     const double* tab;                          // per-chain shape tables [n][6][4] (NULL: shapes)
     const int32_t* tab_t;                       // per-chain Student-t flags [n][6] (NULL: is_t)
     const double* sites;                        // per-chain PV sites [n][8] (NULL: the plan's site)
@@ -67,8 +79,12 @@ enum {
     G_MINF = 0, G_HOURF = 1, G_DAYF = 2, G_FLAGS = 3, G_COSZ = 4, G_CSIMAX = 5, G_GHICS = 6,
     G_I0H = 7, G_I0 = 8, G_KNC = 9, G_AM = 10, G_F2 = 11, G_RB = 12, G_DNIEXTRA = 13,
     G_TERM2 = 14, G_GFAC = 15, G_COSAOI = 16, G_F1 = 17, G_DISCOK = 18,
-    G_LAST = 18   // DISC's zenith test last: the fp32 single-site kernels read it as FL_DISCOK, so their
+    G_LAST = 18,  // DISC's zenith test last: the fp32 single-site kernels read it as FL_DISCOK, so their
                   // scalar loads of a row stop one field early (3 s_loads a second, not 6 around a hole)
+    // fp64 rows only (pv_power_d multiplies where pvmodel.py divides): kt = csi GHI_cs / I0h
+    // and AI = dni / dni_extra as products, within an ulp or two of the quotients
+    G_KTC = 19,     // GHI_cs / I0h
+    G_RDNIX = 20    // 1 / dni_extra (field 21 unused: rows of 22 doubles, 16-byte aligned)
 };
 // fp32 row (ROW32 = 22 floats, the kernels' scalar loads): each clock fraction
 // beside its complement 1 - f (rounded in fp32 exactly as the kernels would),
@@ -986,6 +1002,8 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     f2 = f2 > 0.0 ? f2 : 0.0;
     if (aoi < 0.0) f2 = 0.0;
     g[G_F2] = f2;
+    g[G_KTC] = g[G_GHICS] / g[G_I0H];
+    g[G_RDNIX] = sun[SUN_RDNIX];
     return g[G_GHICS] == 0.0;
 }
 
@@ -999,7 +1017,10 @@ __device__ __forceinline__ void site_row(const double* g, const double* sun, R* 
     R* row = row_base + row_off<R>();
 #pragma unroll
     for (int i = G_COSZ; i <= G_LAST; ++i) row[i] = (R)g[i];
-    if constexpr (sizeof(R) == 4) {
+    if constexpr (sizeof(R) == 8) {
+        row[G_KTC] = g[G_KTC];
+        row[G_RDNIX] = g[G_RDNIX];
+    } else {
         row[G_I0H] = (float)(1.0 / g[G_I0H]);
         row[G_DNIEXTRA] = (float)sun[SUN_RDNIX];
         row[G_AM] = (float)(g[G_AM] * LOG2E);
@@ -1062,82 +1083,77 @@ __device__ __forceinline__ uint32_t lane_flags(uint32_t fl, bool night, const R*
 
 
 // ------------------------------------------------------------ PV (per chain-second)
-// pvmodel.py:53-80 on the precomputed geometry row; R = float | double.
-template <typename R>
-__device__ __forceinline__ R pv_power(const KParams& kp, const R* g, R csi)
+// pvmodel.py:53-80 on the precomputed geometry row, fp64.  `p` points at the folded
+// constants (PV64: in the kernel arguments, or an LDS copy the expansion re-reads each
+// second instead of holding 22 doubles in SGPRs across its loop); `lt` is the LDS table
+// of log_lds, or nullptr for ocml's log.  kt and AI multiply by the row's GHI_cs / I0h
+// and 1 / dni_extra; the SAPM and SNL constants are PV64's affine forms.
+// an LDS pointer re-laundered (its loads cannot move above this point, so the
+// constants are read shortly before their use instead of all at the second's start)
+template <typename PP>
+__device__ __forceinline__ PP lds_fence(PP p)
 {
-    const double* m = kp.module;
-    const double* iv = kp.inverter;
-    R c = csi > g[G_CSIMAX] ? g[G_CSIMAX] : csi;
-    const R ghi = c * g[G_GHICS];
-    R kt;
-    if constexpr (sizeof(R) == 8) kt = ghi / g[G_I0H];
-    else kt = ghi * g[G_I0H];
-    kt = kt > R(0) ? kt : R(0);
-    kt = kt < R(1) ? kt : R(1);
-    const R am = g[G_AM], kt2 = kt * kt, kt3 = kt2 * kt;
-    R a, b, cc;
-    if (kt <= R(0.6)) {
-        a = R(0.512) - R(1.56) * kt + R(2.286) * kt2 - R(2.222) * kt3;
-        b = R(0.37) + R(0.962) * kt;
-        cc = R(-0.28) + R(0.932) * kt - R(2.048) * kt2;
-    } else {
-        a = R(-5.743) + R(21.77) * kt - R(27.49) * kt2 + R(11.56) * kt3;
-        b = R(41.4) - R(118.5) * kt + R(66.05) * kt2 + R(31.9) * kt3;
-        cc = R(-47.01) + R(184.2) * kt - R(222.0) * kt2 + R(73.81) * kt3;
+    if constexpr (__is_same(PP, const PV64*)) return p;
+    else {
+        uint32_t a = (uint32_t)(uintptr_t)p;
+        asm volatile("" : "+v"(a));
+        return (PP)(uintptr_t)a;
     }
-    const R dkn = a + b * exp(cc * am);
-    R dni = (g[G_KNC] - dkn) * g[G_I0];
-    if (g[G_DISCOK] == R(0) || ghi < R(0) || dni < R(0)) dni = R(0);
-    const R dhi = ghi - dni * g[G_COSZ];
-    R AI;
-    if constexpr (sizeof(R) == 8) AI = dni / g[G_DNIEXTRA];
-    else AI = dni * g[G_DNIEXTRA];
-    R sky = dhi * (AI * g[G_RB] + (R(1) - AI) * g[G_TERM2]);
-    sky = sky > R(0) ? sky : R(0);
-    const R ground = ghi * g[G_GFAC];
-    R poa_direct = dni * g[G_COSAOI];
-    poa_direct = poa_direct > R(0) ? poa_direct : R(0);
-    const R poa_diffuse = sky + ground;
-    const R poa_global = poa_direct + poa_diffuse;
-    // sapm_celltemp (pvmodel.py:69-70), open_rack_cell_glassback
-    // (fp32: the divisions by 1000 become products with 1e-3, within the fp32 tolerance)
-    const R tmod = poa_global * R(kp.tmod_k) + R(kp.temp_air);
-    R tcell, Ee;
-    if constexpr (sizeof(R) == 8) {
-        tcell = tmod + (poa_global / R(1000)) * R(m[TMH_MOD_TEMP_DT]);
-        // sapm_effective_irradiance, suns (pvmodel.py:74-76)
-        Ee = g[G_F1] * (poa_direct * g[G_F2] + R(m[TMH_MOD_FD]) * poa_diffuse) / R(1000);
+}
+
+template <typename PP, typename LT>
+__device__ __forceinline__ double pv_power_d(PP p, const double* g, double csi, LT lt)
+{
+    const double c = csi > g[G_CSIMAX] ? g[G_CSIMAX] : csi;
+    const double ghi = c * g[G_GHICS];
+    double kt = c * g[G_KTC];
+    kt = kt > 0.0 ? kt : 0.0;
+    kt = kt < 1.0 ? kt : 1.0;
+    const double am = g[G_AM], kt2 = kt * kt, kt3 = kt2 * kt;
+    double a, b, cc;
+    if (kt <= 0.6) {
+        a = 0.512 - 1.56 * kt + 2.286 * kt2 - 2.222 * kt3;
+        b = 0.37 + 0.962 * kt;
+        cc = -0.28 + 0.932 * kt - 2.048 * kt2;
     } else {
-        tcell = tmod + (poa_global * R(1e-3)) * R(m[TMH_MOD_TEMP_DT]);
-        Ee = g[G_F1] * (poa_direct * g[G_F2] + R(m[TMH_MOD_FD]) * poa_diffuse) * R(1e-3);
+        a = -5.743 + 21.77 * kt - 27.49 * kt2 + 11.56 * kt3;
+        b = 41.4 - 118.5 * kt + 66.05 * kt2 + 31.9 * kt3;
+        cc = -47.01 + 184.2 * kt - 222.0 * kt2 + 73.81 * kt3;
     }
-    // sapm (pvmodel.py:77)
-    const R q = R(1.60218e-19), kb = R(1.38066e-23);
-    const R Bvmpo = R(m[TMH_MOD_BVMPO]) + R(m[TMH_MOD_MBVMP]) * (R(1) - Ee);
-    R delta;
-    if constexpr (sizeof(R) == 8) delta = R(m[TMH_MOD_N]) * kb * (tcell + R(273.15)) / q;
-    else delta = R(m[TMH_MOD_N] * (1.38066e-23 / 1.60218e-19)) * (tcell + R(273.15));   // fp32: no 1e-23 subnormals
-    const R logEe = Ee > R(0) ? log(Ee) : (Ee == R(0) ? -R(INFINITY) : R(NAN));
-    const R imp = R(m[TMH_MOD_IMPO]) * (R(m[TMH_MOD_C0]) * Ee + R(m[TMH_MOD_C1]) * (Ee * Ee)) *
-                  (R(1) + R(m[TMH_MOD_AIMP]) * (tcell - R(25)));
-    const R dl = delta * logEe;
-    R vmp = R(m[TMH_MOD_VMPO]) + R(m[TMH_MOD_C2]) * R(m[TMH_MOD_NS]) * delta * logEe +
-            R(m[TMH_MOD_C3]) * R(m[TMH_MOD_NS]) * (dl * dl) + Bvmpo * (tcell - R(25));
-    if (!isnan(vmp)) vmp = vmp > R(0) ? vmp : R(0);
-    const R pdc = imp * vmp;
-    // snlinverter (pvmodel.py:78)
-    const R dv = vmp - R(iv[2]);
-    const R A = R(iv[1]) * (R(1) + R(iv[5]) * dv);
-    const R B = R(iv[3]) * (R(1) + R(iv[6]) * dv);
-    const R C = R(iv[4]) * (R(1) + R(iv[7]) * dv);
-    R ac;
-    if constexpr (sizeof(R) == 8) ac = (R(iv[0]) / (A - B) - C * (A - B)) * (pdc - B) + C * ((pdc - B) * (pdc - B));
-    else ac = (__fdividef(R(iv[0]), A - B) - C * (A - B)) * (pdc - B) + C * ((pdc - B) * (pdc - B));
-    if (!isnan(ac)) ac = R(iv[0]) < ac ? R(iv[0]) : ac;
-    if (pdc < R(iv[3])) ac = R(-1) * fabs(R(iv[8]));
-    if (isnan(ac)) return R(0);                       // .fillna(0.)
-    return ac > R(0) ? ac : R(0);                      // .clip(lower=0.)
+    const double dkn = a + b * exp(cc * am);
+    double dni = (g[G_KNC] - dkn) * g[G_I0];
+    if (g[G_DISCOK] == 0.0 || ghi < 0.0 || dni < 0.0) dni = 0.0;
+    const double dhi = ghi - dni * g[G_COSZ];
+    const double AI = dni * g[G_RDNIX];
+    double sky = dhi * (AI * g[G_RB] + (1.0 - AI) * g[G_TERM2]);
+    sky = sky > 0.0 ? sky : 0.0;
+    const double ground = ghi * g[G_GFAC];
+    double poa_direct = dni * g[G_COSAOI];
+    poa_direct = poa_direct > 0.0 ? poa_direct : 0.0;
+    const double poa_diffuse = sky + ground;
+    const double poa_global = poa_direct + poa_diffuse;
+    // sapm_celltemp, sapm_effective_irradiance, sapm (pvmodel.py:69-77)
+    p = lds_fence(p);
+    const double tcell = poa_global * p->tk + p->temp_air;
+    const double Ee = g[G_F1] * (poa_direct * g[G_F2] + p->fd * poa_diffuse) * 1e-3;
+    const double Bvmpo = p->bvmpo1 + p->nmbvmp * Ee;
+    const double delta = p->nkq * (tcell + 273.15);
+    double logEe;
+    if constexpr (__is_same(LT, decltype(nullptr))) logEe = Ee > 0.0 ? log(Ee) : (Ee == 0.0 ? -INFINITY : NAN);
+    else logEe = log_lds(Ee, lt);
+    const double imp = Ee * (p->impo_c0 + p->impo_c1 * Ee) * (p->aimp0 + p->aimp * tcell);
+    const double dl = delta * logEe;
+    double vmp = p->vmpo + p->c2ns * dl + p->c3ns * (dl * dl) + Bvmpo * (tcell - 25.0);
+    if (!isnan(vmp)) vmp = vmp > 0.0 ? vmp : 0.0;
+    const double pdc = imp * vmp;
+    // snlinverter (pvmodel.py:78): A - B, B, C affine in vmp
+    p = lds_fence(p);
+    const double AB = p->ab0 + p->ab1 * vmp, B = p->b0 + p->b1 * vmp, C = p->c0 + p->c1 * vmp;
+    double ac = (p->paco / AB - C * AB) * (pdc - B) + C * ((pdc - B) * (pdc - B));
+    if (!isnan(ac)) ac = p->paco < ac ? p->paco : ac;
+    if (pdc < p->pso) ac = p->pnt;
+    if (isnan(ac)) return 0.0;                       // .fillna(0.)
+    return ac > 0.0 ? ac : 0.0;                      // .clip(lower=0.)
 }
 
 
@@ -1304,10 +1320,11 @@ __device__ __forceinline__ R meter_w(uint32_t w)
 
 // risky (fp32 only): pv lies in pv_power_f's guard band; the caller recomputes
 // the second in fp64 (pv_fp64_*) and replaces pv and res
-template <typename R>
+// (fp64: p64 / lt as pv_power_d's; the defaults read the kernel arguments and ocml's log)
+template <typename R, typename P64 = decltype(nullptr), typename LT = decltype(nullptr)>
 __device__ __forceinline__ void second_body(const KParams& kp, const PVF& pk, const R* row, uint32_t fl,
                                             const FSamp<R>& fs, bool covered, R z, R meter_in, R& csi, R& pv, R& meter,
-                                            R& res, bool& risky)
+                                            R& res, bool& risky, P64 p64 = nullptr, LT lt = nullptr)
 {
     risky = false;
     const R cloudcover = rinterp_row(fs, S_CC, row, G_HOURF);   // == interp() bit for bit when R = double
@@ -1319,7 +1336,12 @@ __device__ __forceinline__ void second_body(const KParams& kp, const PVF& pk, co
     const R a_clear = rinterp_row(fs, S_CLEAR_DAY, row, G_DAYF), a_cloudy = rinterp_row(fs, S_CLOUDY_HOUR, row, G_HOURF);
     const R n_clear = rinterp_row(fs, S_CLEAR_NOISE, row, G_MINF), n_cloudy = rinterp_row(fs, S_CLOUDY_NOISE, row, G_MINF);
     csi = (covered ? a_clear : a_cloudy) * ((covered ? n_clear : n_cloudy) + eps);
-    if constexpr (sizeof(R) == 8) pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power<R>(kp, row, csi) : R(0);
+    if constexpr (sizeof(R) == 8) {
+        if constexpr (__is_same(P64, decltype(nullptr)))
+            pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power_d(&kp.pv64, row, csi, lt) : R(0);
+        else
+            pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power_d(p64, row, csi, lt) : R(0);
+    }
     else pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power_f(pk, row + G32, csi, (fl & FL_DISCOK) != 0, risky) : 0.0f;
     meter = meter_in;
     res = meter - pv;
