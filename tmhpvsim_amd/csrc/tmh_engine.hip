@@ -1734,10 +1734,23 @@ __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t rs, uint32_t of
 // sampler pairs and does no fp64 work in fp32 mode.
 // 256-thread workgroups: one-wave workgroups (so the SIMDs take expansion waves
 // independently of a walk wave's footprint) measured +5 % alone, no gain beside the walks
+// statistics workgroups of 512 chains (C3 / C4): one histogram flush per 65,536
+// chain-seconds instead of 32,768 (32-bit LDS bins, 16 KB); round 4, same box: C4
+// 2.41 -> 2.51e11 chain-s/s, C3 2.87e11 either way (its expansion 240 -> 235 ms alone)
+#ifndef TMH_EXP_WG_STATS
+#define TMH_EXP_WG_STATS 512
+#endif
 template <typename R, int OUT, bool SITES>
 constexpr int exp_wg()
 {
-    return 256;
+    return OUT == OUT_STATS && !SITES ? TMH_EXP_WG_STATS : 256;
+}
+// the LDS histogram as 16-bit bin pairs when one tile (WG chains x 128 s) cannot fill a
+// 16-bit bin, else one 32-bit word per bin
+template <typename R, int OUT, bool SITES>
+constexpr bool exp_hist_pack()
+{
+    return exp_wg<R, OUT, SITES>() * BLOCK_STEPS <= 32768;
 }
 constexpr int PVF_VGPR = 0;   // leading PVF fields pinned in VGPRs in the fp32 single-site expansion
 // min waves per SIMD (__launch_bounds__) of each expansion instantiation:
@@ -1749,7 +1762,10 @@ constexpr int PVF_VGPR = 0;   // leading PVF fields pinned in VGPRs in the fp32 
 template <typename R, int OUT, bool SITES>
 constexpr int exp_waves()
 {
-    return SITES ? 2 : (sizeof(R) == 8 ? 4 : (OUT == OUT_TRACE3 ? 7 : 6));
+#ifndef TMH_EXP_WAVES_F64
+#define TMH_EXP_WAVES_F64 4
+#endif
+    return SITES ? 2 : (sizeof(R) == 8 ? TMH_EXP_WAVES_F64 : (OUT == OUT_TRACE3 ? 7 : 6));
 }
 // One (128-second block b, chain block cblk) tile of the expansion: one work-item per
 // chain of the block (the expansion's unit of work, below).  The LDS staging areas are
@@ -1763,7 +1779,7 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
                                             const BlockDesc* __restrict__ desc, const SegView& sg,
                                             const TraceView& tr, const StatsView& sv, uint32_t* lds_hist,
                                             uint32_t (*cov_lds)[WGT], R (*min_lds)[WGT], uint4* held_lds,
-                                            const PV64* pv_lds, const double* log_lds_tab)
+                                            const PV64* pv_lds, const double* pv_lds_tab)
 {
     const uint32_t c = cblk * blockDim.x + threadIdx.x;
     const bool live = c < n;
@@ -1955,7 +1971,7 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
                 asm volatile("" : "+v"(pa));
                 const __attribute__((address_space(3))) PV64* p = (const __attribute__((address_space(3))) PV64*)(uintptr_t)pa;
                 second_body<R>(kp, pkv, row, flp, fs, covered, noise_z<R>(un), meter_w<R>(um), csi, pv, meter, res, held,
-                               p, (LdsD*)log_lds_tab);
+                               p, (LdsD*)pv_lds_tab);
             } else {
                 second_body<R>(kp, pkv, row, flp, fs, covered, noise_z<R>(un), meter_w<R>(um), csi, pv, meter, res, held);
             }
@@ -1980,7 +1996,8 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
             row_store(rs_r, voff, res);
             voff += rowb;
         } else if (live) {
-            emit<R, OUT, true>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok, held);
+            emit<R, OUT, exp_hist_pack<R, OUT, SITES>()>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter,
+                                                         res, acc, ok, held);
         }
     };
     // The per-second draws: the meter's and the noise's streams, one Philox block per four
@@ -2040,23 +2057,12 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
 }
 
 
-// Statistics without per-chain sites (C3, C4): a workgroup runs EXP_TILES consecutive
-// 128-s blocks of its chain block (grid x = ceil(blocks / EXP_TILES), y = chain block)
-// and keeps one LDS histogram of 16-bit bin pairs over them, flushed to the device
-// histogram once at its end (plus, after a block, any bin that reached 2^15: a block
-// adds at most 128 x 256 = 2^15 to a bin, so no bin overflows 16 bits) -- a quarter of
-// the device-scope 64-bit atomics of one flush per block (round 3: 2.38 B of HBM
-// writes per chain-second, almost all of them these flushes).  Round 4 measured a
-// persistent grid (the device's resident workgroups looping over all blocks) 8-40 %
-// slower on C3 / C4 than hardware dispatch of one workgroup per tile; a few blocks per
-// workgroup keep the hardware's dynamic balance.
+// Statistics: one tile per workgroup, its LDS histogram flushed to the device histogram
+// by 64-bit atomics at the end.  Round 4 measured workgroups looping over several tiles
+// (one flush per workgroup): a persistent grid 8-40 % slower on C3 / C4, four tiles per
+// workgroup 13 % slower on C3 (the inlined tile loop spills 45 VGPRs instead of 4).
 template <typename R, int OUT, bool SITES>
-constexpr int exp_tiles()
-{
-    return OUT == OUT_STATS && !SITES ? 4 : 1;
-}
-template <typename R, int OUT, bool SITES>
-__global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0,
+__global__ __launch_bounds__((exp_wg<R, OUT, SITES>()), (exp_waves<R, OUT, SITES>())) void expand_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0,
                                                      uint32_t n, int64_t W0, uint32_t nsteps, int64_t utc0,
                                                      const double* __restrict__ tab64,
                                                      const float* __restrict__ tab32,
@@ -2071,50 +2077,36 @@ __global__ __launch_bounds__(256, (exp_waves<R, OUT, SITES>())) void expand_kern
     __shared__ uint32_t cov_lds[4][WGT];
     __shared__ R min_lds[4][WGT];   // minute boundaries mA, mA + 1 of the block: cloudy, clear noise
     __shared__ uint4 held_lds[WGT];
-    // fp64: the PV constants and log_lds's table (one copy per workgroup)
+    // fp64: the PV constants and the log / exp table (one copy per workgroup)
     __shared__ PV64 pv_lds[1];   // (176 + 16 bytes in the fp32 kernels: unused)
-    __shared__ __attribute__((aligned(16))) double log_tab[sizeof(R) == 8 ? 2 * LOG_TAB : 2];
+    __shared__ __attribute__((aligned(16))) double pv_tab[sizeof(R) == 8 ? PV_TAB : 2];
     if constexpr (sizeof(R) == 8) {
         if (threadIdx.x < PV64_N) reinterpret_cast<double*>(pv_lds)[threadIdx.x] = reinterpret_cast<const double*>(&kp.pv64)[threadIdx.x];
-        log_table_fill(log_tab, threadIdx.x);
+        for (uint32_t i = threadIdx.x; i < PV_TAB; i += blockDim.x) pv_tab[i] = g_pv_tab[i];
         __syncthreads();
     }
-    const uint32_t nw = (sv.n_bins + 1) / 2;   // 16-bit bin pairs
+    constexpr bool PACK = exp_hist_pack<R, OUT, SITES>();
+    const uint32_t nw = PACK ? (sv.n_bins + 1) / 2 : sv.n_bins;   // 16-bit bin pairs, or bins
     if (sv.hist) {
         for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) lds_hist[i] = 0;
         __syncthreads();
     }
     auto tile = [&](uint32_t b, uint32_t cblk) __attribute__((always_inline)) {
         expand_tile<R, OUT, SITES, WGT>(b, cblk, kp, dp, st, chain0, n, W0, nsteps, utc0, tab64, tab32, sun, events,
-                                        n_events, desc, sg, tr, sv, lds_hist, cov_lds, min_lds, held_lds, pv_lds, log_tab);
+                                        n_events, desc, sg, tr, sv, lds_hist, cov_lds, min_lds, held_lds, pv_lds, pv_tab);
     };
-    if constexpr (exp_tiles<R, OUT, SITES>() > 1) {
-        constexpr uint32_t KT = exp_tiles<R, OUT, SITES>();
-        const uint32_t b1 = min((blockIdx.x + 1) * KT, sg.nblk);
-        for (uint32_t b = blockIdx.x * KT; b < b1; ++b) {
-            tile(b, blockIdx.y);
-            if (sv.hist) {   // bins at 2^15 or more go to the device histogram before the next tile
-                __syncthreads();
-                for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) {
-                    const uint32_t w = lds_hist[i], lo = w & 0x8000u ? w & 0xFFFFu : 0u, hi = w & 0x80000000u ? w >> 16 : 0u;
-                    if (lo | hi) {
-                        lds_hist[i] = w - (lo | (hi << 16));
-                        if (lo) atomicAdd((unsigned long long*)&sv.hist[2 * i], (unsigned long long)lo);
-                        if (hi) atomicAdd((unsigned long long*)&sv.hist[2 * i + 1], (unsigned long long)hi);
-                    }
-                }
-                __syncthreads();
-            }
-        }
-    } else {
-        tile(blockIdx.x, blockIdx.y);   // grid: x = time block, y = chain block
-    }
+    tile(blockIdx.x, blockIdx.y);   // grid: x = time block, y = chain block
     if (sv.hist) {
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) {
-            const uint32_t w = lds_hist[i], lo = w & 0xFFFFu, hi = w >> 16;
-            if (lo) atomicAdd((unsigned long long*)&sv.hist[2 * i], (unsigned long long)lo);
-            if (hi) atomicAdd((unsigned long long*)&sv.hist[2 * i + 1], (unsigned long long)hi);   // hi = 0 past n_bins
+            const uint32_t w = lds_hist[i];
+            if constexpr (PACK) {
+                const uint32_t lo = w & 0xFFFFu, hi = w >> 16;
+                if (lo) atomicAdd((unsigned long long*)&sv.hist[2 * i], (unsigned long long)lo);
+                if (hi) atomicAdd((unsigned long long*)&sv.hist[2 * i + 1], (unsigned long long)hi);   // hi = 0 past n_bins
+            } else if (w) {
+                atomicAdd((unsigned long long*)&sv.hist[i], (unsigned long long)w);
+            }
         }
     }
 }
@@ -2770,6 +2762,21 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
     d.fb_loc = p->shapes[fb][0];
     d.fb_bin = fb;
     d.markov = p->cc_mode == TMH_CC_MARKOV;
+    {   // log_tab's / exp_tab's table on this device (the same host values for every engine)
+        double lt[PV_TAB];
+        for (int i = 0; i < LOG_TAB; ++i) {
+            const double c = 1.0 + (i + 0.5) * (1.0 / LOG_TAB);
+            lt[2 * i] = 1.0 / c;
+            lt[2 * i + 1] = std::log(c);
+        }
+        for (int i = 0; i < EXP_TAB; ++i) lt[EXP_OFF + i] = std::exp2(i * (1.0 / EXP_TAB));
+        int rc = hip_check(hipSetDevice(device), "hipSetDevice");
+        if (!rc) rc = hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_pv_tab), lt, sizeof lt), "hipMemcpyToSymbol(g_pv_tab)");
+        if (rc) {
+            delete e;
+            return rc;
+        }
+    }
     e->device = device;
     e->path = path;
     e->local_step0 = clock->local0;
@@ -3118,18 +3125,17 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     const int out = (no_stats && tv.pv && tv.meter && tv.residual && !tv.csi && !tv.covered) ? OUT_TRACE3
                     : (!tv.pv && !tv.meter && !tv.residual && !tv.csi && !tv.covered) ? OUT_STATS
                                                                                       : OUT_ANY;
-    const size_t lds_exp = stats && stats->hist ? (size_t)((stats->n_bins + 1) / 2) * 4 : 0;   // 16-bit bin pairs
-    // x = time blocks (EXP_TILES per workgroup), y = chain blocks
-    auto exp_grid = [&](uint32_t wg, uint32_t kt) {
-        return dim3((sg.nblk + kt - 1) / kt, (n_chains + wg - 1) / wg);
-    };
+    const size_t hist_bins = stats && stats->hist ? stats->n_bins : 0;
+    // x = time blocks, y = chain blocks; LDS: the histogram (16-bit bin pairs or bins)
+    auto exp_grid = [&](uint32_t wg) { return dim3(sg.nblk, (n_chains + wg - 1) / wg); };
+    auto exp_lds = [&](bool pack) { return pack ? (hist_bins + 1) / 2 * 4 : hist_bins * 4; };
     if (out == OUT_TRACE3 && tv.ld * (f64 ? 8u : 4u) * BLOCK_STEPS >= (1ull << 31))   // one block's rows: one buffer range
         return fail(TMH_E_INVAL, "trace ld %llu too large (a 128-step block of rows must stay under 2 GiB)",
                     (unsigned long long)tv.ld);
 #define LAUNCH(R, O, S)                                                                                            \
     hipLaunchKernelGGL((expand_kernel<R, O, S>),                                                                   \
-                       exp_grid(exp_wg<R, O, S>(), exp_tiles<R, O, S>()),                                      \
-                       dim3(exp_wg<R, O, S>()), lds_exp, s, eng->kp, eng->dp, v, chain0, n_chains, step0, n_steps,   \
+                       exp_grid(exp_wg<R, O, S>()), dim3(exp_wg<R, O, S>()), exp_lds(exp_hist_pack<R, O, S>()), s, \
+                       eng->kp, eng->dp, v, chain0, n_chains, step0, n_steps,   \
                        utc0, pv.tab64, pv.tab32, pv.sun, pv.events, pv.n_events, pv.desc, sg, tv, sv)
     if (eng->kp.sites) {   // per-chain sites: one instantiation per precision, any output
         if (f64) LAUNCH(double, OUT_ANY, true);

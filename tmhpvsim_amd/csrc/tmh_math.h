@@ -364,30 +364,27 @@ __device__ __noinline__ double al_ppf(double y, double kappa)
 // fp64 pow out of line (cloud lengths, cloud_cover_binary.py:40): keeps callers' registers low
 __device__ __noinline__ double pow_d(double x, double y) { return pow(x, y); }
 
-// ---- fp64 natural log from an LDS table (the PV chain's log(Ee), pv_power_d) ----
+// ---- fp64 natural log from a table (the PV chain's log(Ee), pv_power_d) ----
 // x = 2^e m, m in [1, 2); c_i = 1 + (i + 1/2) / 128 for the top 7 bits i of m's
 // mantissa, u = m / c_i - 1 (|u| <= 2^-8, as fma(m, 1 / c_i, -1)), and
 // log x = e ln 2 + log c_i + log1p(u) with log1p to u^7 / 7 (truncation < 2^-67).
-// Absolute error a few 1e-16 (the rounding of e ln 2, 1 / c_i and log c_i): the PV
-// chain needs 1e-12 relative.  13 VALU instead of ocml log's ~90.  Zero, negative,
-// NaN, infinite and subnormal x take ocml's log (and its -inf / NaN).
+// Absolute error a few 1e-16 (the rounding of e ln 2, 1 / c_i and log c_i; numpy
+// emulation over 45,000 x in [1e-8, 2]: at most one ulp of the result): the PV chain
+// needs 1e-12 relative.  13 VALU instead of ocml log's ~90.  Zero, negative, NaN,
+// infinite and subnormal x take ocml's log (and its -inf / NaN).
+// g_pv_tab: t[2 i] = 1 / c_i, t[2 i + 1] = log c_i, then exp_tab's 2^(i / 64) at
+// t[EXP_OFF + i]; written once per engine from the host (tmh_engine_create); every fp64
+// PV evaluation reads these same values (the expansion from an LDS copy), so the kernels
+// agree bit for bit.
+constexpr int LOG_TAB = 128, EXP_TAB = 64, EXP_OFF = 2 * LOG_TAB, PV_TAB = EXP_OFF + EXP_TAB;
+__device__ double g_pv_tab[PV_TAB];
 typedef __attribute__((address_space(3))) const double LdsD;
-constexpr int LOG_TAB = 128;
-
-// the table: t[2 i] = 1 / c_i, t[2 i + 1] = log c_i (one thread per entry)
-__device__ __forceinline__ void log_table_fill(double* t, uint32_t i)
-{
-    if (i < (uint32_t)LOG_TAB) {
-        const double c = 1.0 + (i + 0.5) * (1.0 / LOG_TAB);
-        t[2 * i] = 1.0 / c;
-        t[2 * i + 1] = log(c);
-    }
-}
 
 // (out of line: inlined, its constants would be hoisted into registers across the caller's loop)
 __device__ __noinline__ double log_edge(double x) { return x > 0.0 ? log(x) : (x == 0.0 ? -INFINITY : NAN); }
 
-__device__ __forceinline__ double log_lds(double x, LdsD* t)
+template <typename TP>   // TP: LdsD* (an LDS copy) or const double* (g_pv_tab)
+__device__ __forceinline__ double log_tab(double x, TP t)
 {
     if (__builtin_expect(!(x >= 0x1p-1022) || x == INFINITY, 0)) return log_edge(x);
     const uint64_t bits = (uint64_t)__double_as_longlong(x);
@@ -403,6 +400,30 @@ __device__ __forceinline__ double log_lds(double x, LdsD* t)
     h = fma(h, u, 1.0 / 3.0);
     h = fma(h, u, -1.0 / 2.0);
     return fma((double)e, 0.693147180559945309417, t[2 * i + 1]) + fma(u * u, h, u);
+}
+
+// ---- fp64 exp from the same table (DISC's exp(c am), pv_power_d) ----
+// x = (k / 64) ln 2 + r, k = rint(64 x / ln 2), |r| <= ln 2 / 128 (r from a two-part
+// ln 2 / 64 whose high part times k is exact for |k| < 2^16); exp x = 2^(k >> 6)
+// 2^((k & 63) / 64) p(r), p to r^6 / 720.  Numpy emulation over 100,000 x in [-40, 3]:
+// at most 1.5 ulp.  14 VALU instead of ocml exp's ~31; |x| >= 700 and NaN take ocml's.
+__device__ __noinline__ double exp_edge(double x) { return exp(x); }
+
+template <typename TP>
+__device__ __forceinline__ double exp_tab(double x, TP t)
+{
+    if (__builtin_expect(!(fabs(x) < 700.0), 0)) return exp_edge(x);
+    const double kf = rint(x * 92.332482616893656768);   // 64 / ln 2
+    double r = fma(-kf, 0x1.62e42fefa0000p-7, x);
+    r = fma(-kf, 2.572804640231345e-14, r);
+    double p = fma(r, 1.0 / 720.0, 1.0 / 120.0);
+    p = fma(p, r, 1.0 / 24.0);
+    p = fma(p, r, 1.0 / 6.0);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    const int k = (int)kf;
+    return ldexp(t[EXP_OFF + (k & (EXP_TAB - 1))] * p, k >> 6);
 }
 
 }  // namespace tmh

@@ -1085,9 +1085,10 @@ __device__ __forceinline__ uint32_t lane_flags(uint32_t fl, bool night, const R*
 // ------------------------------------------------------------ PV (per chain-second)
 // pvmodel.py:53-80 on the precomputed geometry row, fp64.  `p` points at the folded
 // constants (PV64: in the kernel arguments, or an LDS copy the expansion re-reads each
-// second instead of holding 22 doubles in SGPRs across its loop); `lt` is the LDS table
-// of log_lds, or nullptr for ocml's log.  kt and AI multiply by the row's GHI_cs / I0h
-// and 1 / dni_extra; the SAPM and SNL constants are PV64's affine forms.
+// second instead of holding 22 doubles in SGPRs across its loop); `lt` is an LDS copy of
+// the table of log_tab / exp_tab, or nullptr for the table itself (g_pv_tab).  kt and AI
+// multiply by the row's GHI_cs / I0h and 1 / dni_extra; the SAPM and SNL constants are
+// PV64's affine forms.
 // an LDS pointer re-laundered (its loads cannot move above this point, so the
 // constants are read shortly before their use instead of all at the second's start)
 template <typename PP>
@@ -1120,7 +1121,10 @@ __device__ __forceinline__ double pv_power_d(PP p, const double* g, double csi, 
         b = 41.4 - 118.5 * kt + 66.05 * kt2 + 31.9 * kt3;
         cc = -47.01 + 184.2 * kt - 222.0 * kt2 + 73.81 * kt3;
     }
-    const double dkn = a + b * exp(cc * am);
+    double ex;
+    if constexpr (__is_same(LT, decltype(nullptr))) ex = exp_tab(cc * am, (const double*)g_pv_tab);
+    else ex = exp_tab(cc * am, lt);
+    const double dkn = a + b * ex;
     double dni = (g[G_KNC] - dkn) * g[G_I0];
     if (g[G_DISCOK] == 0.0 || ghi < 0.0 || dni < 0.0) dni = 0.0;
     const double dhi = ghi - dni * g[G_COSZ];
@@ -1139,8 +1143,8 @@ __device__ __forceinline__ double pv_power_d(PP p, const double* g, double csi, 
     const double Bvmpo = p->bvmpo1 + p->nmbvmp * Ee;
     const double delta = p->nkq * (tcell + 273.15);
     double logEe;
-    if constexpr (__is_same(LT, decltype(nullptr))) logEe = Ee > 0.0 ? log(Ee) : (Ee == 0.0 ? -INFINITY : NAN);
-    else logEe = log_lds(Ee, lt);
+    if constexpr (__is_same(LT, decltype(nullptr))) logEe = log_tab(Ee, (const double*)g_pv_tab);
+    else logEe = log_tab(Ee, lt);
     const double imp = Ee * (p->impo_c0 + p->impo_c1 * Ee) * (p->aimp0 + p->aimp * tcell);
     const double dl = delta * logEe;
     double vmp = p->vmpo + p->c2ns * dl + p->c3ns * (dl * dl) + Bvmpo * (tcell - 25.0);
