@@ -1970,8 +1970,8 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
                 uint32_t pa = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) PV64*)pv_lds;
                 asm volatile("" : "+v"(pa));
                 const __attribute__((address_space(3))) PV64* p = (const __attribute__((address_space(3))) PV64*)(uintptr_t)pa;
-                second_body<R>(kp, pkv, row, flp, fs, covered, noise_z<R>(un), meter_w<R>(um), csi, pv, meter, res, held,
-                               p, (LdsD*)pv_lds_tab);
+                second_body<R>(kp, pkv, row, flp, fs, covered, ndtri64(un, (LdsD*)pv_lds_tab), meter_w<R>(um), csi, pv,
+                               meter, res, held, p, (LdsD*)pv_lds_tab);
             } else {
                 second_body<R>(kp, pkv, row, flp, fs, covered, noise_z<R>(un), meter_w<R>(um), csi, pv, meter, res, held);
             }
@@ -2762,7 +2762,7 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
     d.fb_loc = p->shapes[fb][0];
     d.fb_bin = fb;
     d.markov = p->cc_mode == TMH_CC_MARKOV;
-    {   // log_tab's / exp_tab's table on this device (the same host values for every engine)
+    {   // the table of log_tab / exp_tab / ndtri64 on this device (the same host values for every engine)
         double lt[PV_TAB];
         for (int i = 0; i < LOG_TAB; ++i) {
             const double c = 1.0 + (i + 0.5) * (1.0 / LOG_TAB);
@@ -2770,6 +2770,7 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
             lt[2 * i + 1] = std::log(c);
         }
         for (int i = 0; i < EXP_TAB; ++i) lt[EXP_OFF + i] = std::exp2(i * (1.0 / EXP_TAB));
+        for (int i = 0; i <= NDTRI_DEG; ++i) lt[NDTRI_OFF + i] = NDTRI_COEF[i];
         int rc = hip_check(hipSetDevice(device), "hipSetDevice");
         if (!rc) rc = hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_pv_tab), lt, sizeof lt), "hipMemcpyToSymbol(g_pv_tab)");
         if (rc) {

@@ -373,10 +373,12 @@ __device__ __noinline__ double pow_d(double x, double y) { return pow(x, y); }
 // needs 1e-12 relative.  13 VALU instead of ocml log's ~90.  Zero, negative, NaN,
 // infinite and subnormal x take ocml's log (and its -inf / NaN).
 // g_pv_tab: t[2 i] = 1 / c_i, t[2 i + 1] = log c_i, then exp_tab's 2^(i / 64) at
-// t[EXP_OFF + i]; written once per engine from the host (tmh_engine_create); every fp64
+// t[EXP_OFF + i], then ndtri64's coefficients at t[NDTRI_OFF + k] (degree k); written
+// once per engine from the host (tmh_engine_create); every fp64
 // PV evaluation reads these same values (the expansion from an LDS copy), so the kernels
 // agree bit for bit.
-constexpr int LOG_TAB = 128, EXP_TAB = 64, EXP_OFF = 2 * LOG_TAB, PV_TAB = EXP_OFF + EXP_TAB;
+constexpr int LOG_TAB = 128, EXP_TAB = 64, EXP_OFF = 2 * LOG_TAB, NDTRI_OFF = EXP_OFF + EXP_TAB, NDTRI_DEG = 22,
+              PV_TAB = NDTRI_OFF + NDTRI_DEG + 1;
 __device__ double g_pv_tab[PV_TAB];
 typedef __attribute__((address_space(3))) const double LdsD;
 
@@ -400,6 +402,68 @@ __device__ __forceinline__ double log_tab(double x, TP t)
     h = fma(h, u, 1.0 / 3.0);
     h = fma(h, u, -1.0 / 2.0);
     return fma((double)e, 0.693147180559945309417, t[2 * i + 1]) + fma(u * u, h, u);
+}
+
+// ---- fp64 normal quantile of a 32-bit word (the per-second noise, noise_z<double>) ----
+// p = (w + 1/2) 2^-32, x = 2p - 1 (exact), ndtri(p) = sqrt(2) erfinv(x) = sqrt(2) x f(w')
+// with w' = -log(1 - x^2) = -log(4 p (1 - p)) and, for w' < 6.25 (p in ~[5e-4, 1 - 5e-4],
+// 99.9 % of the draws), f a degree-22 polynomial in w' - 3.125 (Giles' form, "Approximating
+// the erfinv function", refitted: scripts/fit_ndtri_f64.py, <= 4.2e-16 relative in an fp64
+// Horner evaluation); the rest take ocml's quantile out of line (ndtri_fast).  About 40 VALU
+// instead of ocml's ~150 and a call.  The coefficients come from the table (an LDS copy in
+// the expansion, read through `tab_fence` in chunks so they are loaded shortly before use).
+constexpr double NDTRI_COEF[NDTRI_DEG + 1] = {   // degree 0 first (the host copies them into g_pv_tab)
+    1.6536545626831027,
+    0.2401581824255897,
+    -0.006033670871427011,
+    -0.0007407025341669402,
+    0.0001867342080212427,
+    -1.3882523361276876e-05,
+    -1.3654691796592068e-06,
+    4.2347877672780653e-07,
+    -2.907038666019143e-08,
+    -4.112633104297614e-09,
+    1.0512202440121784e-09,
+    -5.4154417754696635e-11,
+    -1.2977505202014966e-11,
+    2.6335724924608484e-12,
+    -8.106594456438496e-14,
+    -4.0554139746886e-14,
+    6.581955305929239e-15,
+    2.166994626283574e-17,
+    -1.290702354613073e-16,
+    1.1125794759379464e-17,
+    1.1027771591500033e-18,
+    -1.6787330615256773e-19,
+    -2.362369698566107e-22};
+
+template <typename TP>
+__device__ __forceinline__ TP tab_fence(TP t)
+{
+    if constexpr (__is_same(TP, const double*)) return t;
+    else {
+        uint32_t a = (uint32_t)(uintptr_t)t;
+        asm volatile("" : "+v"(a));
+        return (TP)(uintptr_t)a;
+    }
+}
+
+template <typename TP>
+__device__ __forceinline__ double ndtri64(uint32_t w, TP t)
+{
+    const double p = ((double)w + 0.5) * 0x1p-32;
+    const double x = 2.0 * p - 1.0;
+    const double ww = -log_tab(4.0 * p * (1.0 - p), t);
+    if (__builtin_expect(!(ww < 6.25), 0)) return ndtri_fast(p);
+    const double u = ww - 3.125;
+    t = tab_fence(t);
+    double f = t[NDTRI_OFF + 22];
+#pragma unroll
+    for (int k = 21; k >= 0; --k) {
+        if (k % 6 == 5) t = tab_fence(t);
+        f = fma(f, u, t[NDTRI_OFF + k]);
+    }
+    return (1.4142135623730950488 * x) * f;
 }
 
 // ---- fp64 exp from the same table (DISC's exp(c am), pv_power_d) ----

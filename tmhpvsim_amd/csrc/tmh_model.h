@@ -1307,8 +1307,8 @@ __device__ __forceinline__ R rinterp_row(const FSamp<R>& f, int k, const R* row,
 template <typename R>
 __device__ __forceinline__ R noise_z(uint32_t w)
 {
-    // fp64: ocml's ncdfinv alone, within 7e-16 of the exact quantile, far inside the fp64 bar
-    if constexpr (sizeof(R) == 8) return ndtri_fast(u32d(w));
+    // fp64: ndtri64 (<= ~1e-15 relative, far inside the fp64 bar)
+    if constexpr (sizeof(R) == 8) return ndtri64(w, (const double*)g_pv_tab);
     else return ndtri_w(w);
 }
 
