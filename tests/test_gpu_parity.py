@@ -68,6 +68,19 @@ def test_probe_math():
     w = np.random.default_rng(1).integers(0, 2 ** 32, 20000, dtype=np.uint64)
     u32 = (w.astype(np.float64) + 0.5) * 2.0 ** -32            # the fp64 per-second noise's uniforms
     np.testing.assert_allclose(probe(8, 0, u32), O.ndtri(u32), rtol=2e-15)
+    # the fp64 PV chain's table functions (round 4): the noise quantile of the 32-bit word
+    # itself (refitted erfinv polynomial, ocml's beyond p ~ 5e-4), the word range's extremes
+    # included; log and exp over the ranges the PV chain feeds them (Ee, DISC's c am)
+    wx = np.concatenate([w, [0, 1, 2 ** 31 - 1, 2 ** 31, 2 ** 32 - 2, 2 ** 32 - 1]]).astype(np.float64)
+    ux = (wx + 0.5) * 2.0 ** -32
+    np.testing.assert_allclose(probe(11, 0, wx), O.ndtri(ux), rtol=2e-15)
+    xl = np.concatenate([10.0 ** np.random.default_rng(2).uniform(-12, 0.5, 20000), [1.0, 0.5, 2.0, 1 - 2 ** -52]])
+    np.testing.assert_allclose(probe(12, 0, xl), np.log(xl), rtol=0, atol=4e-15)
+    edge = probe(12, 0, np.array([0.0, -1.0, np.nan, np.inf, 5e-324]))
+    np.testing.assert_array_equal(edge[:4], [-np.inf, np.nan, np.nan, np.inf])
+    np.testing.assert_allclose(edge[4], np.log(5e-324), rtol=1e-15)
+    xe = np.concatenate([np.random.default_rng(3).uniform(-45, 5, 20000), [0.0, -700.5, 710.0]])
+    np.testing.assert_allclose(probe(13, 0, xe), np.exp(xe), rtol=5e-16, atol=0)
     # pv_power_f's final clamp relies on v_med3_f32(NaN, 0, Paco) = 0 (min3 on a NaN operand)
     x = np.array([np.nan, -5.0, 0.5, 3000.0, 1e9])
     np.testing.assert_array_equal(probe(9, 2500.0, x), [0.0, 0.0, 0.5, 2500.0, 2500.0])

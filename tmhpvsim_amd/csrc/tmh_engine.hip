@@ -2332,6 +2332,10 @@ __global__ void probe_kernel(int fn, double a, const double* x, double* out, uin
         case 7: v = readlane_f64(x[i], 63); break;
         case 9: v = (double)__builtin_amdgcn_fmed3f((float)x[i], 0.0f, (float)a); break;   // pv_power_f's final clamp
         case 10: v = (double)__builtin_amdgcn_fmed3f((float)x[i], -INFINITY, (float)a); break;   // its min(csi, csimax)
+        // the fp64 PV chain's table functions (g_pv_tab): the noise quantile of a 32-bit word, log, exp
+        case 11: v = ndtri64((uint32_t)x[i], (const double*)g_pv_tab); break;
+        case 12: v = log_tab(x[i], (const double*)g_pv_tab); break;
+        case 13: v = exp_tab(x[i], (const double*)g_pv_tab); break;
         default: v = NAN;
     }
     out[i] = v;
@@ -2635,6 +2639,22 @@ size_t tmh_engine_scratch_bytes(const struct tmh_engine* eng, uint32_t n_chains,
     return scratch_layout(n_chains, n_steps, nullptr, nullptr, tmh_engine_scratch_rbytes(eng));
 }
 
+// the table of log_tab / exp_tab / ndtri64 (g_pv_tab) on `device`: the same host values
+// for every engine and process, so every kernel's fp64 PV agrees bit for bit
+static int pv_tab_upload(int device)
+{
+    double lt[PV_TAB];
+    for (int i = 0; i < LOG_TAB; ++i) {
+        const double c = 1.0 + (i + 0.5) * (1.0 / LOG_TAB);
+        lt[2 * i] = 1.0 / c;
+        lt[2 * i + 1] = std::log(c);
+    }
+    for (int i = 0; i < EXP_TAB; ++i) lt[EXP_OFF + i] = std::exp2(i * (1.0 / EXP_TAB));
+    for (int i = 0; i <= NDTRI_DEG; ++i) lt[NDTRI_OFF + i] = NDTRI_COEF[i];
+    if (int rc = hip_check(hipSetDevice(device), "hipSetDevice")) return rc;
+    return hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_pv_tab), lt, sizeof lt), "hipMemcpyToSymbol(g_pv_tab)");
+}
+
 int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, struct tmh_engine** out)
 {
     if (!p || !clock || !out) return fail(TMH_E_INVAL, "NULL argument to tmh_engine_create");
@@ -2762,21 +2782,9 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
     d.fb_loc = p->shapes[fb][0];
     d.fb_bin = fb;
     d.markov = p->cc_mode == TMH_CC_MARKOV;
-    {   // the table of log_tab / exp_tab / ndtri64 on this device (the same host values for every engine)
-        double lt[PV_TAB];
-        for (int i = 0; i < LOG_TAB; ++i) {
-            const double c = 1.0 + (i + 0.5) * (1.0 / LOG_TAB);
-            lt[2 * i] = 1.0 / c;
-            lt[2 * i + 1] = std::log(c);
-        }
-        for (int i = 0; i < EXP_TAB; ++i) lt[EXP_OFF + i] = std::exp2(i * (1.0 / EXP_TAB));
-        for (int i = 0; i <= NDTRI_DEG; ++i) lt[NDTRI_OFF + i] = NDTRI_COEF[i];
-        int rc = hip_check(hipSetDevice(device), "hipSetDevice");
-        if (!rc) rc = hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_pv_tab), lt, sizeof lt), "hipMemcpyToSymbol(g_pv_tab)");
-        if (rc) {
-            delete e;
-            return rc;
-        }
+    if (int rc = pv_tab_upload(device)) {
+        delete e;
+        return rc;
     }
     e->device = device;
     e->path = path;
@@ -3262,6 +3270,11 @@ int tmh_debug_walk_prof(unsigned long long* host, uint32_t waves)
 
 int tmh_probe(int fn, double a, const double* x, double* out, uint32_t n, void* stream)
 {
+    if (fn >= 11 && fn <= 13) {   // the table functions need the table on the current device
+        int dev = 0;
+        if (int rc = hip_check(hipGetDevice(&dev), "hipGetDevice")) return rc;
+        if (int rc = pv_tab_upload(dev)) return rc;
+    }
     if (!x || !out) return fail(TMH_E_INVAL, "NULL probe buffers");
     if (n == 0) return TMH_OK;
     hipLaunchKernelGGL(probe_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, fn, a, x, out, n);
