@@ -27,9 +27,10 @@ if [ "$WHAT" = c2 ]; then
 else
   bash scripts/pmc_workload.sh ${TAG}_c3 c3 1048576 86400 fp32 stats faithful -- --workload c3 --steps 1 --warmup 1 || exit 1
   bash scripts/pmc_workload.sh ${TAG}_c5 c5 65536 86400 fp32 stats markov compact=1 -- --workload c5 --steps 1 --warmup 1 || exit 1
-  PMC_PASS_TIMEOUT=240 bash scripts/pmc_workload.sh ${TAG}_c4 c4 16384 86400 fp32 stats faithful -- --workload c4 --steps 1 --warmup 1 || exit 1
+  C4WIN=$(python3 -c "from tmhpvsim_amd.pipeline import pipeline_defaults as d; print(d('c4').window)")
+  PMC_PASS_TIMEOUT=240 bash scripts/pmc_workload.sh ${TAG}_c4 c4 16384 $C4WIN fp32 stats faithful -- --workload c4 --steps 1 --warmup 1 || exit 1
   cp gpurun_out/pmc_kernels.json profiles/pmc_kernels.json
-  for wl in "c3 --steps 4 --warmup 1" "c4 --steps 2 --warmup 1" "c5 --steps 2 --warmup 1"; do
+  for wl in "c3 --steps 4 --warmup 1" "c4 --steps 6 --warmup 1" "c5 --steps 3 --warmup 1"; do
     set -- $wl
     timeout -k 10 600 python -u bench.py --workload $wl > gpurun_out/bench_${TAG}_$1.json 2> gpurun_out/bench_${TAG}_$1.err || exit 1
     cat gpurun_out/bench_${TAG}_$1.json

@@ -1949,7 +1949,8 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
         const bool covered = (cov_w >> (jb & 31)) & 1u;
         uint32_t flp = fl;
         if constexpr (SITES) {   // this chain's own site: geometry per chain-second (none in a night block)
-            flp = lane_flags(fl, blk_night || lane_row<R>(ls, sun + (size_t)j * SUN_W, kp.module, row), row);
+            flp = lane_flags(fl, blk_night || lane_row<R>(ls, sun + (size_t)j * SUN_W, kp.module, row,
+                                                          (LdsD*)pv_lds_tab), row);
         }
         R csi, pv, meter, res;
         bool held = false;   // fp32: PV in a guard band, recomputed in fp64 by fixup_kernel
@@ -2077,10 +2078,10 @@ __global__ __launch_bounds__((exp_wg<R, OUT, SITES>()), (exp_waves<R, OUT, SITES
     __shared__ uint32_t cov_lds[4][WGT];
     __shared__ R min_lds[4][WGT];   // minute boundaries mA, mA + 1 of the block: cloudy, clear noise
     __shared__ uint4 held_lds[WGT];
-    // fp64: the PV constants and the log / exp table (one copy per workgroup)
+    // fp64: the PV constants; fp64 and per-chain sites: the log / exp table (one copy per workgroup)
     __shared__ PV64 pv_lds[1];   // (176 + 16 bytes in the fp32 kernels: unused)
-    __shared__ __attribute__((aligned(16))) double pv_tab[sizeof(R) == 8 ? PV_TAB : 2];
-    if constexpr (sizeof(R) == 8) {
+    __shared__ __attribute__((aligned(16))) double pv_tab[sizeof(R) == 8 || SITES ? PV_TAB : 2];
+    if constexpr (sizeof(R) == 8 || SITES) {
         if (threadIdx.x < PV64_N) reinterpret_cast<double*>(pv_lds)[threadIdx.x] = reinterpret_cast<const double*>(&kp.pv64)[threadIdx.x];
         for (uint32_t i = threadIdx.x; i < PV_TAB; i += blockDim.x) pv_tab[i] = g_pv_tab[i];
         __syncthreads();

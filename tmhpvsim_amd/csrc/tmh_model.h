@@ -874,7 +874,9 @@ __device__ __forceinline__ void sincos_pi(double x, double* sp, double* cp)
 
 // x^y for x > 0 as exp2(y log2 x): within a few ulps of pow (|y log2 x| < 16 here),
 // about half of ocml's pow (its extra-precise log and special cases)
-__device__ __forceinline__ double pow_pos(double x, double y) { return exp2(y * log2(x)); }
+// x^y for x > 0 from the PV table's log and exp (a few 1e-16 relative for the airmass powers)
+template <typename TP>
+__device__ __forceinline__ double pow_pos(double x, double y, TP t) { return exp_tab(y * log_tab(x, t), t); }
 
 // per-site constants of the geometry (site row: lat, lon, altitude, tilt, azimuth, albedo)
 struct SiteK {
@@ -907,9 +909,11 @@ __device__ __forceinline__ SiteK site_k(const double* site)
 
 // geometry row fields G_COSZ..G_LAST of one site and step (fp64); returns true
 // when the clear-sky GHI is 0 (pv = 0 whatever the csi).  FULL = false stops
-// there at night (the per-chain-second path); FULL fills every field.
-template <bool FULL, bool F32 = false>
-__device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, double tl, const double* m, double* g)
+// there at night (the per-chain-second path); FULL fills every field.  t: the PV table
+// (g_pv_tab, or an LDS copy of it) for the airmass powers.
+template <bool FULL, bool F32 = false, typename TP = const double*>
+__device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, double tl, const double* m, double* g,
+                                          TP t = (const double*)g_pv_tab)
 {
     // fmod(x, 1440) for x in (-1440, 2880): one exact subtraction (Sterbenz) or none
     double tst = sun[SUN_MIN] + sun[SUN_EOT] + 4.0 * k.lon;
@@ -966,7 +970,7 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     // polynomial (factors of GHI_cs and of the effective irradiance): fp32 power, ~2e-7
     // relative; DISC's airmass (amd, below, ill-conditioned at low sun) stays fp64
     const double am_rel = azen <= 90.0 ? 1.0 / (czs + 0.50572 * (F32 ? (double)__powf((float)(6.07995 + (90.0 - azen)), -1.6364f)
-                                                                      : pow_pos(6.07995 + (90.0 - azen), -1.6364)))
+                                                                      : pow_pos(6.07995 + (90.0 - azen), -1.6364, t)))
                                        : NAN;
     const double am_abs = am_rel * k.pres / 101325.0;
     const double cz = czs > 0.0 ? czs : 0.0;
@@ -977,7 +981,7 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     const double I0 = sun[SUN_I0];
     g[G_I0] = I0;                                                              // disc (pvmodel.py:63)
     g[G_I0H] = I0 * (ct > 0.065 ? ct : 0.065);
-    double amd = zen <= 90.0 ? 1.0 / (ct + 0.15 * pow_pos(93.885 - zen, -1.253)) : NAN;
+    double amd = zen <= 90.0 ? 1.0 / (ct + 0.15 * pow_pos(93.885 - zen, -1.253, t)) : NAN;
     amd = amd * 101325.0 / 101325.0;
     amd = amd < 12.0 ? amd : (isnan(amd) ? amd : 12.0);
     g[G_AM] = amd;
@@ -1053,8 +1057,9 @@ struct LaneSite {
 };
 
 // the geometry of lane site `ls` at the plan's sun row; true = night
-template <typename R>
-__device__ __forceinline__ bool lane_row(LaneSite& ls, const double* sun, const double* module, R* row)
+template <typename R, typename TP = const double*>
+__device__ __forceinline__ bool lane_row(LaneSite& ls, const double* sun, const double* module, R* row,
+                                         TP t = (const double*)g_pv_tab)
 {
     double tl = sun[SUN_TL];
     if (ls.linke) {
@@ -1066,7 +1071,7 @@ __device__ __forceinline__ bool lane_row(LaneSite& ls, const double* sun, const 
         tl = ls.tl;
     }
     double g[ROW];
-    if (site_geom<false, sizeof(R) == 4>(ls.k, sun, tl, module, g)) return true;
+    if (site_geom<false, sizeof(R) == 4>(ls.k, sun, tl, module, g, t)) return true;
     site_row<R>(g, sun, row);
     return g[G_GHICS] == 0.0;
 }
