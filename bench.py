@@ -152,7 +152,7 @@ def parse():
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
                     help="c2: the headline (BASELINE.json configs[1]); c3: 1,048,576 chains x 1 day, stats, two "
                          "batches in flight (~33 GB of state + scratch each); c4: 16,384 chains x the year 2019 "
-                         "(Europe/Berlin wall clock, stats, day windows); c5: the lat/lon sweep (65,536 sites x 1 "
+                         "(Europe/Berlin wall clock, stats, 30-day windows); c5: the lat/lon sweep (65,536 sites x 1 "
                          "week, markov cc with per-site tables, per-site PV geometry, stats mode, day windows)")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8)

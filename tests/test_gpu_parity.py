@@ -80,7 +80,8 @@ def test_probe_math():
     np.testing.assert_array_equal(edge[:4], [-np.inf, np.nan, np.nan, np.inf])
     np.testing.assert_allclose(edge[4], np.log(5e-324), rtol=1e-15)
     xe = np.concatenate([np.random.default_rng(3).uniform(-45, 5, 20000), [0.0, -700.5, 710.0]])
-    np.testing.assert_allclose(probe(13, 0, xe), np.exp(xe), rtol=5e-16, atol=0)
+    with np.errstate(over="ignore"):   # exp(710) = inf on both sides
+        np.testing.assert_allclose(probe(13, 0, xe), np.exp(xe), rtol=5e-16, atol=0)
     # pv_power_f's final clamp relies on v_med3_f32(NaN, 0, Paco) = 0 (min3 on a NaN operand)
     x = np.array([np.nan, -5.0, 0.5, 3000.0, 1e9])
     np.testing.assert_array_equal(probe(9, 2500.0, x), [0.0, 0.0, 0.5, 2500.0, 2500.0])

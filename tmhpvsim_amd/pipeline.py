@@ -55,7 +55,7 @@ def pipeline_defaults(workload, precision="fp32", seconds=None, window=None, wal
     pipeline", "C3, C4, C5"): bench.py's defaults, shared with the tests that check
     the timed schedule.  chains: the chains of one batch on this GPU (a rank's shard of
     a strong-scaled workload); C4 / C5 shards smaller than the one-GPU batch keep more
-    batches in flight (their day windows are walk-latency-bound at small batches, so the
+    batches in flight (their windows' walks are latency-bound at small batches, so the
     GPU has room for several: as many contexts as keep ~3 one-GPU batches' chains in
     flight, at most 8)."""
     c5, c4 = workload == "c5", workload == "c4"
@@ -72,9 +72,12 @@ def pipeline_defaults(workload, precision="fp32", seconds=None, window=None, wal
         if (c4 or c5) and chains:
             full = 16384 if c4 else 65536
             pipeline = max(pipeline, min(8, -(-3 * full // int(chains))))
+    # C4: 30-day windows (round 4, same box: 2.41e11 chain-s/s with day windows, 2.73e11 with
+    # 7-day, 2.78e11 with 30-day; the N = 8 shard alone 1.24e11 / 2.36e11 / 2.47e11 -- the
+    # per-window plan, draws and walk latency no longer dominate a small shard's day)
     cfg = PipelineConfig(
         mode=mode,
-        window=min(window or (86400 if (c5 or c4) else secs), secs),
+        window=min(window or (30 * 86400 if c4 else 86400 if c5 else secs), secs),
         pipeline=pipeline, walks=walks, build_ahead=build_ahead,
         # C2 (same-box A/B, r01): construction on the walk stream at normal priority
         # 1.94e11 chain-s/s vs 1.82e11 on the expansion stream with high-priority walks
