@@ -61,11 +61,12 @@ SIMD_CYCLES_PER_S = 256 * 4 * 2.4e9   # SIMDs x nominal clock
 
 
 def valu_busy(rec, ms):
-    """Cycle-weighted VALU-busy fractions of one launch of `ms` milliseconds:
-    'weighted' = the per-class wave-instruction counts x their issue cycles over the
-    SIMDs' cycles; 'active' = SQ_ACTIVE_INST_VALU (quad-cycles each wave spends on
-    VALU instructions, summed over waves) x 4 over the same.  The instruction-count
-    'frac' beside them prices every instruction at the 2-cycle fp32 rate."""
+    """Cycle-weighted VALU-busy fraction of one launch of `ms` milliseconds: the
+    per-class wave-instruction counts x their issue cycles over the SIMDs' cycles.
+    The instruction-count 'frac' beside it prices every instruction at the 2-cycle
+    fp32 rate.  (SQ_ACTIVE_INST_VALU, kept in the PMC record, counts each wave's VALU
+    cycles with the waves of a SIMD overlapping -- C3 reads 1.01 of the SIMD cycles --
+    so it is not a busy fraction.)"""
     out = {}
     denom = SIMD_CYCLES_PER_S * ms / 1e3
     mix = rec.get("valu_mix")
@@ -75,8 +76,6 @@ def valu_busy(rec, ms):
         cyc = sum(mix.get(k, 0.0) * w for k, w in VALU_CYCLES.items()) + other * VALU_OTHER_CYCLES
         out.update(busy_frac_weighted=cyc / denom, valu_cycles_per_launch=cyc,
                    valu_other_insts_per_launch=other)
-    if rec.get("active_inst_valu"):
-        out["busy_frac_active"] = 4 * rec["active_inst_valu"] / denom
     return out
 
 # BASELINE.json configs[1..4]: C2 4,096 sites on one GPU (weak scaling: per GPU);
@@ -313,8 +312,7 @@ def secondary_lines(args):
             out[name] = {"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"],
                          "steps": d["steps"], "dtype": d["dtype"], "workload": d["config"]["workload"],
                          "roofline": {k: roof.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
-                                                               "kernel_ms", "busy_frac_weighted",
-                                                               "busy_frac_active")},
+                                                               "kernel_ms", "busy_frac_weighted", "aggregate")},
                          "roofline_alone": roof.get("alone"), "faulted_chains": d.get("faulted_chains"),
                          "chain_seconds_live": d.get("chain_seconds_live")}
             if d.get("proxy_world"):
@@ -536,12 +534,18 @@ def main():
     else:
         v = valu(kms_launch) or {}
         va = valu(alone_ms / nwin) or {}   # the same launch with no other batch in flight
+        agg = rec["valu_insts_per_launch"] * 64 * nwin * args.steps / elapsed / 1e12 if rec else None
         roof = {"bound": "valu", "achieved": v.get("achieved"), "peak": VALU_PEAK_TLANE, "unit": "T lane-ops/s",
                 "frac": v.get("frac"), "traffic": rec["traffic_bytes_per_launch"] if rec else None,
                 "alone": {"kernel_ms": alone_ms / nwin, "achieved": va.get("achieved"), "frac": va.get("frac"),
-                          "busy_frac_weighted": va.get("busy_frac_weighted"),
-                          "busy_frac_active": va.get("busy_frac_active")},
-                "busy_frac_weighted": v.get("busy_frac_weighted"), "busy_frac_active": v.get("busy_frac_active"),
+                          "busy_frac_weighted": va.get("busy_frac_weighted")},
+                "busy_frac_weighted": v.get("busy_frac_weighted"),
+                # several batches' expansions overlap (C4 / C5 contexts): a launch's HIP-event
+                # duration then spans its neighbours' work too; this is the expansion lane-ops
+                # of the whole timed region over its wall time
+                "aggregate": ({"achieved": agg, "frac": agg / VALU_PEAK_TLANE,
+                               "busy_frac_weighted": valu_busy(rec, elapsed * 1e3 / (args.steps * nwin))
+                               .get("busy_frac_weighted")} if rec else None),
                 "kernel": "expand_kernel (P2, " + sim.path + ")", "kernel_ms": kms_launch,
                 "launches_per_batch": nwin, "chain_seconds_per_launch": n * launch_secs,
                 "valu_per_chain_second": v.get("valu_per_chain_second"),
