@@ -207,15 +207,16 @@ def test_stats_pipeline_c3_shape_equals_batches():
 
 
 def test_c4_shape_pipeline_equals_batches():
-    """The multi-window schedule of bench.py's C4 line (pipeline_defaults("c4"): day
+    """The multi-window schedule of bench.py's C4 line (pipeline_defaults("c4"): 30-day
     windows, each window's walk beside the previous window's expansion, batches on
-    their contexts' streams) on 2,048 chains x 4 days from 2019-03-30 (the DST
-    spring-forward): per-chain statistics equal BatchedSim.run of the same chains."""
+    their contexts' streams) on 2,048 chains x 34 days from 2019-03-10 (a 30-day window
+    across the DST spring-forward, then 4 days): per-chain statistics equal
+    BatchedSim.run of the same chains."""
     from tmhpvsim_amd.pipeline import BatchPipeline, pipeline_defaults
     from tmhpvsim_amd.engine import BatchedSim
-    n, secs, start = 2048, 4 * 86400, "2019-03-30 00:00:00"
+    n, secs, start = 2048, 34 * 86400, "2019-03-10 00:00:00"
     cfg = pipeline_defaults("c4", seconds=secs)
-    assert cfg.window == 86400 and cfg.mode == "stats"
+    assert cfg.window == 30 * 86400 and cfg.mode == "stats"
     sim = BatchedSim(n, start, tz=TZ, device="cuda:0", horizon=secs)
     pipe = BatchPipeline(sim, n, secs, cfg, lambda k: 9_000_000 + k * n, torch.device("cuda:0"))
     pipe.run(0, len(pipe.ctxs))
@@ -223,7 +224,7 @@ def test_c4_shape_pipeline_equals_batches():
     for ci, cx in enumerate(pipe.ctxs):
         s = BatchedSim(n, start, tz=TZ, device="cuda:0", horizon=secs, chain0=9_000_000 + ci * n)
         s.enable_stats()
-        s.run(secs, trace=(), window=86400)
+        s.run(secs, trace=(), window=cfg.window)   # the same windows (the fixed-point unit follows the window length)
         torch.cuda.synchronize()
         assert torch.equal(cx.hist, s.hist), ci
         assert _same(cx.acc, s.chain_acc), ci

@@ -2227,9 +2227,7 @@ __global__ __launch_bounds__(256) void fixup_kernel(KParams kp, DrawParams dp, S
             __hip_atomic_fetch_max(sg.acc_mx + c, max_key((double)res), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (sv.hist) {
-            const double x = ((double)res - sv.lo) * sv.scale;
-            const int bin = x < 0.0 ? 0 : (x >= (double)(sv.n_bins - 1) ? (int)sv.n_bins - 1 : (int)x);
-            atomicAdd((unsigned long long*)&sv.hist[bin], 1ull);
+            atomicAdd((unsigned long long*)&sv.hist[hist_bin<float>(sv, res)], 1ull);
         }
     }
 }
@@ -3051,6 +3049,8 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
         sv.n_bins = stats->hist ? stats->n_bins : 0;
         sv.lo = stats->lo;
         sv.scale = stats->hist ? stats->n_bins / (stats->hi - stats->lo) : 0.0;
+        sv.scale_f = (float)sv.scale;
+        sv.off_f = (float)(-sv.lo * sv.scale);
         sv.acc = stats->chain_acc;
         lds = stats->hist ? (size_t)stats->n_bins * 4 : 0;
     }

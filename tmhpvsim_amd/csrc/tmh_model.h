@@ -130,7 +130,22 @@ struct StatsView {
     uint32_t n_bins;
     double lo, scale;
     double* acc;
+    float scale_f, off_f;   // fp32 kernels' bin position: res scale + off, off = -lo scale
 };
+
+// the histogram bin of a residual: fp64 kernels (res - lo) scale in fp64; fp32 kernels one
+// fp32 FMA and a clamp (the bin position within ~3e-4 of a bin, 7e-4 W, of the fp64 one:
+// inside the fp32 bar's 2e-3 W edge tolerance of the tests; no fp64 conversions per second)
+template <typename R>
+__device__ __forceinline__ int hist_bin(const StatsView& sv, R res)
+{
+    if constexpr (sizeof(R) == 8) {
+        const double x = (res - sv.lo) * sv.scale;
+        return x < 0.0 ? 0 : (x >= (double)(sv.n_bins - 1) ? (int)sv.n_bins - 1 : (int)x);
+    } else {
+        return (int)__builtin_amdgcn_fmed3f(fmaf(res, sv.scale_f, sv.off_f), 0.0f, (float)(sv.n_bins - 1));
+    }
+}
 
 struct Samp {
     double b[6], a[6];
@@ -1405,8 +1420,7 @@ __device__ __forceinline__ void emit(const TraceView& tr, const StatsView& sv, u
             if (!held) acc.mx = fmax(acc.mx, (double)res);
         }
         if (sv.hist && !held) {
-            const double x = ((double)res - sv.lo) * sv.scale;
-            const int bin = x < 0.0 ? 0 : (x >= (double)(sv.n_bins - 1) ? (int)sv.n_bins - 1 : (int)x);
+            const int bin = hist_bin<R>(sv, res);
             if constexpr (PACK) atomicAdd(&lds_hist[bin >> 1], 1u << ((bin & 1) << 4));
             else atomicAdd(&lds_hist[bin], 1u);
         }
