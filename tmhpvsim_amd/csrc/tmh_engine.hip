@@ -1794,8 +1794,7 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
 #pragma unroll
         for (int i = 0; i < PVF_VGPR; ++i) asm volatile("v_mov_b32 %0, %1" : "=v"(f[i]) : "s"(f[i]));
     }
-    // the block's sums: fp32 in the fp32 kernels (AccF), fp64 in the fp64 ones
-    typename std::conditional<sizeof(R) == 4, AccF, Acc>::type acc{R(0), R(0), R(0), -R(INFINITY)};
+    Acc acc{0.0, 0.0, 0.0, -INFINITY};
     bool alive = false;
     int32_t fault = INT_MAX;
     uint32_t jr = 0, evi = 0;
@@ -2051,10 +2050,10 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
     }
     if (live && sv.acc) {   // the block's sums into the chain's fixed-point window totals (order-free)
         unsigned long long* fx = reinterpret_cast<unsigned long long*>(sg.acc_fx);
-        atomicAdd(fx + c, (unsigned long long)llrint((double)acc.pv * sg.fx_scale));
-        atomicAdd(fx + (size_t)n + c, (unsigned long long)llrint((double)acc.m * sg.fx_scale));
-        atomicAdd(fx + 2 * (size_t)n + c, (unsigned long long)llrint((double)acc.r * sg.fx_scale));
-        __hip_atomic_fetch_max(sg.acc_mx + c, max_key((double)acc.mx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        atomicAdd(fx + c, (unsigned long long)llrint(acc.pv * sg.fx_scale));
+        atomicAdd(fx + (size_t)n + c, (unsigned long long)llrint(acc.m * sg.fx_scale));
+        atomicAdd(fx + 2 * (size_t)n + c, (unsigned long long)llrint(acc.r * sg.fx_scale));
+        __hip_atomic_fetch_max(sg.acc_mx + c, max_key(acc.mx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 

@@ -1382,13 +1382,6 @@ __device__ __forceinline__ void trace_store(void* p, uint64_t i, R v)
 struct Acc {
     double pv, m, r, mx;
 };
-// a 128-second block's sums in the fp32 expansion: at most 128 terms of <= 9,001 W, so
-// the fp32 sum is within ~1e-6 of its fp64 value (the fp32 bar is 1e-5), and the peak is
-// exact; the block end converts them for the fixed-point window totals (no fp64 adds and
-// conversions per chain-second)
-struct AccF {
-    float pv, m, r, mx;
-};
 
 // output specialisations of the time-parallel expansion (chosen on the host)
 enum : int {
@@ -1402,9 +1395,9 @@ enum : int {
 // the histogram (fixup_kernel adds its final value)
 // PACK: the workgroup's LDS histogram holds two 16-bit bins per word (a 128-second
 // block of 256 chains adds at most 32,768 to a bin), half the LDS of one word each
-template <typename R, int OUT = OUT_ANY, bool PACK = false, typename A = Acc>
+template <typename R, int OUT = OUT_ANY, bool PACK = false>
 __device__ __forceinline__ void emit(const TraceView& tr, const StatsView& sv, uint32_t* lds_hist, uint64_t o,
-                                     uint8_t cov, R csi, R pv, R meter, R res, A& acc, bool ok, bool held = false)
+                                     uint8_t cov, R csi, R pv, R meter, R res, Acc& acc, bool ok, bool held = false)
 {
     if constexpr (OUT == OUT_TRACE3) {
         __builtin_nontemporal_store(pv, reinterpret_cast<R*>(tr.pv) + o);
@@ -1421,11 +1414,10 @@ __device__ __forceinline__ void emit(const TraceView& tr, const StatsView& sv, u
     }
     if (ok) {
         if (sv.acc) {
-            using T = decltype(acc.pv);
-            acc.pv += (T)pv;
-            acc.m += (T)meter;
-            acc.r += (T)res;
-            if (!held) acc.mx = acc.mx < (T)res ? (T)res : acc.mx;   // res is never NaN here (ok)
+            acc.pv += (double)pv;
+            acc.m += (double)meter;
+            acc.r += (double)res;
+            if (!held) acc.mx = fmax(acc.mx, (double)res);
         }
         if (sv.hist && !held) {
             const int bin = hist_bin<R>(sv, res);
