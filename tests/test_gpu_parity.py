@@ -400,7 +400,10 @@ def test_stats_match_trace():
     np.testing.assert_allclose(s.chain_acc[0].cpu().numpy(), out["pv"].double().sum(0).cpu().numpy(), rtol=1e-9)
     np.testing.assert_allclose(s.chain_acc[2].cpu().numpy(), res.sum(0).cpu().numpy(), rtol=1e-9)
     np.testing.assert_array_equal(s.chain_acc[3].cpu().numpy(), res.max(0).values.cpu().numpy())
-    x = ((res.cpu().numpy() - (-300.0)) * (4096 / 9300.0))
+    # the fp32 kernels' bin position: one fp32 FMA of res with the fp32-rounded scale and
+    # offset (hist_bin; exact in fp64 here, 48 + 24 bits, then rounded once like the FMA)
+    scale = 4096 / 9300.0
+    x = (res.cpu().numpy() * np.float64(np.float32(scale)) + np.float64(np.float32(300.0 * scale))).astype(np.float32)
     bins = np.clip(np.floor(x), 0, 4095).astype(np.int64)
     np.testing.assert_array_equal(s.hist.cpu().numpy(), np.bincount(bins.ravel(), minlength=4096))
 
