@@ -71,7 +71,7 @@ extern "C" {
 #define TMH_PATH_TIME_PARALLEL 2 /* segment pass + (chain x 128 s block) expansion */
 
 #define TMH_SIGMA_CAP 512  /* capacity of sigma_cloud / sigma_clear per chain (max seen: 132) */
-#define TMH_GEOM_FIELDS 22 /* doubles per step in the clock/geometry table */
+#define TMH_GEOM_FIELDS 22 /* doubles per step in the clock/geometry table (DESIGN.md "Data layout") */
 
 /* ---- SAPM module parameter order (tmh_params.module) ---- */
 enum {
@@ -356,8 +356,9 @@ int tmh_engine_last_expand(const struct tmh_engine* eng);
 
 /* Device math probes for parity tests: out[i] = f(a, x[i]) with
  * f = 0 ndtri, 1 gammaincinv, 2 stdtrit, 3 al_ppf, 4 ndtri (fp32 path),
- * 8 ndtri of the fp64 per-second noise (unpolished), 9 / 10 the fp32 PV chain's
- * v_med3_f32 clamps med3(x, 0, a) / med3(x, -inf, a). */
+ * 8 ocml's ndtri (the fp64 noise quantile's tails), 9 / 10 the fp32 PV chain's
+ * v_med3_f32 clamps med3(x, 0, a) / med3(x, -inf, a), and the fp64 PV chain's
+ * table functions: 11 the noise quantile of the 32-bit word x[i], 12 log, 13 exp. */
 int tmh_probe(int fn, double a, const double* x, double* out, uint32_t n, void* stream);
 
 #ifdef __cplusplus

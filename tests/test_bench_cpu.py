@@ -188,3 +188,15 @@ def test_pipeline_defaults_match_bench_schedule():
     finally:
         sys.argv = old
     assert a.cfg == c2
+
+
+def test_build_stamp_ignores_comments():
+    """The PMC records' build stamp hashes the code the compiler sees: comment and
+    blank-line edits keep it, code edits change it."""
+    from tmhpvsim_amd.build import _code_only
+    a = 'int f(int x) { return x + 1; }  // one\n/* block\n comment */\n'
+    b = 'int f(int x) { return x + 1; }\n\n// two\n'
+    c = 'int f(int x) { return x + 2; }\n'
+    d = 'const char* s = "// not a comment";\n'
+    assert _code_only(a) == _code_only(b) != _code_only(c)
+    assert "// not a comment" in _code_only(d)

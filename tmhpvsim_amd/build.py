@@ -26,14 +26,31 @@ def hipcc():
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off"]
 
 
+def _code_only(text):
+    """C / C++ source without comments and blank-line / trailing-space differences: what
+    the compiler sees (a comment-only edit does not change the stamp)."""
+    import re
+    out, i, n = [], 0, len(text)
+    pat = re.compile(r'//[^\n]*|/\*.*?\*/|"(?:\\.|[^"\\])*"|\'(?:\\.|[^\'\\])*\'', re.S)
+    for m in pat.finditer(text):
+        out.append(text[i:m.start()])
+        tok = m.group(0)
+        out.append(tok if tok[0] in "\"'" else " ")
+        i = m.end()
+    out.append(text[i:])
+    lines = (ln.rstrip() for ln in "".join(out).splitlines())
+    return "\n".join(ln for ln in lines if ln)
+
+
 def build_stamp():
-    """Hash of the library's sources and compile flags: measurement records taken
-    with another build (profiles/pmc_kernels.json) are recognised as stale."""
+    """Hash of the library's sources (code only, comments stripped) and compile flags:
+    measurement records taken with another build (profiles/pmc_kernels.json) are
+    recognised as stale."""
     import hashlib
     h = hashlib.sha256(" ".join([ARCH] + FLAGS).encode())
     for d in DEPS:
         h.update(os.path.basename(d).encode())
-        h.update(open(d, "rb").read())
+        h.update(_code_only(open(d, encoding="utf-8", errors="replace").read()).encode())
     return h.hexdigest()[:16]
 
 
