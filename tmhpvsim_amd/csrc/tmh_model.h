@@ -962,7 +962,8 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     // than sincos(rad(azen)), the same to a few ulps
     double szs, czs;
     {
-        const double sz = sqrt(fmax(1.0 - czr * czr, 0.0));
+        // (F32 rows: fp32 sine of the true zenith; it enters czs only through sin(de) <= 0.01)
+        const double sz = F32 ? (double)__builtin_sqrtf((float)fmax(1.0 - czr * czr, 0.0)) : sqrt(fmax(1.0 - czr * czr, 0.0));
         const double d = rad(de), d2 = d * d;
         const double sd = d * (1.0 - d2 * (1.0 / 6.0) * (1.0 - d2 * (1.0 / 20.0) * (1.0 - d2 * (1.0 / 42.0))));
         const double cd = 1.0 - d2 * 0.5 * (1.0 - d2 * (1.0 / 12.0) * (1.0 - d2 * (1.0 / 30.0) * (1.0 - d2 * (1.0 / 56.0))));
@@ -973,8 +974,14 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     // azimuth az = atan2(Y, X) + 180 deg (NOAA, the oracle's solpos): only cos(az - saz) is
     // used (Hay-Davies / AOI projection), = -(X cos saz + Y sin saz) / hypot(X, Y)
     const double azY = sha, azX = cha * k.slat - sun[SUN_TAND] * k.clat;
-    const double azr = sqrt(azX * azX + azY * azY);
-    const double caz = azr > 0.0 ? -(azX * k.csaz + azY * k.ssaz) / azr : -k.csaz;   // atan2(0, 0) = 0: az = 180
+    double caz;
+    if constexpr (F32) {   // fp32 reciprocal square root: ~1e-7 relative on the AOI projection
+        const float r2 = (float)(azX * azX + azY * azY);
+        caz = r2 > 0.0f ? (double)(-(float)(azX * k.csaz + azY * k.ssaz) * __builtin_amdgcn_rsqf(r2)) : -k.csaz;
+    } else {
+        const double azr = sqrt(azX * azX + azY * azY);
+        caz = azr > 0.0 ? -(azX * k.csaz + azY * k.ssaz) / azr : -k.csaz;   // atan2(0, 0) = 0: az = 180
+    }
     const double ct = czr;   // cos(rad(deg(acos(czr)))): the same to ~3e-16 absolute
     g[G_COSZ] = ct;
     // pvmodel.py:52-58; F32 (a per-chain site's fp32 row): in fp32, 1e-7 relative -- the bound
@@ -988,20 +995,27 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     // F32 rows: the relative airmass only feeds Ineichen's exponent and the SAPM spectral
     // polynomial (factors of GHI_cs and of the effective irradiance): fp32 power, ~2e-7
     // relative; DISC's airmass (amd, below, ill-conditioned at low sun) stays fp64
-    const double am_rel = azen <= 90.0 ? 1.0 / (czs + 0.50572 * (F32 ? (double)__powf((float)(6.07995 + (90.0 - azen)), -1.6364f)
-                                                                      : pow_pos(6.07995 + (90.0 - azen), -1.6364, t)))
-                                       : NAN;
-    const double am_abs = am_rel * k.pres / 101325.0;
+    double am_rel, am_abs;
+    if constexpr (F32) {   // fp32 quotient; the pressure ratio as a product
+        am_rel = azen <= 90.0 ? (double)__builtin_amdgcn_rcpf(
+                                    (float)(czs + 0.50572 * (double)__powf((float)(6.07995 + (90.0 - azen)), -1.6364f)))
+                              : NAN;
+        am_abs = am_rel * (k.pres * (1.0 / 101325.0));
+    } else {
+        am_rel = azen <= 90.0 ? 1.0 / (czs + 0.50572 * pow_pos(6.07995 + (90.0 - azen), -1.6364, t)) : NAN;
+        am_abs = am_rel * k.pres / 101325.0;
+    }
     const double cz = czs > 0.0 ? czs : 0.0;
     const double gx = -k.cg2 * am_abs * (k.fh1 + k.fh2 * (tl - 1.0));
     const double gexp = F32 ? (double)__expf((float)gx) : exp(gx);   // F32: ~1e-7 relative on GHI_cs (kt guard band 4e-6)
     const double gmax = isnan(gexp) ? 0.0 : (gexp > 0.0 ? gexp : 0.0);
-    g[G_GHICS] = k.cg1 * dni_extra * cz * tl / tl * gmax;                     // ineichen (pvmodel.py:60)
+    // ineichen (pvmodel.py:60); F32 rows drop its tl / tl (an identity to one ulp)
+    g[G_GHICS] = F32 ? k.cg1 * dni_extra * cz * gmax : k.cg1 * dni_extra * cz * tl / tl * gmax;
     const double I0 = sun[SUN_I0];
     g[G_I0] = I0;                                                              // disc (pvmodel.py:63)
     g[G_I0H] = I0 * (ct > 0.065 ? ct : 0.065);
     double amd = zen <= 90.0 ? 1.0 / (ct + 0.15 * pow_pos(93.885 - zen, -1.253, t)) : NAN;
-    amd = amd * 101325.0 / 101325.0;
+    if constexpr (!F32) amd = amd * 101325.0 / 101325.0;   // (pvlib's pressure scaling: an identity to one ulp)
     amd = amd < 12.0 ? amd : (isnan(amd) ? amd : 12.0);
     g[G_AM] = amd;
     const double amd2 = amd * amd;
@@ -1010,7 +1024,8 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     double proj = k.ctilt * czs + k.stilt * szs * caz;                      // haydavies / aoi (pvmodel.py:66-72)
     proj = proj > 1.0 ? 1.0 : (proj < -1.0 ? -1.0 : proj);
     const double cos_tt = proj > 0.0 ? proj : 0.0;
-    g[G_RB] = cos_tt / (czs > 0.01745 ? czs : 0.01745);
+    if constexpr (F32) g[G_RB] = cos_tt * (double)__builtin_amdgcn_rcpf((float)(czs > 0.01745 ? czs : 0.01745));
+    else g[G_RB] = cos_tt / (czs > 0.01745 ? czs : 0.01745);
     g[G_DNIEXTRA] = dni_extra;
     g[G_TERM2] = k.term2;
     g[G_GFAC] = k.gfac;
@@ -1025,8 +1040,10 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     f2 = f2 > 0.0 ? f2 : 0.0;
     if (aoi < 0.0) f2 = 0.0;
     g[G_F2] = f2;
-    g[G_KTC] = g[G_GHICS] / g[G_I0H];
-    g[G_RDNIX] = sun[SUN_RDNIX];
+    if constexpr (!F32) {   // the fp64 rows' products (the fp32 rows hold reciprocals in place)
+        g[G_KTC] = g[G_GHICS] / g[G_I0H];
+        g[G_RDNIX] = sun[SUN_RDNIX];
+    }
     return g[G_GHICS] == 0.0;
 }
 
@@ -1044,7 +1061,7 @@ __device__ __forceinline__ void site_row(const double* g, const double* sun, R* 
         row[G_KTC] = g[G_KTC];
         row[G_RDNIX] = g[G_RDNIX];
     } else {
-        row[G_I0H] = (float)(1.0 / g[G_I0H]);
+        row[G_I0H] = __builtin_amdgcn_rcpf((float)g[G_I0H]);
         row[G_DNIEXTRA] = (float)sun[SUN_RDNIX];
         row[G_AM] = (float)(g[G_AM] * LOG2E);
         row[G_F1] = (float)(g[G_F1] * 1e-3);   // pv_power_f: Ee = F1 (...) without the / 1000
