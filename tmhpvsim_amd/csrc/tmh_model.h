@@ -1014,12 +1014,22 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     const double I0 = sun[SUN_I0];
     g[G_I0] = I0;                                                              // disc (pvmodel.py:63)
     g[G_I0H] = I0 * (ct > 0.065 ? ct : 0.065);
-    double amd = zen <= 90.0 ? 1.0 / (ct + 0.15 * pow_pos(93.885 - zen, -1.253, t)) : NAN;
+    // DISC's airmass from the fp64 zenith (its conditioning at low sun); F32 rows (which hold
+    // am and Kn_c as floats) take the reciprocal and Kn_c's polynomial in fp32 (~1e-7)
+    double amd;
+    if constexpr (F32) amd = zen <= 90.0 ? (double)__builtin_amdgcn_rcpf((float)(ct + 0.15 * pow_pos(93.885 - zen, -1.253, t)))
+                                         : NAN;
+    else amd = zen <= 90.0 ? 1.0 / (ct + 0.15 * pow_pos(93.885 - zen, -1.253, t)) : NAN;
     if constexpr (!F32) amd = amd * 101325.0 / 101325.0;   // (pvlib's pressure scaling: an identity to one ulp)
     amd = amd < 12.0 ? amd : (isnan(amd) ? amd : 12.0);
     g[G_AM] = amd;
-    const double amd2 = amd * amd;
-    g[G_KNC] = 0.866 - 0.122 * amd + 0.0121 * amd2 - 0.000653 * (amd2 * amd) + 0.000014 * (amd2 * amd2);
+    if constexpr (F32) {
+        const float a = (float)amd;
+        g[G_KNC] = fmaf(fmaf(fmaf(fmaf(0.000014f, a, -0.000653f), a, 0.0121f), a, -0.122f), a, 0.866f);
+    } else {
+        const double amd2 = amd * amd;
+        g[G_KNC] = 0.866 - 0.122 * amd + 0.0121 * amd2 - 0.000653 * (amd2 * amd) + 0.000014 * (amd2 * amd2);
+    }
     g[G_DISCOK] = zen > 87.0 ? 0.0 : 1.0;
     double proj = k.ctilt * czs + k.stilt * szs * caz;                      // haydavies / aoi (pvmodel.py:66-72)
     proj = proj > 1.0 ? 1.0 : (proj < -1.0 ? -1.0 : proj);
