@@ -303,7 +303,7 @@ def secondary_lines(args):
         if args.secondary != "all" and name not in args.secondary.split(","):
             continue
         cmd = [sys.executable, os.path.abspath(__file__), "--no-cpu-baseline", "--secondary", "none"] + extra
-        if args.hw_queues_given:
+        if getattr(args, "hw_queues_given", False):
             cmd += ["--hw-queues", str(args.hw_queues)]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
