@@ -12,3 +12,6 @@ cat gpurun_out/dist2_c2.json
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
     --master-port 29518 bench.py --gpus 2 --workload c3 --chains 131072 --steps 2 --warmup 1 > gpurun_out/dist2_c3.json 2> gpurun_out/dist2_c3.err || exit $?
 cat gpurun_out/dist2_c3.json
+# C4 (multi-window statistics schedule, 30-day windows) through bench.py's own launcher
+timeout -k 10 300 python bench.py --gpus 2 --workload c4 --chains 4096 --steps 2 --warmup 1 > gpurun_out/dist2_c4.json 2> gpurun_out/dist2_c4.err || exit $?
+cat gpurun_out/dist2_c4.json
