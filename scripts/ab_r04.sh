@@ -3,6 +3,10 @@
 #   c5 with the current library vs the 3-waves-per-SIMD C5 expansion (libtmh_c5w3.so);
 #   the C4 one-GPU proxies at N = 8 with day windows vs 7-day windows, 32 vs 16 hardware queues;
 #   C3 / C4 persistent statistics expansion vs one tile per workgroup (libtmh_nopersist.so).
+# The variant libraries were built from the sources of their day (scripts/build_variant.sh,
+# or -D flags: TMH_EXP_WAVES_F64, TMH_EXP_WG_STATS); the results are in DESIGN.md's round-4
+# section, and the code they compared has since moved on, so this script records the runs
+# rather than reproducing them on the current tree (scripts/ab_runs.sh runs new A/B lists).
 set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
