@@ -278,9 +278,9 @@ def parse():
 SECONDARY = {   # --secondary: the other BASELINE.json configs, each in a child process of its own
     "c2_fp64": ["--precision", "fp64", "--steps", "10", "--warmup", "3"],
     "c3": ["--workload", "c3", "--steps", "4", "--warmup", "1"],
-    # C4 / C5 at N = 1 keep 3 batches in flight: whole rounds of them (6 / 3 timed batches)
+    # C4 / C5 at N = 1 keep 3 / 5 batches in flight: whole rounds of them (6 / 5 timed batches)
     "c4": ["--workload", "c4", "--steps", "6", "--warmup", "1"],
-    "c5": ["--workload", "c5", "--steps", "3", "--warmup", "1"],
+    "c5": ["--workload", "c5", "--steps", "5", "--warmup", "1"],
     # one-GPU proxies of the strong-scaled configurations at N = 8 (and C4 at 2, 4): rank 0's
     # shard timed alone (8 batches in flight for C4 / C5 shards, pipeline_defaults);
     # `projected_efficiency` = T_1 / (N T_N) = its (rank) rate / the N = 1 rate above

@@ -30,7 +30,7 @@ else
   C4WIN=$(python3 -c "from tmhpvsim_amd.pipeline import pipeline_defaults as d; print(d('c4').window)")
   PMC_PASS_TIMEOUT=240 bash scripts/pmc_workload.sh ${TAG}_c4 c4 16384 $C4WIN fp32 stats faithful -- --workload c4 --steps 1 --warmup 1 || exit 1
   cp gpurun_out/pmc_kernels.json profiles/pmc_kernels.json
-  for wl in "c3 --steps 4 --warmup 1" "c4 --steps 6 --warmup 1" "c5 --steps 3 --warmup 1"; do
+  for wl in "c3 --steps 4 --warmup 1" "c4 --steps 6 --warmup 1" "c5 --steps 5 --warmup 1"; do
     set -- $wl
     timeout -k 10 600 python -u bench.py --workload $wl > gpurun_out/bench_${TAG}_$1.json 2> gpurun_out/bench_${TAG}_$1.err || exit 1
     cat gpurun_out/bench_${TAG}_$1.json

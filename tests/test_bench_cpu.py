@@ -170,7 +170,7 @@ def test_pipeline_defaults_match_bench_schedule():
     """bench.py and the GPU tests of the timed schedule (tests/test_gpu_trace3.py) take the
     schedule from tmhpvsim_amd.pipeline.pipeline_defaults: C2 runs the gated schedule with
     five contexts, two walks in flight and construction four batches ahead; C3 two stats
-    contexts; C4 30-day and C5 day windows (C5 compacted)."""
+    contexts; C4 30-day and C5 day windows (C5 compacted), three and five contexts."""
     import sys
     from tmhpvsim_amd.pipeline import pipeline_defaults
     c2 = pipeline_defaults("c2")
@@ -180,6 +180,7 @@ def test_pipeline_defaults_match_bench_schedule():
     assert (c3.mode, c3.pipeline, c3.walks) == ("stats", 2, 1)
     c4, c5 = pipeline_defaults("c4"), pipeline_defaults("c5")
     assert c4.window == 30 * 86400 and c5.window == 86400 and c5.compact and not c4.compact
+    assert (c4.pipeline, c5.pipeline) == (3, 5)
     import bench
     old = sys.argv
     try:

@@ -68,7 +68,9 @@ def pipeline_defaults(workload, precision="fp32", seconds=None, window=None, wal
     build_ahead = build_ahead or max(1, walks) + (2 if walks > 1 else 1)
     # c3: two 1 M-chain batches in flight (2 x ~27 GB of state + scratch): +3 % over one (r02)
     if not pipeline:
-        pipeline = 2 if workload == "c3" else build_ahead + 1
+        # c5: five compacted batches in flight (round 4, same box: 3.40 / 3.46 / 3.51 / 3.51e10
+        # live chain-s/s with 3 / 4 / 5 / 6; the compacted windows shrink as chains fault)
+        pipeline = 2 if workload == "c3" else (5 if c5 else build_ahead + 1)
         if (c4 or c5) and chains:
             full = 16384 if c4 else 65536
             pipeline = max(pipeline, min(8, -(-3 * full // int(chains))))
