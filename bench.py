@@ -263,7 +263,10 @@ def parse():
         setattr(a, k, getattr(a.cfg, k))
     # C5's compacted windows walk and expand in turn (latency-bound walk): 16 lanes per
     # chain (1.76e10 against 1.73e10 with the batch-size default, r02 same box)
-    a.walk_lanes = a.walk_lanes or (16 if c5 else 0)
+    # C3 / C4 batches above 8,192 chains: 8 lanes per chain (round 4, same box, twice: C3
+    # 2.95 -> 2.99e11, C4 2.81-2.82 -> 2.86e11 against the library's batch-size default of 4);
+    # smaller shards keep the default 16 (the C4 N = 8 shard: 2.50 against 2.46e11 with 8)
+    a.walk_lanes = a.walk_lanes or (16 if c5 else (8 if a.workload in ("c3", "c4") and per_gpu > 8192 else 0))
     if a.secondary is None:
         # the full report (the default C2 run with its CPU baseline) carries them; quick runs do not
         a.secondary = "all" if (a.workload == "c2" and a.precision == "fp32" and not a.no_cpu_baseline) else "none"

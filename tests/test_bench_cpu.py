@@ -201,3 +201,13 @@ def test_build_stamp_ignores_comments():
     d = 'const char* s = "// not a comment";\n'
     assert _code_only(a) == _code_only(b) != _code_only(c)
     assert "// not a comment" in _code_only(d)
+
+
+def test_walk_lanes_defaults(monkeypatch):
+    """8 walk lanes per chain for C3 / C4 batches above 8,192 chains, 16 for C5, the
+    library's batch-size default (0) otherwise (C2, and the small C4 shards of N = 8)."""
+    for argv, want in (([], 0), (["--workload", "c3"], 8), (["--workload", "c4"], 8),
+                       (["--workload", "c4", "--proxy-world", "8"], 0), (["--workload", "c5"], 16),
+                       (["--workload", "c3", "--proxy-world", "8"], 8), (["--workload", "c4", "--walk-lanes", "4"], 4)):
+        monkeypatch.setattr(sys, "argv", ["bench.py"] + argv)
+        assert bench.parse().walk_lanes == want, argv
