@@ -198,6 +198,9 @@ def parse():
                          "stream shares a queue with another pipeline stream and waits for its kernels (same "
                          "box: 1.74-1.76 ms per C2 batch with 4 queues, 1.49-1.51 with 8, 1.47-1.51 with 16); "
                          "default 16, 32 for c4 / c5 (three streams per batch in flight, up to 8 batches)")
+    ap.add_argument("--queues", default="dedicated", choices=["dedicated", "shared"],
+                    help="pipeline streams on hardware queues of their own (dedicated: CU-masked over every CU, "
+                         "independent of GPU_MAX_HW_QUEUES) or plain streams sharing HIP's queue pool (shared)")
     ap.add_argument("--secondary", default=None,
                     help="after the headline measurement (one GPU only), run the other configurations in child "
                          "processes and add their lines under 'secondary': all | none | a comma list of "
@@ -257,7 +260,7 @@ def parse():
                               minutes_ahead=None if a.minutes_ahead is None else bool(a.minutes_ahead),
                               commit_stream=None if a.commit_stream is None else bool(a.commit_stream),
                               walk_order=bool(a.walk_order), walk_cus=a.walk_cus, other_cus=a.other_cus,
-                              timeline=a.timeline)
+                              timeline=a.timeline, queues=a.queues)
     for k in ("mode", "window", "pipeline", "walks", "build_ahead", "build_on", "walk_priority", "compact",
               "minutes_ahead", "commit_stream"):
         setattr(a, k, getattr(a.cfg, k))
@@ -576,7 +579,7 @@ def main():
                    "construction_on": args.build_on, "walk_priority": args.walk_priority,
                    "schedule": args.schedule if pipe.gated() else None,
                    "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"), "walks_in_flight": pipe.W, "walk_order": bool(args.walk_order), "walk_cus": args.walk_cus or "all", "other_cus": args.other_cus if args.walk_cus else "all",
-                   "walk_chains_per_row": args.walk_cpr, "walk_lanes": args.walk_lanes or "auto", "build_ahead": pipe.A,
+                   "walk_chains_per_row": args.walk_cpr, "queues": args.queues, "walk_lanes": args.walk_lanes or "auto", "build_ahead": pipe.A,
                    "minutes_ahead": bool(args.minutes_ahead), "commit_stream": bool(args.commit_stream),
                    "compacted_windows": bool(args.compact and args.mode == "stats" and nwin > 1)},
         "roofline": roof,

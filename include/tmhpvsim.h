@@ -182,8 +182,11 @@ int tmh_set_walk_order(struct tmh_engine* eng, int on);
  * counterpart: a scheduling helper for callers that pipeline batches).  CU-mask
  * bits cu_first .. cu_first + cu_count - 1 of the current device; the driver
  * spreads consecutive mask bits over the XCDs, so a range is an even share of
- * every XCD.  cu_count == 0: all CUs (a plain stream).  *stream receives the
- * hipStream_t; release it with tmh_stream_destroy. */
+ * every XCD.  cu_count == 0: all CUs (a plain stream).  A range of every CU runs
+ * anywhere like a plain stream but, being CU-masked, on a hardware queue of its own
+ * (plain streams share GPU_MAX_HW_QUEUES queues round-robin, a queue running its
+ * packets in order across them): the pipelines' streams (tmhpvsim_amd.pipeline).
+ * *stream receives the hipStream_t; release it with tmh_stream_destroy. */
 int tmh_stream_create_cus(uint32_t cu_first, uint32_t cu_count, void** stream);
 int tmh_stream_destroy(void* stream);
 /* Compaction (batches whose chains fault, e.g. the reference's markov-mode

@@ -59,6 +59,7 @@ def lib():
                               p, p, p, p, p, p, p, p]
         L.orc_set_tables.argtypes = [p, p, C.c_uint32]
         L.orc_set_sites.argtypes = [p, p, C.c_uint32]
+        L.orc_set_chain_ids.argtypes = [p, C.c_uint32]
         L.orc_injected_streams.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, p, C.c_int]
         L.orc_set_stats.argtypes = [p, p, p, C.c_uint32, C.c_double, C.c_double, C.c_double]
         _lib = L
@@ -109,7 +110,8 @@ def _ptr(a):
 
 
 def run(mp, chain0, n_chains, n_steps, start, tz=None, inj=None, n_threads=1,
-        outputs=("csi", "covered", "pv", "meter", "residual", "pos"), tables=None, sites=None, stats=None):
+        outputs=("csi", "covered", "pv", "meter", "residual", "pos"), tables=None, sites=None, stats=None,
+        chain_ids=None):
     """Run the oracle; returns dict of time-major [n_steps, n_chains] arrays + status/init.
 
     tables: optional per-chain shape tables (shapes [n_chains, 6, 4] float64,
@@ -117,7 +119,8 @@ def run(mp, chain0, n_chains, n_steps, start, tz=None, inj=None, n_threads=1,
     sites: optional per-chain PV sites [n_chains, 8] (or (sites, linke [n_chains, 12])).
     stats: optional dict(n_bins, lo, hi, amb_eps): per-chain statistics of the good
     seconds as the GPU's stats mode keeps them -> res["acc"] [n, 4] (sum pv, sum
-    meter, sum residual, max residual), res["hist"] [n, n_bins], res["amb"] [n]."""
+    meter, sum residual, max residual), res["hist"] [n, n_bins], res["amb"] [n].
+    chain_ids: optional global ids [n_chains] (chain c is chain_ids[c], not chain0 + c)."""
     P = make_params(mp, n_threads)
     cal, utc = calendar(start, n_steps, tz)
     out = {}
@@ -145,6 +148,11 @@ def run(mp, chain0, n_chains, n_steps, start, tz=None, inj=None, n_threads=1,
             sli = np.ascontiguousarray(sli, dtype=np.float64)
             assert sli.shape == (n_chains, 12)
         lib().orc_set_sites(_ptr(ssi), _ptr(sli), n_chains)
+    ids = None
+    if chain_ids is not None:
+        ids = np.ascontiguousarray(chain_ids, dtype=np.uint64)
+        assert ids.shape == (n_chains,)
+        lib().orc_set_chain_ids(_ptr(ids), n_chains)
     if stats is not None:
         acc = np.zeros((n_chains, 4))
         hist = np.zeros((n_chains, int(stats["n_bins"])), dtype=np.uint64)
@@ -162,6 +170,8 @@ def run(mp, chain0, n_chains, n_steps, start, tz=None, inj=None, n_threads=1,
             lib().orc_set_sites(None, None, 0)
         if stats is not None:
             lib().orc_set_stats(None, None, None, 0, 0.0, 1.0, 0.0)
+        if ids is not None:
+            lib().orc_set_chain_ids(None, 0)
     if rc != 0:
         raise RuntimeError(f"orc_run failed: {rc}")
     res = {k: v for k, v in out.items() if v is not None}

@@ -747,6 +747,17 @@ void orc_set_sites(const double* sites /* [n][8] */, const double* linke /* [n][
     g_sites_n = n;
 }
 
+/* optional global chain ids (tests comparing scattered chains of a large GPU batch
+ * in one run): chain c of the orc_run call is global chain g_ids[c] instead of
+ * chain0 + c; keyed draws follow the global id exactly as on the GPU */
+static const uint64_t* g_ids;
+static uint32_t g_ids_n;
+void orc_set_chain_ids(const uint64_t* ids, uint32_t n)
+{
+    g_ids = ids;
+    g_ids_n = n;
+}
+
 /* optional on-host statistics of orc_run (the GPU's stats mode, tmh_stats): per
  * chain c: acc[c][4] = sum pv, sum meter, sum residual (W s), max residual over
  * its good seconds; hist[c][n_bins] its residual histogram (edge bins absorb
@@ -817,7 +828,7 @@ int orc_run(const orc_params* P, uint64_t chain0, uint32_t n_chains, uint32_t n_
 #pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
     for (uint32_t c = 0; c < n_chains; ++c) {
         chain_t* ch = (chain_t*)calloc(1, sizeof(chain_t));
-        ch->chain = chain0 + c;
+        ch->chain = (g_ids && c < g_ids_n) ? g_ids[c] : chain0 + c;
         orc_params Pc;
         const orc_params* Ps = P;   /* the chain's PV site */
         if (g_sites && c < g_sites_n) {

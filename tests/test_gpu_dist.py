@@ -1,7 +1,8 @@
 """The multi-GPU stats path on the one test GPU: two ranks (gloo, both on cuda:0) run
 tmhpvsim_amd.dist.simulate_stats on their chain shards through the product path and
-all-reduce; the node totals equal one unsharded run (histogram bit for bit: keyed
-Philox makes every chain independent of the partition)."""
+all-reduce; the node totals equal one unsharded run bit for bit -- histogram, peak and
+energies (keyed Philox makes every chain independent of the partition, SURVEY.md §8e,
+and the node energies are integer fixed-point sums, dist.chain_totals)."""
 import os
 import socket
 import subprocess
@@ -38,5 +39,6 @@ def test_simulate_stats_two_ranks_equal_one(tmp_path):
         assert int(got["bad"]) == bad1
         np.testing.assert_array_equal(got["hist"], want["hist"])
         assert float(got["peak_residual"]) == float(want["peak_residual"])
+        np.testing.assert_array_equal(got["energy_fx"], want["energy_fx"])   # integer energy sums: bit for bit
         for k in ("energy_pv", "energy_meter", "energy_residual"):
-            assert float(got[k]) == pytest.approx(float(want[k]), rel=1e-12)
+            assert float(got[k]) == float(want[k])

@@ -174,6 +174,19 @@ def cu_stream(cu_first, cu_count, device):
     return torch.cuda.ExternalStream(h.value, device=device)
 
 
+def dedicated_stream(device):
+    """A torch stream on a hardware queue of its own: a CU-masked HIP stream whose mask
+    holds every CU (tmh_stream_create_cus(0, all)).  HIP maps plain streams onto a pool
+    of GPU_MAX_HW_QUEUES hardware queues (4 by default) shared round-robin by every
+    stream of the process -- torch's stream pool included -- and a queue runs its
+    packets in order across the streams sharing it; a CU-masked stream always gets a
+    queue of its own, so the pipeline's streams never wait behind each other's kernels
+    whatever GPU_MAX_HW_QUEUES is.  Lives as long as the process."""
+    import torch
+    ncu = torch.cuda.get_device_properties(device).multi_processor_count
+    return cu_stream(0, ncu, device)
+
+
 def profile_read(eng, kernel):
     """(total ms, launches) of one kernel since the last read (tmh_profile_read)."""
     ms, n = C.c_double(), C.c_int()

@@ -313,16 +313,12 @@ class BatchedSim:
         return plan[: n_steps * _lib.TMH_GEOM_FIELDS * 8].view(torch.float64).view(n_steps, _lib.TMH_GEOM_FIELDS)
 
     def stats_totals(self):
-        """Node-local totals: histogram, energy sums (W*s) and peak residual (W)."""
-        acc = self.chain_acc
-        ok = _torch().as_tensor(self.status() == 0, device=self.device)
-        tot = dict(
-            energy_pv=acc[0][ok].sum(), energy_meter=acc[1][ok].sum(), energy_residual=acc[2][ok].sum(),
-            peak_residual=acc[3][ok].max() if bool(ok.any()) else _torch().tensor(float("-inf"), device=self.device),
-        )
-        if self.hist is not None:
-            tot["hist"] = self.hist.clone()
-        return tot
+        """Node-local totals: histogram, energy sums (W*s, exact fixed-point limbs and the
+        fp64 values of them) and peak residual (W) over every chain's accumulated
+        seconds -- a faulted chain's seconds before its fault included, in energies
+        and histogram alike (dist.chain_totals)."""
+        from .dist import chain_totals
+        return chain_totals(self.chain_acc, self.hist.clone() if self.hist is not None else None)
 
 
 WINDOW_BUFFERS = 3   # plan + scratch sets of the multi-window pipeline (run_windows)

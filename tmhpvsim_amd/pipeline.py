@@ -44,6 +44,8 @@ class PipelineConfig:
     other_cus: str = "all"       # with walk_cus: the other streams on all CUs or the rest
     compact: bool = False        # multi-window stats batches: later windows on the live chains only
     timeline: bool = False       # gated: HIP events around every build, walk and expansion
+    queues: str = "dedicated"    # "dedicated": normal-priority streams on hardware queues of their own
+                                 # (_lib.dedicated_stream); "shared": plain streams (GPU_MAX_HW_QUEUES pool)
     hist_bins: int = 4096
     hist_lo: float = -300.0
     hist_hi: float = 9000.0
@@ -108,6 +110,19 @@ class BatchPipeline:
         self._prio = lambda s: prio_hi if s == "high" else prio_lo
         pipe = self
 
+        def mk(prio="normal"):
+            # HIP maps plain streams round-robin onto GPU_MAX_HW_QUEUES hardware queues (4 by
+            # default) and a queue runs its packets in order across the streams sharing it:
+            # with 4, the C2 expansion stream shared a queue with another pipeline stream and
+            # waited for its kernels (1.74-1.76 ms per batch against 1.47-1.51 with 16 queues,
+            # round 3).  A dedicated stream (CU-masked over every CU) has a queue of its own
+            # at any GPU_MAX_HW_QUEUES.  (High-priority streams keep HIP's priority pool: the
+            # CU-masked constructor takes no priority.)
+            if cfg.queues == "dedicated" and prio != "high":
+                return _lib.dedicated_stream(device)
+            return torch.cuda.Stream(device, priority=pipe._prio(prio))
+        self._mk = mk
+
         class Ctx:   # one batch in flight: its own state, plan, scratch, outputs and HIP streams
             # The context's own streams are created on first use: the gated schedule runs on
             # shared streams, and every extra stream shares one of HIP's few hardware queues
@@ -115,7 +130,7 @@ class BatchPipeline:
             @property
             def stream(self):
                 if self._stream is None:
-                    self._stream = torch.cuda.Stream(device)
+                    self._stream = mk()
                 return self._stream
 
             @property
@@ -125,7 +140,7 @@ class BatchPipeline:
             @property
             def wstream(self):   # the walk runs on a stream of its own
                 if self._wstream is None:
-                    self._wstream = torch.cuda.Stream(device, priority=pipe._prio(cfg.walk_priority))
+                    self._wstream = mk(cfg.walk_priority)
                 return self._wstream
 
             @property
@@ -140,14 +155,21 @@ class BatchPipeline:
                 self.kernel_done = torch.cuda.Event()
                 self.expanded = None   # recorded after this context's last expansion
                 self.state = torch.zeros(L.tmh_state_bytes(n), dtype=torch.uint8, device=device)
-                self.plan = torch.empty(L.tmh_plan_bytes(win), dtype=torch.uint8, device=device)
-                self.scratch = torch.empty(L.tmh_engine_scratch_bytes(sim._eng, n, win), dtype=torch.uint8,
-                                           device=device)
-                if cfg.compact and cfg.mode == "stats" and nwin > 1:   # compacted windows: a working state
+                compacted = cfg.compact and cfg.mode == "stats" and nwin > 1
+                # multi-window batches of the time-parallel path run on the window buffers
+                # (engine.run_windows) only: no plan + scratch set of their own (a 30-day window
+                # of 16,384 chains is ~10 GB of scratch)
+                windowed = nwin > 1 and not compacted and sim.path == "time_parallel"
+                self.plan = self.scratch = None
+                if not windowed:
+                    self.plan = torch.empty(L.tmh_plan_bytes(win), dtype=torch.uint8, device=device)
+                    self.scratch = torch.empty(L.tmh_engine_scratch_bytes(sim._eng, n, win), dtype=torch.uint8,
+                                               device=device)
+                if compacted:   # compacted windows: a working state
                     self.work = torch.empty_like(self.state)
                     self.ids = torch.empty(n, dtype=torch.int32, device=device)
                     self.nlive = torch.zeros(1, dtype=torch.int32, device=device)
-                if nwin > 1 and not (cfg.compact and cfg.mode == "stats"):
+                if windowed:
                     # plan + scratch sets of the multi-window pipeline (engine.run_windows): the
                     # walks of the next windows run ahead of this window's expansion
                     wb = L.tmh_plan_bytes(win) + L.tmh_engine_scratch_bytes(sim._eng, n, win)
@@ -174,18 +196,17 @@ class BatchPipeline:
         # order across the streams sharing it, so streams nobody uses are not created (bench.py
         # raises the queues to 32 for these workloads' 3 streams per context).
         W = self.W = max(1, cfg.walks)
-        self.estream = self.bst = self.cst = None
+        self.estream = self.bst = self._cst = None
         self.wsts = []
         if nwin == 1:
-            self.estream = torch.cuda.Stream(device, priority=self._prio(cfg.expand_priority))
-            self.wsts = [torch.cuda.Stream(device, priority=self._prio(cfg.walk_priority)) for _ in range(W)]
-            self.bst = torch.cuda.Stream(device, priority=self._prio(cfg.build_priority))
-            self.cst = torch.cuda.Stream(device)
+            self.estream = mk(cfg.expand_priority)
+            self.wsts = [mk(cfg.walk_priority) for _ in range(W)]
+            self.bst = mk(cfg.build_priority)
             if cfg.walk_cus:   # the walks on a share of every XCD's CUs (CU-masked streams)
                 ncu = torch.cuda.get_device_properties(device).multi_processor_count
                 self.wsts = [_lib.cu_stream(0, cfg.walk_cus, device) for _ in range(W)]
                 if cfg.other_cus == "rest":
-                    self.bst, self.cst = (_lib.cu_stream(cfg.walk_cus, ncu - cfg.walk_cus, device) for _ in range(2))
+                    self.bst, self._cst = (_lib.cu_stream(cfg.walk_cus, ncu - cfg.walk_cus, device) for _ in range(2))
                     self.estream = _lib.cu_stream(cfg.walk_cus, ncu - cfg.walk_cus, device)
             self.eptr = C.c_void_p(self.estream.cuda_stream)
             self.bst_p = C.c_void_p(self.bst.cuda_stream)
@@ -193,6 +214,12 @@ class BatchPipeline:
         self.tl = {}   # timeline: per-batch HIP timing events (build done, walk start / end, expansion start / end)
 
     # ------------------------------------------------------------------ helpers
+    @property
+    def cst(self):   # the commit stream (gated schedule with commit_stream only): created on first use
+        if self._cst is None:
+            self._cst = self._mk()
+        return self._cst
+
     def ctx_of(self, k):
         return self.ctxs[k % len(self.ctxs)]
 
@@ -232,7 +259,7 @@ class BatchPipeline:
         # up to two windows ahead of the expansions on its stream (engine.run_windows)
         wins = [(s0, min(win, secs - s0)) for s0 in range(0, secs, win)]
         if getattr(cx, "pstream", None) is None:   # the context's plan stream (plans are per batch)
-            cx.pstream = self.torch.cuda.Stream(self.dev)
+            cx.pstream = self._mk()
         run_windows(L, sim._eng, cx.state, chain0, n, wins, cx.wbufs, cx.stream, cx.wstream, lambda w: cx.tr, cx.st,
                     plan_stream=cx.pstream)
 
@@ -445,12 +472,11 @@ class BatchPipeline:
                     st_.synchronize()
 
     def totals(self):
-        """stats mode: the node-local totals over every context (histogram, energies, peak)."""
-        torch = self.torch
+        """stats mode: the node-local totals over every context (histogram, energies, peak;
+        dist.chain_totals: every chain's accumulated seconds, exact integer energy sums)."""
+        from .dist import chain_totals
         hist = sum(cx.hist for cx in self.ctxs)
-        acc = torch.stack([cx.acc for cx in self.ctxs])
-        return dict(energy_pv=acc[:, 0].sum(), energy_meter=acc[:, 1].sum(), energy_residual=acc[:, 2].sum(),
-                    peak_residual=acc[:, 3].max(), hist=hist)
+        return chain_totals(self.torch.cat([cx.acc for cx in self.ctxs], dim=1), hist)
 
     def reset_stats(self):
         for cx in self.ctxs:
