@@ -221,9 +221,6 @@ def parse():
                          "released (default A = walks + 2 with two or more walks, else walks + 1; needs --pipeline >= A + 1)")
     ap.add_argument("--build-priority", default="normal", choices=["high", "normal"],
                     help="gated schedule: HIP stream priority of the construction stream")
-    ap.add_argument("--minutes-ahead", type=int, default=None,
-                    help="gated schedule: build each batch's minute table with its construction (1) instead of "
-                         "before its expansion on the expansion stream (0, the default)")
     ap.add_argument("--commit-stream", type=int, default=None,
                     help="gated schedule: each batch's fixup + commit on a stream of their own beside the next "
                          "expansion (1) or after its expansion on the expansion stream (0, the default)")
@@ -257,12 +254,11 @@ def parse():
                               stagger=a.stagger, schedule=a.schedule, build_on=a.build_on,
                               walk_priority=a.walk_priority, expand_priority=a.expand_priority,
                               build_priority=a.build_priority,
-                              minutes_ahead=None if a.minutes_ahead is None else bool(a.minutes_ahead),
                               commit_stream=None if a.commit_stream is None else bool(a.commit_stream),
                               walk_order=bool(a.walk_order), walk_cus=a.walk_cus, other_cus=a.other_cus,
                               timeline=a.timeline, queues=a.queues)
     for k in ("mode", "window", "pipeline", "walks", "build_ahead", "build_on", "walk_priority", "compact",
-              "minutes_ahead", "commit_stream"):
+              "commit_stream"):
         setattr(a, k, getattr(a.cfg, k))
     # C5's compacted windows walk and expand in turn (latency-bound walk): 16 lanes per
     # chain (1.76e10 against 1.73e10 with the batch-size default, r02 same box)
@@ -580,7 +576,7 @@ def main():
                    "schedule": args.schedule if pipe.gated() else None,
                    "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"), "walks_in_flight": pipe.W, "walk_order": bool(args.walk_order), "walk_cus": args.walk_cus or "all", "other_cus": args.other_cus if args.walk_cus else "all",
                    "walk_chains_per_row": args.walk_cpr, "queues": args.queues, "walk_lanes": args.walk_lanes or "auto", "build_ahead": pipe.A,
-                   "minutes_ahead": bool(args.minutes_ahead), "commit_stream": bool(args.commit_stream),
+                   "commit_stream": bool(args.commit_stream),
                    "compacted_windows": bool(args.compact and args.mode == "stats" and nwin > 1)},
         "roofline": roof,
         "chain_seconds_total": chain_seconds, "chain_seconds_live": live,

@@ -175,7 +175,7 @@ def test_pipeline_defaults_match_bench_schedule():
     from tmhpvsim_amd.pipeline import pipeline_defaults
     c2 = pipeline_defaults("c2")
     assert (c2.mode, c2.pipeline, c2.walks, c2.build_ahead, c2.window, c2.schedule) == ("trace", 5, 2, 4, 86400, "gated")
-    assert not c2.minutes_ahead and not c2.commit_stream and c2.walk_order
+    assert not c2.commit_stream and c2.walk_order and c2.queues == "dedicated"
     c3 = pipeline_defaults("c3")
     assert (c3.mode, c3.pipeline, c3.walks) == ("stats", 2, 1)
     c4, c5 = pipeline_defaults("c4"), pipeline_defaults("c5")

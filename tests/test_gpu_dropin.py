@@ -68,8 +68,9 @@ def test_readme_noon_pv_plausibility(noon_distribution):
 
 def test_reference_pvmodel_test(noon_distribution):
     """tests/test_pvmodel.py:6-10: one day at 1 s, generation >= 0; the chain's noon mean within
-    the 4,096-chain distribution of the same quantity (the band the fixture measures, in place
-    of a fixed window)."""
+    the 4,096-chain distribution of the same quantity (the band the fixture measures) and inside
+    the absolute physical window 10-250 W as well (a regression shared by PVModel and BatchedSim,
+    e.g. in the folded PV constants, would move the distribution with the chain)."""
     from tmhpvsim_amd import PVModel
     _, noon_means = noon_distribution
     lo, hi = np.percentile(noon_means, [0.05, 99.95])
@@ -79,6 +80,8 @@ def test_reference_pvmodel_test(noon_distribution):
     assert (pv >= 0).all() and pv.max() > 0
     noon = pv[12 * 3600:12 * 3600 + 600]
     assert lo <= noon.mean() <= hi, (noon.mean(), lo, hi)
+    assert 10.0 <= noon.mean() <= 250.0, noon.mean()          # the system's physical noon range
+    assert hi <= 250.0, hi                                     # no chain above the clear-sky ceiling
 
 
 def test_pvmodel_default_time_streams_a_day():

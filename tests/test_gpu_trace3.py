@@ -107,21 +107,33 @@ def test_trace3_equals_any_odd_count():
     np.testing.assert_array_equal(a.status(), b.status())
 
 
+# histogram specs: the default; 21 kW in 2,048 bins (wider than [-300, 9000), still binned
+# in fp32: the fp32 bin position's error bound 3.6e-4 bins); a 100 W range far from 0
+# and a 500 kW range in 16,384 bins, both beyond the 1e-3-bin bound, so the fp32 kernel
+# bins them in fp64 (StatsView::bin64, hist_bin)
+HISTS = {"default": dict(n_bins=4096, lo=-300.0, hi=9000.0), "wide": dict(n_bins=2048, lo=-1000.0, hi=20000.0),
+         "offset": dict(n_bins=1024, lo=4000.0, hi=4100.0), "huge": dict(n_bins=16384, lo=-2e5, hi=3e5)}
+
+
+@pytest.mark.parametrize("spec", list(HISTS))
 @pytest.mark.parametrize("prec", ["fp32", "fp64"])
-def test_stats_odd_count_vs_oracle(prec):
+def test_stats_odd_count_vs_oracle(prec, spec):
     """OUT_STATS with 1,000 chains (a partial last wavefront: lanes past the last chain
     must not record guard-band seconds or touch another chain's corrections): per-chain
-    energies, peak residual and the histogram against the oracle's statistics."""
+    energies, peak residual and the histogram against the oracle's statistics, for
+    histogram ranges that bin in fp32 and ranges that fall back to fp64 binning.  The
+    bin-edge tolerance is a residual tolerance in W (fp32 4.5e-3 W, fp64 2.3e-6 W) times
+    the spec's bins per W."""
     from tmhpvsim_amd import _lib
     n = 1000
-    hist = dict(n_bins=4096, lo=-300.0, hi=9000.0)
+    hist = HISTS[spec]
     mp = ModelParams(seed=0x0DD)
     sim = _sim(n, prec, chain0=123, mp=mp)
     sim.enable_stats(**hist)
     sim.run(86400, trace=())
     torch.cuda.synchronize()
     assert sim.L.tmh_engine_last_expand(sim._eng) == _lib.OUT_STATS | (_lib.OUT_FP64 if prec == "fp64" else 0)
-    amb = 1e-6 if prec == "fp64" else 2e-3
+    amb = (2.3e-6 if prec == "fp64" else 4.5e-3) * hist["n_bins"] / (hist["hi"] - hist["lo"])
     ref = O.run(mp, 123, n, 86400, START, tz=TZ, n_threads=16, outputs=(), stats=dict(hist, amb_eps=amb))
     st = sim.status()
     np.testing.assert_array_equal(st, ref["status"])

@@ -681,9 +681,12 @@ __device__ __forceinline__ double minute_cc(const StateView& st, const PrevView&
 // pair come from that walk, so these draws may run before that window's expansion and
 // commit (tmh_walk_part).  Built with the construction (TMH_WALK_DRAWS), the minute
 // table is off the expansion's stream.
+// rows y of the launch: y < kcap the try-0 candidate of the chain's call ncalls + y;
+// y = kcap + m the draws of the window's minute boundary m.  Grid-stride over y (ny
+// rows, gridDim.y <= 65,535), so no window length is bounded by the grid.
 template <typename R>
 __global__ __launch_bounds__(256) void draws_tail_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
-                                                         int64_t W0, uint32_t nsteps, int64_t fm,
+                                                         int64_t W0, uint32_t nsteps, int64_t fm, uint32_t ny,
                                                          const double* __restrict__ tab64,
                                                          const int2* __restrict__ events,
                                                          const uint32_t* __restrict__ n_events,
@@ -691,8 +694,7 @@ __global__ __launch_bounds__(256) void draws_tail_kernel(DrawParams dp, StateVie
                                                          PrevView prev)
 {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t y = blockIdx.y;
-    if (y == 0) {
+    if (blockIdx.y == 0) {
         if (c == 0) {   // the walk that follows hands out overflow chunks and queued chains
             *sg.pool_n = 0;
             *sg.walk_q = 0;
@@ -708,30 +710,33 @@ __global__ __launch_bounds__(256) void draws_tail_kernel(DrawParams dp, StateVie
     }
     if (c >= n) return;
     const uint64_t chain = chain0 + gid(dp.ids, c);
-    if (y < sg.kcap) {
-        if ((prev.status ? prev.status[c] : st.status[c]) != 0) return;
-        const U4 b = keyed_block(dp.seed, chain, (uint64_t)(st.ncalls[c] + y), TAG_CLOUD, 0);
-        // stored by walk row: the chains of a walk wavefront read adjacent words
-        sg.cand[(size_t)y * n + (sg.rank ? sg.rank[c] : c)] = pow_d(dp.alpha + dp.delta * u52(b.x, b.y), dp.expo);
-        return;
-    }
-    const uint32_t m = y - sg.kcap;
-    const int64_t jm = fm + 60 * (int64_t)m;
-    if (jm >= (int64_t)nsteps) return;
+    const bool live = (prev.status ? prev.status[c] : st.status[c]) == 0;
     const int ne = (int)min(*n_events, ev_cap_dev(nsteps));
-    const double cc = minute_cc(st, prev, sg, n, c, W0, jm, events, ne, tab64);
-    double cloudy, clear;
-    minute_draws<R>(dp, chain, W0 + jm, cc, cloudy, clear);
-    R* t = reinterpret_cast<R*>(sg.mtab);
-    t[(size_t)(2 * m) * n + c] = (R)cloudy;
-    t[(size_t)(2 * m + 1) * n + c] = (R)clear;
-    if constexpr (sizeof(R) == 4) {   // the window end's last two minute boundaries, in fp64
-        const BlockDesc de = *desc_end;
-        const int q = (int32_t)m == de.q0 ? 1 : ((int32_t)m == de.q1 ? 0 : -1);
-        if (q >= 0) {
-            minute_draws<double>(dp, chain, W0 + jm, cc, cloudy, clear);
-            sg.mend[(size_t)(2 * q) * n + c] = cloudy;
-            sg.mend[(size_t)(2 * q + 1) * n + c] = clear;
+    for (uint32_t y = blockIdx.y; y < ny; y += gridDim.y) {
+        if (y < sg.kcap) {
+            if (!live) continue;
+            const U4 b = keyed_block(dp.seed, chain, (uint64_t)(st.ncalls[c] + y), TAG_CLOUD, 0);
+            // stored by walk row: the chains of a walk wavefront read adjacent words
+            sg.cand[(size_t)y * n + (sg.rank ? sg.rank[c] : c)] = pow_d(dp.alpha + dp.delta * u52(b.x, b.y), dp.expo);
+            continue;
+        }
+        const uint32_t m = y - sg.kcap;
+        const int64_t jm = fm + 60 * (int64_t)m;
+        if (jm >= (int64_t)nsteps) continue;
+        const double cc = minute_cc(st, prev, sg, n, c, W0, jm, events, ne, tab64);
+        double cloudy, clear;
+        minute_draws<R>(dp, chain, W0 + jm, cc, cloudy, clear);
+        R* t = reinterpret_cast<R*>(sg.mtab);
+        t[(size_t)(2 * m) * n + c] = (R)cloudy;
+        t[(size_t)(2 * m + 1) * n + c] = (R)clear;
+        if constexpr (sizeof(R) == 4) {   // the window end's last two minute boundaries, in fp64
+            const BlockDesc de = *desc_end;
+            const int q = (int32_t)m == de.q0 ? 1 : ((int32_t)m == de.q1 ? 0 : -1);
+            if (q >= 0) {
+                minute_draws<double>(dp, chain, W0 + jm, cc, cloudy, clear);
+                sg.mend[(size_t)(2 * q) * n + c] = cloudy;
+                sg.mend[(size_t)(2 * q + 1) * n + c] = clear;
+            }
         }
     }
 }
@@ -3051,6 +3056,11 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
         sv.scale = stats->hist ? stats->n_bins / (stats->hi - stats->lo) : 0.0;
         sv.scale_f = (float)sv.scale;
         sv.off_f = (float)(-sv.lo * sv.scale);
+        if (stats->hist) {   // hist_bin: the fp32 bin position's error bound, in bins
+            const double rmax = std::max({9001.0 + std::fabs(eng->kp.inverter[0]), std::fabs(stats->lo), std::fabs(stats->hi)});
+            const double err = std::ldexp(sv.scale * (2.0 * rmax + std::fabs(stats->lo)) + stats->n_bins, -24);
+            sv.bin64 = err > 1e-3 ? 1u : 0u;
+        }
         sv.acc = stats->chain_acc;
         lds = stats->hist ? (size_t)stats->n_bins * 4 : 0;
     }
@@ -3097,14 +3107,15 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
         {   // candidates + the window's minute draws (+ counter resets), one launch
             const int64_t fmh = first_minute_host(utc0, step0);
             const uint32_t nm = fmh < (int64_t)n_steps ? (uint32_t)((n_steps - 1 - fmh) / 60 + 1) : 0;
-            const dim3 grid(cb, sg.kcap + nm);
+            const uint32_t ny = sg.kcap + nm;   // rows; the kernel strides over y past 65,535 (long windows)
+            const dim3 grid(cb, std::min(ny, 65535u));
             const BlockDesc* de = pv.desc + nblk_of(n_steps);
             if (f64)
                 hipLaunchKernelGGL(draws_tail_kernel<double>, grid, dim3(256), 0, s, eng->dp, v, chain0, n_chains, step0,
-                                   n_steps, fmh, pv.tab64, pv.events, pv.n_events, de, sg, prev);
+                                   n_steps, fmh, ny, pv.tab64, pv.events, pv.n_events, de, sg, prev);
             else
                 hipLaunchKernelGGL(draws_tail_kernel<float>, grid, dim3(256), 0, s, eng->dp, v, chain0, n_chains, step0,
-                                   n_steps, fmh, pv.tab64, pv.events, pv.n_events, de, sg, prev);
+                                   n_steps, fmh, ny, pv.tab64, pv.events, pv.n_events, de, sg, prev);
         }
         eng->close(TMH_K_CANDIDATES, t_cand, s);
         if (int rc = hip_check(hipGetLastError(), "draws kernels launch")) return rc;

@@ -131,19 +131,24 @@ struct StatsView {
     double lo, scale;
     double* acc;
     float scale_f, off_f;   // fp32 kernels' bin position: res scale + off, off = -lo scale
+    uint32_t bin64;         // fp32 kernels bin in fp64 (a histogram spec whose fp32 binning error is too large)
 };
 
 // the histogram bin of a residual: fp64 kernels (res - lo) scale in fp64; fp32 kernels one
-// fp32 FMA and a clamp (the bin position within ~3e-4 of a bin, 7e-4 W, of the fp64 one:
-// inside the fp32 bar's 2e-3 W edge tolerance of the tests; no fp64 conversions per second)
+// fp32 FMA and a clamp, no fp64 conversions per second.  That bin position's error is
+// below 2^-24 (scale (2 max(|res|, |lo|) + |lo|) + n_bins) bins (the roundings of scale,
+// of -lo scale and of the FMA): ~3e-4 of a bin for the default [-300, 9000) W in 4,096
+// bins.  The host (step_phases) sets bin64 when that bound exceeds 1e-3 bins (a narrow
+// range far from 0, very many bins): such a spec is binned in fp64 like the fp64 kernels
+// (a scalar branch per second, taken the same way by every wave).
 template <typename R>
 __device__ __forceinline__ int hist_bin(const StatsView& sv, R res)
 {
-    if constexpr (sizeof(R) == 8) {
-        const double x = (res - sv.lo) * sv.scale;
+    if (sizeof(R) == 8 || sv.bin64) {
+        const double x = ((double)res - sv.lo) * sv.scale;
         return x < 0.0 ? 0 : (x >= (double)(sv.n_bins - 1) ? (int)sv.n_bins - 1 : (int)x);
     } else {
-        return (int)__builtin_amdgcn_fmed3f(fmaf(res, sv.scale_f, sv.off_f), 0.0f, (float)(sv.n_bins - 1));
+        return (int)__builtin_amdgcn_fmed3f(fmaf((float)res, sv.scale_f, sv.off_f), 0.0f, (float)(sv.n_bins - 1));
     }
 }
 

@@ -37,7 +37,6 @@ class PipelineConfig:
     walk_priority: str = "normal"
     expand_priority: str = "normal"
     build_priority: str = "normal"
-    minutes_ahead: bool = False  # gated: minute table with the construction instead of before the expansion
     commit_stream: bool = False  # gated: fixup + commit on a stream of their own
     walk_order: bool = True      # walk rows windiest chain first (the run's first walk in chain order)
     walk_cus: int = 0            # gated: segment walks on CU-mask bits 0 .. K-1 (0 = all CUs)
@@ -364,8 +363,6 @@ class BatchPipeline:
         _lib.check(L.tmh_plan(sim._eng, 0, self.secs, self._p(cx.plan), bp))
         _lib.check(L.tmh_walk_part(sim._eng, self._p(cx.state), cx.chain0, self.n, 0, self.secs, self._p(cx.plan),
                                    self._p(cx.scratch), cx.scratch.numel(), None, 0, _lib.WALK_DRAWS, bp))
-        if cfg.minutes_ahead:   # the minute table needs the draws, not the walk
-            _lib.check(L.tmh_expand_part(*self.expand_args(cx), _lib.EXPAND_MINUTES, bp))
         cx.done.record(bst)
         self.tl_mark("built", j, bst)
 
@@ -388,8 +385,7 @@ class BatchPipeline:
         es.wait_event(cx.walked)
         args_ = self.expand_args(cx)
         self.tl_mark("exp0", j, es)
-        _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_KERNEL | (_lib.EXPAND_NO_MINUTES if cfg.minutes_ahead else 0),
-                                     ep))
+        _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_KERNEL, ep))
         self.tl_mark("exp1", j, es)
         if cx.expanded is None:
             cx.expanded = self.torch.cuda.Event()
