@@ -314,7 +314,7 @@ def secondary_lines(args):
             out[name] = {"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"],
                          "steps": d["steps"], "dtype": d["dtype"], "workload": d["config"]["workload"],
                          "roofline": {k: roof.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
-                                                               "kernel_ms", "busy_frac_weighted", "aggregate")},
+                                                               "kernel_ms", "busy_frac_weighted", "aggregate", "per_launch")},
                          "roofline_alone": roof.get("alone"), "faulted_chains": d.get("faulted_chains"),
                          "chain_seconds_live": d.get("chain_seconds_live")}
             if d.get("proxy_world"):
@@ -537,17 +537,21 @@ def main():
         v = valu(kms_launch) or {}
         va = valu(alone_ms / nwin) or {}   # the same launch with no other batch in flight
         agg = rec["valu_insts_per_launch"] * 64 * nwin * args.steps / elapsed / 1e12 if rec else None
-        roof = {"bound": "valu", "achieved": v.get("achieved"), "peak": VALU_PEAK_TLANE, "unit": "T lane-ops/s",
-                "frac": v.get("frac"), "traffic": rec["traffic_bytes_per_launch"] if rec else None,
+        agg_w = valu_busy(rec, elapsed * 1e3 / (args.steps * nwin)).get("busy_frac_weighted") if rec else None
+        # `achieved` / `frac`: the expansion lane-ops of the whole timed region over its wall
+        # time.  With several batches' expansions overlapping (C4 / C5 contexts, C3's two
+        # batches) a launch's HIP-event span also covers its neighbours' work, so the
+        # per-launch figure (`per_launch`) understates the chip's VALU use there
+        roof = {"bound": "valu", "achieved": agg, "peak": VALU_PEAK_TLANE, "unit": "T lane-ops/s",
+                "frac": agg / VALU_PEAK_TLANE if agg else None,
+                "traffic": rec["traffic_bytes_per_launch"] if rec else None,
+                "busy_frac_weighted": agg_w,
+                "per_launch": {"kernel_ms": kms_launch, "achieved": v.get("achieved"), "frac": v.get("frac"),
+                               "busy_frac_weighted": v.get("busy_frac_weighted")},
                 "alone": {"kernel_ms": alone_ms / nwin, "achieved": va.get("achieved"), "frac": va.get("frac"),
                           "busy_frac_weighted": va.get("busy_frac_weighted")},
-                "busy_frac_weighted": v.get("busy_frac_weighted"),
-                # several batches' expansions overlap (C4 / C5 contexts): a launch's HIP-event
-                # duration then spans its neighbours' work too; this is the expansion lane-ops
-                # of the whole timed region over its wall time
-                "aggregate": ({"achieved": agg, "frac": agg / VALU_PEAK_TLANE,
-                               "busy_frac_weighted": valu_busy(rec, elapsed * 1e3 / (args.steps * nwin))
-                               .get("busy_frac_weighted")} if rec else None),
+                "aggregate": ({"achieved": agg, "frac": agg / VALU_PEAK_TLANE, "busy_frac_weighted": agg_w}
+                              if rec else None),
                 "kernel": "expand_kernel (P2, " + sim.path + ")", "kernel_ms": kms_launch,
                 "launches_per_batch": nwin, "chain_seconds_per_launch": n * launch_secs,
                 "valu_per_chain_second": v.get("valu_per_chain_second"),

@@ -349,6 +349,21 @@ __global__ __launch_bounds__(256) void geom_kernel(GParams gp, int64_t step0, ui
     civil_doy(dn, doy, leap);
     double sn[SUN_W];
     sun_at(ck.utc0 + s, doy, leap, gp.linke, sn);
+    {   // the hour angle's advance since the step's 128-s block start (lane_row's rotation)
+        const uint32_t jb = j / BLOCK_STEPS * BLOCK_STEPS;
+        double sb[SUN_W];
+        if (jb == j) {
+            sb[SUN_MIN] = sn[SUN_MIN];
+            sb[SUN_EOT] = sn[SUN_EOT];
+        } else {
+            const int64_t ltb = local_at(ck, step0 + jb);
+            int doyb, leapb;
+            civil_doy(floordiv(ltb, 86400), doyb, leapb);
+            sun_at(ck.utc0 + step0 + jb, doyb, leapb, nullptr, sb);
+        }
+        const double dh = rad(((sn[SUN_MIN] + sn[SUN_EOT]) - (sb[SUN_MIN] + sb[SUN_EOT])) / 4.0);
+        sincos(dh, &sn[SUN_SDH], &sn[SUN_CDH]);
+    }
     for (int i = 0; i < SUN_W; ++i) sun[(size_t)j * SUN_W + i] = sn[i];
     site_geom<true>(site_k(gp.site), sn, sn[SUN_TL], gp.module, g);
     if (g[G_GHICS] == 0.0) fl |= FL_NIGHT;   // ghi_cs = 0 -> pv = 0 whatever the csi
@@ -883,6 +898,7 @@ __device__ __forceinline__ bool redo_second(const KParams& kp, const DrawParams&
         ls.k = site_k(kp.sites + (size_t)gid(kp.ids, c) * 8);
         ls.linke = kp.site_linke ? kp.site_linke + (size_t)gid(kp.ids, c) * 12 : nullptr;
         ls.tl_doy = -1;
+        lane_anchor(ls, sun + (size_t)(j / BLOCK_STEPS * BLOCK_STEPS) * SUN_W);
     }
     bool risky;
     {   // fp32, as expand_kernel<float>
@@ -958,6 +974,7 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
     }
     Acc acc{0.0, 0.0, 0.0, -INFINITY};
     LaneSite ls{};   // per-chain sites (tmh_set_sites)
+    uint32_t ls_block = ~0u;   // the block whose start anchors ls's hour angle
     if (kp.sites) {
         ls.k = site_k(kp.sites + (size_t)(live ? gid(kp.ids, c) : 0) * 8);
         ls.linke = kp.site_linke ? kp.site_linke + (size_t)(live ? gid(kp.ids, c) : 0) * 12 : nullptr;
@@ -1037,7 +1054,12 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
                     const bool covered = ch.sec < ch.t1;
                     cov = covered ? 1 : 0;
                     uint32_t flp = fl;
-                    if (kp.sites) {   // this chain's own site
+                    if (kp.sites) {   // this chain's own site (hour angle anchored at the 128-s block start)
+                        const uint32_t jb = j / BLOCK_STEPS * BLOCK_STEPS;
+                        if (jb != ls_block) {
+                            lane_anchor(ls, sun + (size_t)jb * SUN_W);
+                            ls_block = jb;
+                        }
                         flp = lane_flags(fl, lane_row<R>(ls, sun + (size_t)j * SUN_W, kp.module, row), row);
                     }
                     bool risky;
@@ -1816,6 +1838,7 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
         ls.linke = kp.site_linke ? kp.site_linke + (size_t)(live ? gid(kp.ids, c) : 0) * 12 : nullptr;
         ls.tl_doy = -1;
         blk_night = site_block_night(ls.k, sun + (size_t)(b * BLOCK_STEPS) * SUN_W);
+        if (!blk_night) lane_anchor(ls, sun + (size_t)(b * BLOCK_STEPS) * SUN_W);
     }
     if (live) {
         alive = st.status[c] == 0;

@@ -825,8 +825,11 @@ __device__ double linke_at(const double* lts, int doy, int leap)
 // restatement).  The sun's place depends on the instant only: one plan row per
 // step (sun_at).  The site part runs once per site and step in geom_kernel, or
 // per chain-second when every chain has its own site (tmh_set_sites, C5).
+// SUN_SDH / SUN_CDH: sine and cosine of the hour angle's advance since the start of the
+// step's 128-s expansion block (lane-independent: the site's longitude cancels), so a
+// per-chain site rotates its block-start hour angle instead of a sincos per second (lane_row)
 enum { SUN_SIND = 0, SUN_COSD, SUN_TAND, SUN_EOT, SUN_MIN, SUN_DNIX, SUN_I0, SUN_TL, SUN_DOY, SUN_LEAP, SUN_RDNIX,
-       SUN_W = 12 };
+       SUN_SDH, SUN_CDH, SUN_W = 14 };
 
 __device__ void sun_at(int64_t utc, int doy, int leap, const double* linke, double* o)
 {
@@ -931,17 +934,21 @@ __device__ __forceinline__ SiteK site_k(const double* site)
 // when the clear-sky GHI is 0 (pv = 0 whatever the csi).  FULL = false stops
 // there at night (the per-chain-second path); FULL fills every field.  t: the PV table
 // (g_pv_tab, or an LDS copy of it) for the airmass powers.
-template <bool FULL, bool F32 = false, typename TP = const double*>
-__device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, double tl, const double* m, double* g,
-                                          TP t = (const double*)g_pv_tab)
+// the hour angle (rad) of site k at a sun row: true solar time, fmod(x, 1440) for x in
+// (-1440, 2880) as one exact subtraction (Sterbenz) or none
+__device__ __forceinline__ double hour_angle(const SiteK& k, const double* sun)
 {
-    // fmod(x, 1440) for x in (-1440, 2880): one exact subtraction (Sterbenz) or none
     double tst = sun[SUN_MIN] + sun[SUN_EOT] + 4.0 * k.lon;
     if (tst >= 1440.0) tst -= 1440.0;
     if (tst < 0) tst += 1440.0;
-    const double ha = rad(tst / 4.0 - 180.0);
-    double sha, cha;
-    sincos_pi(ha, &sha, &cha);
+    return rad(tst / 4.0 - 180.0);
+}
+
+// site_geom from the hour angle's sine and cosine (sha, cha) at this sun row
+template <bool FULL, bool F32 = false, typename TP = const double*>
+__device__ __forceinline__ bool site_geom_hc(const SiteK& k, const double* sun, double tl, const double* m, double* g,
+                                             TP t, double sha, double cha)
+{
     double czr = k.slat * sun[SUN_SIND] + k.clat * sun[SUN_COSD] * cha;
     czr = czr > 1.0 ? 1.0 : (czr < -1.0 ? -1.0 : czr);
     // the sun below -0.83 deg elevation (cos z < cos(90.84 deg) = -0.0147): outside the
@@ -1062,6 +1069,15 @@ __device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, dou
     return g[G_GHICS] == 0.0;
 }
 
+template <bool FULL, bool F32 = false, typename TP = const double*>
+__device__ __forceinline__ bool site_geom(const SiteK& k, const double* sun, double tl, const double* m, double* g,
+                                          TP t = (const double*)g_pv_tab)
+{
+    double sha, cha;
+    sincos_pi(hour_angle(k, sun), &sha, &cha);
+    return site_geom_hc<FULL, F32>(k, sun, tl, m, g, t, sha, cha);
+}
+
 constexpr double LOG2E = 1.44269504088896340736;   // the fp32 row's airmass is am log2 e (pv_power_f)
 
 // the kernels' row of one chain's own site (fp32 rows carry the reciprocals
@@ -1099,15 +1115,28 @@ __device__ __forceinline__ bool site_block_night(const SiteK& k, const double* s
     return czr < -0.027;
 }
 
-// per-chain site state of a kernel lane: constants + the day's Linke turbidity
+// per-chain site state of a kernel lane: constants + the day's Linke turbidity + the hour
+// angle's sine and cosine at the current 128-s block's start (lane_anchor)
 struct LaneSite {
     SiteK k;
     const double* linke;   // the chain's 12 monthly values, or NULL (the plan's per-step value)
     int tl_doy;
     double tl;
+    double s0, c0;
 };
 
-// the geometry of lane site `ls` at the plan's sun row; true = night
+// the lane's hour-angle anchor at a block's first sun row (every kernel that evaluates a
+// per-chain site sets it at each 128-s block start of the window, so all of them rotate
+// from the same anchors and agree bit for bit)
+__device__ __forceinline__ void lane_anchor(LaneSite& ls, const double* sun0)
+{
+    sincos_pi(hour_angle(ls.k, sun0), &ls.s0, &ls.c0);
+}
+
+// the geometry of lane site `ls` at the plan's sun row; true = night.  The hour angle's
+// sine and cosine: the block-start anchor rotated by the row's advance (SUN_SDH, SUN_CDH;
+// four fp64 operations instead of a sincos per chain-second, a few 1e-16 off the direct
+// evaluation)
 template <typename R, typename TP = const double*>
 __device__ __forceinline__ bool lane_row(LaneSite& ls, const double* sun, const double* module, R* row,
                                          TP t = (const double*)g_pv_tab)
@@ -1122,7 +1151,9 @@ __device__ __forceinline__ bool lane_row(LaneSite& ls, const double* sun, const 
         tl = ls.tl;
     }
     double g[ROW];
-    if (site_geom<false, sizeof(R) == 4>(ls.k, sun, tl, module, g, t)) return true;
+    const double sdh = sun[SUN_SDH], cdh = sun[SUN_CDH];
+    const double sha = fma(ls.s0, cdh, ls.c0 * sdh), cha = fma(ls.c0, cdh, -(ls.s0 * sdh));
+    if (site_geom_hc<false, sizeof(R) == 4>(ls.k, sun, tl, module, g, t, sha, cha)) return true;
     site_row<R>(g, sun, row);
     return g[G_GHICS] == 0.0;
 }
