@@ -1787,7 +1787,8 @@ constexpr int PVF_VGPR = 0;   // leading PVF fields pinned in VGPRs in the fp32 
 //  fp32 single-site trace (C2): 7 = at most 72 VGPRs (alone -4 % vs 6, no VGPR spills);
 //  fp32 statistics / other outputs (C3, C4): 6 = 80 VGPRs (the 16-bit-pair LDS histogram,
 //    8 KB, + 12 KB staging: 8 workgroups per CU; +6 % over 5 waves);
-//  fp64 single-site: 4 = 128 VGPRs, 4-8 spilled (fp64 C2 6.2 -> 6.5e10, same box);
+//  fp64 single-site: 4 = at most 128 VGPRs (the trace kernel takes 110, no VGPR spills since the
+//    round-4 PV-constant and table changes; 5 waves = 96 VGPRs spill 11 and run the same);
 //  per-chain sites (C5): 2 (a few spills) is 35 % faster than 1
 template <typename R, int OUT, bool SITES>
 constexpr int exp_waves()
@@ -1932,6 +1933,9 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
     // NaN selects at all (if-converted, they cost a compare and three selects per second
     // even when wave_ok holds), and the general one (below).
     const bool wave_ok = __builtin_amdgcn_ballot_w64(live && fault_eff < (int32_t)j1) == 0;
+    // per-chain sites: some lane's site sees daylight in this block (else every second of the
+    // wave is night: no noise block, no geometry)
+    const bool wave_day = !SITES || __builtin_amdgcn_ballot_w64(live && !blk_night) != 0;
     auto second = [&](uint32_t j, uint32_t un, uint32_t um, auto ff) __attribute__((always_inline)) {
         constexpr bool FF = decltype(ff)::value;
         R row[row_w<R>()];
@@ -2043,8 +2047,8 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
             for (; j + 4 <= j1; j += 4) {
                 const uint64_t g = (uint64_t)(W0 + j) >> 2;
                 const U4 pm = keyed_block(kp.seed, chain, g, TAG_METER4, 0);
-                bool need = OUT == OUT_ANY || SITES || !kp.with_pv;
-                if (!need) {   // any daylight second among the four (scalar loads of their flags)
+                bool need = OUT == OUT_ANY || !kp.with_pv || (SITES && wave_day);
+                if (!need && !SITES) {   // any daylight second among the four (scalar loads of their flags)
                     uint32_t nf = FL_NIGHT;
 #pragma unroll
                     for (int q = 0; q < 4; ++q)
@@ -3204,9 +3208,14 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
                        exp_grid(exp_wg<R, O, S>()), dim3(exp_wg<R, O, S>()), exp_lds(exp_hist_pack<R, O, S>()), s, \
                        eng->kp, eng->dp, v, chain0, n_chains, step0, n_steps,   \
                        utc0, pv.tab64, pv.tab32, pv.sun, pv.events, pv.n_events, pv.desc, sg, tv, sv)
-    if (eng->kp.sites) {   // per-chain sites: one instantiation per precision, any output
-        if (f64) LAUNCH(double, OUT_ANY, true);
-        else LAUNCH(float, OUT_ANY, true);
+    if (eng->kp.sites) {   // per-chain sites: statistics only (C5), or any output
+        if (f64) {
+            if (out == OUT_STATS) LAUNCH(double, OUT_STATS, true);
+            else LAUNCH(double, OUT_ANY, true);
+        } else {
+            if (out == OUT_STATS) LAUNCH(float, OUT_STATS, true);
+            else LAUNCH(float, OUT_ANY, true);
+        }
     } else if (f64) {
         if (out == OUT_TRACE3) LAUNCH(double, OUT_TRACE3, false);
         else if (out == OUT_STATS) LAUNCH(double, OUT_STATS, false);
@@ -3217,7 +3226,8 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
         else LAUNCH(float, OUT_ANY, false);
     }
 #undef LAUNCH
-    eng->last_expand = (eng->kp.sites ? (TMH_OUT_ANY | TMH_OUT_SITES) : out) | (f64 ? TMH_OUT_FP64 : 0);
+    eng->last_expand = (eng->kp.sites ? ((out == OUT_STATS ? TMH_OUT_STATS : TMH_OUT_ANY) | TMH_OUT_SITES) : out) |
+                       (f64 ? TMH_OUT_FP64 : 0);
     eng->close(TMH_K_EXPAND, t_exp, s);
     if (int rc = hip_check(hipGetLastError(), "expand_kernel launch")) return rc;
     }
