@@ -14,7 +14,7 @@ histograms with the oracle's (tmh_oracle.c), not with another GPU run:
     fp32 within 1e-5; and 64 chains x 60 days in 30-day windows (across the spring DST
     change) with every chain and the whole histogram against the oracle;
   * C5: 512 sites x 3 days (markov, per-site tables and sites, compacted windows, the
-    five-context group schedule), fp32 (1e-5) and fp64 (1e-12): every chain's
+    group schedule, eight contexts at this batch size), fp32 (1e-5) and fp64 (1e-12): every chain's
     energies and peak -- the faulted chains' seconds before their fault included --,
     status, and the histogram, whose count equals the oracle's chain-seconds, so
     energies and histogram cover the same chain-seconds (dist.chain_totals).
@@ -130,10 +130,22 @@ def test_c4_year_pipeline_shard_vs_oracle(n, lanes):
     cx = pipe.ctxs[0]
     pipe.sim.state = cx.state
     st = pipe.sim.status()
-    assert set(np.unique(st)) <= {0, 1}, np.unique(st)
     loc = C4_CONFIGS[(n, lanes)]
-    _check_chains(cx.acc[:, loc].cpu().numpy().T, st[loc], _c4_ref(loc), "fp32", f"c4 {n}/{lanes}")
-    assert int(cx.hist.sum()) == int((st == 0).sum()) * YEAR
+    acc = cx.acc.cpu().numpy().T
+    _check_chains(acc[loc], st[loc], _c4_ref(loc), "fp32", f"c4 {n}/{lanes}")
+    # a chain-year in faithful mode can end in the reference's AssertionError (20 + 20 rejected
+    # cloud lengths, cloud_cover_binary.py:90-98: 0.02 % of the N = 1 batch's chain-years);
+    # every chain faulting during the year is checked against the oracle too
+    odd = np.flatnonzero(~np.isin(st, (0, 1)))
+    assert set(np.unique(st[odd])) <= {2} and len(odd) <= n // 1000, (len(odd), np.unique(st))
+    if len(odd):
+        ref = O.run(ModelParams(), 0, len(odd), YEAR, Y0, tz=TZ, n_threads=16, outputs=(),
+                    stats=dict(HIST, amb_eps=AMB["fp32"]), chain_ids=odd.astype(np.uint64))
+        _check_chains(acc[odd], st[odd], ref, "fp32", f"c4 {n}/{lanes} faulted")
+    # the histogram counts every chain's seconds before its fault: the oracle's count for the
+    # faulted ones, a full year for the rest
+    want = int((st == 0).sum()) * YEAR + (int(ref["hist"].sum()) if len(odd) else 0)
+    assert int(cx.hist.sum()) == want
 
 
 def test_c4_thirty_day_windows_every_chain_vs_oracle():
@@ -169,8 +181,8 @@ def _c5_oracle(chain0, prec):
 @pytest.mark.parametrize("prec", ["fp32", "fp64"])
 def test_c5_pipeline_vs_oracle(prec):
     """bench.py's C5 schedule (pipeline_defaults("c5"): markov cc, per-site tables and
-    sites, day windows compacted to the live chains, five batches advanced window by
-    window together): contexts 0 and 4 against the oracle -- every chain's energies and
+    sites, day windows compacted to the live chains, the batches of every context advanced
+    window by window together): the first and the last context against the oracle -- every chain's energies and
     peak (faulted chains' seconds before the fault included), status (a quarter or more
     of the chains fault: the reference's AssertionError), and the histogram, whose count
     equals the oracle's count of those chain-seconds."""
@@ -178,7 +190,8 @@ def test_c5_pipeline_vs_oracle(prec):
     tables, sites = _c5_inputs()
     pipe = _pipeline("c5", C5_N, C5_SECS, C5_START, prec=prec, chain0=C5_CHAIN0, lanes=16,
                      mp=ModelParams(cc_mode=CC_MARKOV), shape_tables=tables, sites=sites)
-    assert pipe.cfg.compact and pipe.cfg.window == 86400 and len(pipe.ctxs) == 5
+    # a 512-site batch is below the one-GPU C5 batch: pipeline_defaults keeps more contexts in flight
+    assert pipe.cfg.compact and pipe.cfg.window == 86400 and len(pipe.ctxs) == pipe.cfg.pipeline >= 5
     for ci in (0, len(pipe.ctxs) - 1):
         cx = pipe.ctxs[ci]
         ref = _c5_oracle(C5_CHAIN0 + ci * C5_N, prec)

@@ -1767,6 +1767,12 @@ __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t rs, uint32_t of
 #ifndef TMH_EXP_WG_STATS
 #define TMH_EXP_WG_STATS 512
 #endif
+#ifndef TMH_ROW_LDS
+#define TMH_ROW_LDS 0   // fp32 single-site expansion: the tile's geometry rows staged in LDS (A/B builds)
+#endif
+#ifndef TMH_ROW_LDS_WAVES
+#define TMH_ROW_LDS_WAVES 6
+#endif
 #ifndef TMH_EXP_TILE_ORDER
 #define TMH_EXP_TILE_ORDER 1   // expand_kernel: XCD-aware tile order (0: launch order)
 #endif
@@ -1796,7 +1802,7 @@ constexpr int exp_waves()
 #ifndef TMH_EXP_WAVES_F64
 #define TMH_EXP_WAVES_F64 4
 #endif
-    return SITES ? 2 : (sizeof(R) == 8 ? TMH_EXP_WAVES_F64 : (OUT == OUT_TRACE3 ? 7 : 6));
+    return SITES ? 2 : (sizeof(R) == 8 ? TMH_EXP_WAVES_F64 : (OUT == OUT_TRACE3 ? (TMH_ROW_LDS ? TMH_ROW_LDS_WAVES : 7) : 6));
 }
 // One (128-second block b, chain block cblk) tile of the expansion: one work-item per
 // chain of the block (the expansion's unit of work, below).  The LDS staging areas are
@@ -1810,8 +1816,11 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
                                             const BlockDesc* __restrict__ desc, const SegView& sg,
                                             const TraceView& tr, const StatsView& sv, uint32_t* lds_hist,
                                             uint32_t (*cov_lds)[WGT], R (*min_lds)[WGT], uint4* held_lds,
-                                            const PV64* pv_lds, const double* pv_lds_tab)
+                                            const PV64* pv_lds, const double* pv_lds_tab, float* row_lds)
 {
+    // TMH_ROW_LDS: the tile's fp32 geometry rows copied to LDS once (coalesced vector loads),
+    // read back per second with broadcast ds_reads instead of per-second scalar loads
+    constexpr bool ROWL = TMH_ROW_LDS && sizeof(R) == 4 && !SITES;
     const uint32_t c = cblk * blockDim.x + threadIdx.x;
     const bool live = c < n;
     const uint32_t j0 = b * BLOCK_STEPS, j1 = min(j0 + (uint32_t)BLOCK_STEPS, nsteps);
@@ -1913,6 +1922,12 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
     constexpr int RW = sizeof(R) == 8 ? ROW : ROW32;   // geometry row: wave-uniform, scalar loads
     const R* rowp = (sizeof(R) == 8 ? reinterpret_cast<const R*>(tab64) : reinterpret_cast<const R*>(tab32)) +
                     (size_t)j0 * RW;
+    if constexpr (ROWL) {
+        const uint32_t nw = (j1 - j0) * ROW32;
+        const float* src = tab32 + (size_t)j0 * ROW32;
+        for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) row_lds[i] = src[i];
+        __syncthreads();
+    }
     __amdgpu_buffer_rsrc_t rs_pv, rs_m, rs_r;
     uint32_t voff = live ? c * (uint32_t)sizeof(R) : 0x80000000u;
     const uint32_t rowb = (uint32_t)(tr.ld * sizeof(R));
@@ -1939,10 +1954,18 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
     auto second = [&](uint32_t j, uint32_t un, uint32_t um, auto ff) __attribute__((always_inline)) {
         constexpr bool FF = decltype(ff)::value;
         R row[row_w<R>()];
+        uint32_t fl;
+        if constexpr (ROWL) {
+            const float* lr = row_lds + (j - j0) * ROW32;
 #pragma unroll
-        for (int i = 0; i < row_w<R>(); ++i) row[i] = rowp[i];
-        rowp += RW;
-        const uint32_t fl = sizeof(R) == 8 ? (uint32_t)(double)rowp[G_FLAGS - RW] : __float_as_uint(row[G_FLAGS + G32]);
+            for (int i = 0; i < ROW32; ++i) row[i] = lr[i];
+            fl = __builtin_amdgcn_readfirstlane(__float_as_uint(row[G_FLAGS + G32]));
+        } else {
+#pragma unroll
+            for (int i = 0; i < row_w<R>(); ++i) row[i] = rowp[i];
+            rowp += RW;
+            fl = sizeof(R) == 8 ? (uint32_t)(double)rowp[G_FLAGS - RW] : __float_as_uint(row[G_FLAGS + G32]);
+        }
         const bool ok = FF || (int32_t)j < fault_eff;
         if (fl & (FL_DAY | FL_HOUR)) {            // _next_day, _next_hour (rare: loads waited here)
             const size_t eo = (size_t)evi * 4 * n;
@@ -2050,10 +2073,16 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
                 bool need = OUT == OUT_ANY || !kp.with_pv || (SITES && wave_day);
                 if (!need && !SITES) {   // any daylight second among the four (scalar loads of their flags)
                     uint32_t nf = FL_NIGHT;
+                    if constexpr (ROWL) {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        nf &= sizeof(R) == 8 ? (uint32_t)(double)rowp[q * RW + G_FLAGS]
-                                             : __float_as_uint((float)rowp[q * RW + G_FLAGS + G32]);
+                        for (int q = 0; q < 4; ++q) nf &= __float_as_uint(row_lds[(j - j0 + q) * ROW32 + G_FLAGS + G32]);
+                        nf = __builtin_amdgcn_readfirstlane(nf);
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            nf &= sizeof(R) == 8 ? (uint32_t)(double)rowp[q * RW + G_FLAGS]
+                                                 : __float_as_uint((float)rowp[q * RW + G_FLAGS + G32]);
+                    }
                     need = nf == 0;
                 }
                 U4 pn{0u, 0u, 0u, 0u};
@@ -2116,6 +2145,7 @@ __global__ __launch_bounds__((exp_wg<R, OUT, SITES>()), (exp_waves<R, OUT, SITES
     // fp64: the PV constants; fp64 and per-chain sites: the log / exp table (one copy per workgroup)
     __shared__ PV64 pv_lds[1];   // (176 + 16 bytes in the fp32 kernels: unused)
     __shared__ __attribute__((aligned(16))) double pv_tab[sizeof(R) == 8 || SITES ? PV_TAB : 2];
+    __shared__ __attribute__((aligned(16))) float row_lds[TMH_ROW_LDS && sizeof(R) == 4 && !SITES ? BLOCK_STEPS * ROW32 : 1];
     if constexpr (sizeof(R) == 8 || SITES) {
         if (threadIdx.x < PV64_N) reinterpret_cast<double*>(pv_lds)[threadIdx.x] = reinterpret_cast<const double*>(&kp.pv64)[threadIdx.x];
         for (uint32_t i = threadIdx.x; i < PV_TAB; i += blockDim.x) pv_tab[i] = g_pv_tab[i];
@@ -2129,7 +2159,8 @@ __global__ __launch_bounds__((exp_wg<R, OUT, SITES>()), (exp_waves<R, OUT, SITES
     }
     auto tile = [&](uint32_t b, uint32_t cblk) __attribute__((always_inline)) {
         expand_tile<R, OUT, SITES, WGT>(b, cblk, kp, dp, st, chain0, n, W0, nsteps, utc0, tab64, tab32, sun, events,
-                                        n_events, desc, sg, tr, sv, lds_hist, cov_lds, min_lds, held_lds, pv_lds, pv_tab);
+                                        n_events, desc, sg, tr, sv, lds_hist, cov_lds, min_lds, held_lds, pv_lds, pv_tab,
+                                        row_lds);
     };
     {   // grid: x = time block, y = chain block; XCD-aware tile order (speed only): the
         // hardware deals workgroups round-robin over the 8 XCDs in launch order (x fastest),
