@@ -1783,10 +1783,20 @@ constexpr int exp_wg()
 }
 // the LDS histogram as 16-bit bin pairs when one tile (WG chains x 128 s) cannot fill a
 // 16-bit bin, else one 32-bit word per bin
+// time blocks per workgroup: the statistics-only single-site expansion (C3, C4) may loop over
+// TMH_STATS_TPW consecutive blocks, one histogram flush for all of them (A/B builds)
+#ifndef TMH_STATS_TPW
+#define TMH_STATS_TPW 1
+#endif
+template <typename R, int OUT, bool SITES>
+constexpr int exp_tpw()
+{
+    return OUT == OUT_STATS && !SITES ? TMH_STATS_TPW : 1;
+}
 template <typename R, int OUT, bool SITES>
 constexpr bool exp_hist_pack()
 {
-    return exp_wg<R, OUT, SITES>() * BLOCK_STEPS <= 32768;
+    return exp_wg<R, OUT, SITES>() * BLOCK_STEPS * exp_tpw<R, OUT, SITES>() <= 32768;
 }
 constexpr int PVF_VGPR = 0;   // leading PVF fields pinned in VGPRs in the fp32 single-site expansion
 // min waves per SIMD (__launch_bounds__) of each expansion instantiation:
@@ -2177,11 +2187,24 @@ __global__ __launch_bounds__((exp_wg<R, OUT, SITES>()), (exp_waves<R, OUT, SITES
         const uint32_t m = k / CB, qt = T >> 3, rt = T & 7u, big = rt * (qt + 1);
         const uint32_t xm = m < big ? m / (qt + 1) : rt + (m - big) / max(qt, 1u);
         const uint32_t b = xm + 8u * (m - (xm * qt + min(xm, rt)));
-#if TMH_EXP_TILE_ORDER
-        tile(b, k % CB);
+#if !TMH_EXP_TILE_ORDER
+        const uint32_t bs = blockIdx.x, cs = blockIdx.y;   // launch order (A/B builds)
 #else
-        tile(blockIdx.x, blockIdx.y);   // launch order (A/B builds)
+        // (uniform, but computed by VALU integer division: readfirstlane keeps them in SGPRs, so
+        // the row pointer and the tile's block loads stay scalar)
+        const uint32_t bs = __builtin_amdgcn_readfirstlane(b), cs = __builtin_amdgcn_readfirstlane(k % CB);
 #endif
+        constexpr int TPW = exp_tpw<R, OUT, SITES>();
+        if constexpr (TPW == 1) tile(bs, cs);
+        else {   // time blocks bs TPW .. bs TPW + TPW - 1 (x counts super-blocks of TPW blocks)
+            for (int t = 0; t < TPW; ++t) {
+                // laundered per tile: nothing of a tile is hoisted out of the loop and held in
+                // registers across it (the per-chain loads are repeated instead)
+                uint32_t bb = bs * TPW + t, cc = cs;
+                asm volatile("" : "+s"(bb), "+s"(cc));
+                if (bb < sg.nblk) tile(bb, cc);
+            }
+        }
     }
     if (sv.hist) {
         __syncthreads();
@@ -3224,22 +3247,27 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     if (phases & PH_EXPAND) {
     hipEvent_t t_exp = eng->mark(s);
     const bool no_stats = !sv.hist && !sv.acc;
-    const int out = (no_stats && tv.pv && tv.meter && tv.residual && !tv.csi && !tv.covered) ? OUT_TRACE3
+    int out = (no_stats && tv.pv && tv.meter && tv.residual && !tv.csi && !tv.covered) ? OUT_TRACE3
                     : (!tv.pv && !tv.meter && !tv.residual && !tv.csi && !tv.covered) ? OUT_STATS
                                                                                       : OUT_ANY;
     const size_t hist_bins = stats && stats->hist ? stats->n_bins : 0;
     // x = time blocks, y = chain blocks; LDS: the histogram (16-bit bin pairs or bins)
-    auto exp_grid = [&](uint32_t wg) { return dim3(sg.nblk, (n_chains + wg - 1) / wg); };
+    auto exp_grid = [&](uint32_t wg, uint32_t tpw) { return dim3((sg.nblk + tpw - 1) / tpw, (n_chains + wg - 1) / wg); };
     auto exp_lds = [&](bool pack) { return pack ? (hist_bins + 1) / 2 * 4 : hist_bins * 4; };
     if (out == OUT_TRACE3 && tv.ld * (f64 ? 8u : 4u) * BLOCK_STEPS >= (1ull << 31))   // one block's rows: one buffer range
         return fail(TMH_E_INVAL, "trace ld %llu too large (a 128-step block of rows must stay under 2 GiB)",
                     (unsigned long long)tv.ld);
 #define LAUNCH(R, O, S)                                                                                            \
     hipLaunchKernelGGL((expand_kernel<R, O, S>),                                                                   \
-                       exp_grid(exp_wg<R, O, S>()), dim3(exp_wg<R, O, S>()), exp_lds(exp_hist_pack<R, O, S>()), s, \
+                       exp_grid(exp_wg<R, O, S>(), exp_tpw<R, O, S>()), dim3(exp_wg<R, O, S>()),                 \
+                       exp_lds(exp_hist_pack<R, O, S>()), s,                                                      \
                        eng->kp, eng->dp, v, chain0, n_chains, step0, n_steps,   \
                        utc0, pv.tab64, pv.tab32, pv.sun, pv.events, pv.n_events, pv.desc, sg, tv, sv)
+#ifndef TMH_SITES_STATS
+#define TMH_SITES_STATS 1   // per-chain sites: the statistics-only instantiation (0: OUT_ANY for every output, A/B)
+#endif
     if (eng->kp.sites) {   // per-chain sites: statistics only (C5), or any output
+        if (!TMH_SITES_STATS && out == OUT_STATS) out = OUT_ANY;
         if (f64) {
             if (out == OUT_STATS) LAUNCH(double, OUT_STATS, true);
             else LAUNCH(double, OUT_ANY, true);

@@ -1151,8 +1151,16 @@ __device__ __forceinline__ bool lane_row(LaneSite& ls, const double* sun, const 
         tl = ls.tl;
     }
     double g[ROW];
+#ifndef TMH_HA_ROTATE
+#define TMH_HA_ROTATE 1   // 0: a sincos per chain-second (A/B builds)
+#endif
+#if TMH_HA_ROTATE
     const double sdh = sun[SUN_SDH], cdh = sun[SUN_CDH];
     const double sha = fma(ls.s0, cdh, ls.c0 * sdh), cha = fma(ls.c0, cdh, -(ls.s0 * sdh));
+#else
+    double sha, cha;
+    sincos_pi(hour_angle(ls.k, sun), &sha, &cha);
+#endif
     if (site_geom_hc<false, sizeof(R) == 4>(ls.k, sun, tl, module, g, t, sha, cha)) return true;
     site_row<R>(g, sun, row);
     return g[G_GHICS] == 0.0;
