@@ -1774,7 +1774,7 @@ __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t rs, uint32_t of
 #define TMH_ROW_LDS_WAVES 6
 #endif
 #ifndef TMH_EXP_TILE_ORDER
-#define TMH_EXP_TILE_ORDER 1   // expand_kernel: XCD-aware tile order (0: launch order)
+#define TMH_EXP_TILE_ORDER 0   // expand_kernel tile order: 0 launch order, 1 / 2 XCD-aware (A/B builds)
 #endif
 template <typename R, int OUT, bool SITES>
 constexpr int exp_wg()
@@ -2187,8 +2187,20 @@ __global__ __launch_bounds__((exp_wg<R, OUT, SITES>()), (exp_waves<R, OUT, SITES
         const uint32_t m = k / CB, qt = T >> 3, rt = T & 7u, big = rt * (qt + 1);
         const uint32_t xm = m < big ? m / (qt + 1) : rt + (m - big) / max(qt, 1u);
         const uint32_t b = xm + 8u * (m - (xm * qt + min(xm, rt)));
-#if !TMH_EXP_TILE_ORDER
+#if TMH_EXP_TILE_ORDER == 0
         const uint32_t bs = blockIdx.x, cs = blockIdx.y;   // launch order (A/B builds)
+#elif TMH_EXP_TILE_ORDER == 2
+        // order 2: the tiles listed class by class (time blocks b = x mod 8), chain block major
+        // inside a class (consecutive workgroups of an XCD: different time blocks, as in launch
+        // order, so the trace rows written at a time spread over the HBM channels); XCD x's
+        // contiguous range of that list is (nearly) class x: 1/8 of the rows per L2
+        const uint32_t kbig = big * CB;   // tiles of the rt classes with qt + 1 blocks
+        const uint32_t x2 = k < kbig ? k / (CB * (qt + 1)) : rt + (k - kbig) / max(CB * qt, 1u);
+        const uint32_t cum = x2 <= rt ? x2 * CB * (qt + 1) : kbig + (x2 - rt) * CB * qt;
+        const uint32_t nbx = qt + (x2 < rt ? 1u : 0u), i2 = k - cum;
+        const uint32_t bs = __builtin_amdgcn_readfirstlane(x2 + 8u * (i2 % nbx)),
+                       cs = __builtin_amdgcn_readfirstlane(i2 / nbx);
+        (void)b;
 #else
         // (uniform, but computed by VALU integer division: readfirstlane keeps them in SGPRs, so
         // the row pointer and the tile's block loads stay scalar)
