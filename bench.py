@@ -470,6 +470,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    t0ev = None
+    if args.timeline:   # the timed region's start on the GPU clock (the pipeline fill is measured from it)
+        t0ev = torch.cuda.Event(enable_timing=True)
+        t0ev.record()
     run_batches(args.warmup, args.steps)
     tot = exchange() if args.mode == "stats" else None
     torch.cuda.synchronize()
@@ -602,7 +606,14 @@ def main():
         late = [tl["exp1"][k].elapsed_time(tl["walk1"][k + 1]) for k in ks if k + 1 in tl.get("walk1", {})]
         wdur = [tl["walk0"][k].elapsed_time(tl["walk1"][k]) for k in ks if k in tl.get("walk0", {})]
         bwait = [tl["built"][k].elapsed_time(tl["walk0"][k]) for k in ks if k in tl.get("built", {}) and k in tl.get("walk0", {})]
-        line["timeline"] = {"expansion_gap_ms": gaps, "walk_end_after_prev_expansion_ms": late,
+        k0 = args.warmup
+        fill = {}
+        for key, name in (("built", "first_build_done_ms"), ("walk0", "first_walk_start_ms"),
+                          ("walk1", "first_walk_end_ms"), ("exp0", "first_expansion_start_ms"),
+                          ("exp1", "first_expansion_end_ms")):
+            if k0 in tl.get(key, {}):
+                fill[name] = t0ev.elapsed_time(tl[key][k0])
+        line["timeline"] = {"fill": fill, "expansion_gap_ms": gaps, "walk_end_after_prev_expansion_ms": late,
                             "walk_ms": wdur, "walk_start_after_build_ms": bwait}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args, kw)

@@ -1083,7 +1083,7 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
                 }
             }
         }
-        if (live) emit<R>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok);
+        if (live) emit<R, OUT_ANY | OUT_BRT>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter, res, acc, ok);
     }
     if (live) {
         store_chain(st, c, ch);
@@ -1779,7 +1779,7 @@ __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t rs, uint32_t of
 template <typename R, int OUT, bool SITES>
 constexpr int exp_wg()
 {
-    return OUT == OUT_STATS && !SITES ? TMH_EXP_WG_STATS : 256;
+    return out_base(OUT) == OUT_STATS && !SITES ? TMH_EXP_WG_STATS : 256;
 }
 // the LDS histogram as 16-bit bin pairs when one tile (WG chains x 128 s) cannot fill a
 // 16-bit bin, else one 32-bit word per bin
@@ -1791,7 +1791,7 @@ constexpr int exp_wg()
 template <typename R, int OUT, bool SITES>
 constexpr int exp_tpw()
 {
-    return OUT == OUT_STATS && !SITES ? TMH_STATS_TPW : 1;
+    return out_base(OUT) == OUT_STATS && !SITES ? TMH_STATS_TPW : 1;
 }
 template <typename R, int OUT, bool SITES>
 constexpr bool exp_hist_pack()
@@ -1812,7 +1812,7 @@ constexpr int exp_waves()
 #ifndef TMH_EXP_WAVES_F64
 #define TMH_EXP_WAVES_F64 4
 #endif
-    return SITES ? 2 : (sizeof(R) == 8 ? TMH_EXP_WAVES_F64 : (OUT == OUT_TRACE3 ? (TMH_ROW_LDS ? TMH_ROW_LDS_WAVES : 7) : 6));
+    return SITES ? 2 : (sizeof(R) == 8 ? TMH_EXP_WAVES_F64 : (out_base(OUT) == OUT_TRACE3 ? (TMH_ROW_LDS ? TMH_ROW_LDS_WAVES : 7) : 6));
 }
 // One (128-second block b, chain block cblk) tile of the expansion: one work-item per
 // chain of the block (the expansion's unit of work, below).  The LDS staging areas are
@@ -1941,7 +1941,7 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
     __amdgpu_buffer_rsrc_t rs_pv, rs_m, rs_r;
     uint32_t voff = live ? c * (uint32_t)sizeof(R) : 0x80000000u;
     const uint32_t rowb = (uint32_t)(tr.ld * sizeof(R));
-    if constexpr (OUT == OUT_TRACE3) {
+    if constexpr (out_base(OUT) == OUT_TRACE3) {
         const size_t bo = (size_t)j0 * tr.ld * sizeof(R);
         const int nb = (int)((j1 - j0) * rowb);
         rs_pv = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(tr.pv) + bo, 0, nb, 0x00020000);
@@ -2022,7 +2022,7 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
         }
         R csi, pv, meter, res;
         bool held = false;   // fp32: PV in a guard band, recomputed in fp64 by fixup_kernel
-        if (OUT != OUT_ANY && (!kp.with_pv || (flp & FL_NIGHT))) {
+        if (out_base(OUT) != OUT_ANY && (!kp.with_pv || (flp & FL_NIGHT))) {
             // the CSI is not an output (trace of pv / meter / residual, or statistics) and
             // pv = 0 whatever it is (second_body: night, or no PV): no noise quantile, no
             // samplers, no PV chain; the same values.  Wave-uniform for a single site.
@@ -2059,7 +2059,7 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
             res = ok ? res : R(NAN);
         }
         const uint8_t cov = ok ? (covered ? 1 : 0) : 255;
-        if constexpr (OUT == OUT_TRACE3) {
+        if constexpr (out_base(OUT) == OUT_TRACE3) {
             row_store(rs_pv, voff, pv);
             row_store(rs_m, voff, meter);
             row_store(rs_r, voff, res);
@@ -2080,7 +2080,7 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
             for (; j + 4 <= j1; j += 4) {
                 const uint64_t g = (uint64_t)(W0 + j) >> 2;
                 const U4 pm = keyed_block(kp.seed, chain, g, TAG_METER4, 0);
-                bool need = OUT == OUT_ANY || !kp.with_pv || (SITES && wave_day);
+                bool need = out_base(OUT) == OUT_ANY || !kp.with_pv || (SITES && wave_day);
                 if (!need && !SITES) {   // any daylight second among the four (scalar loads of their flags)
                     uint32_t nf = FL_NIGHT;
                     if constexpr (ROWL) {
@@ -2348,7 +2348,7 @@ __global__ __launch_bounds__(256) void fixup_kernel(KParams kp, DrawParams dp, S
             __hip_atomic_fetch_max(sg.acc_mx + c, max_key((double)res), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (sv.hist) {
-            atomicAdd((unsigned long long*)&sv.hist[hist_bin<float>(sv, res)], 1ull);
+            atomicAdd((unsigned long long*)&sv.hist[hist_bin_rt<float>(sv, res)], 1ull);
         }
     }
 }
@@ -3278,11 +3278,17 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
 #ifndef TMH_SITES_STATS
 #define TMH_SITES_STATS 1   // per-chain sites: the statistics-only instantiation (0: OUT_ANY for every output, A/B)
 #endif
+    // fp32 kernels and a histogram spec their fp32 binning cannot resolve (StatsView::bin64):
+    // the OUT_B64 instantiations bin in fp64 (no per-second branch in the others)
+    const bool b64 = !f64 && sv.hist && sv.bin64;
     if (eng->kp.sites) {   // per-chain sites: statistics only (C5), or any output
         if (!TMH_SITES_STATS && out == OUT_STATS) out = OUT_ANY;
         if (f64) {
             if (out == OUT_STATS) LAUNCH(double, OUT_STATS, true);
             else LAUNCH(double, OUT_ANY, true);
+        } else if (b64) {
+            if (out == OUT_STATS) LAUNCH(float, OUT_STATS | OUT_B64, true);
+            else LAUNCH(float, OUT_ANY | OUT_B64, true);
         } else {
             if (out == OUT_STATS) LAUNCH(float, OUT_STATS, true);
             else LAUNCH(float, OUT_ANY, true);
@@ -3291,6 +3297,9 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
         if (out == OUT_TRACE3) LAUNCH(double, OUT_TRACE3, false);
         else if (out == OUT_STATS) LAUNCH(double, OUT_STATS, false);
         else LAUNCH(double, OUT_ANY, false);
+    } else if (b64) {
+        if (out == OUT_STATS) LAUNCH(float, OUT_STATS | OUT_B64, false);
+        else LAUNCH(float, OUT_ANY | OUT_B64, false);
     } else {
         if (out == OUT_TRACE3) LAUNCH(float, OUT_TRACE3, false);
         else if (out == OUT_STATS) LAUNCH(float, OUT_STATS, false);

@@ -141,15 +141,23 @@ struct StatsView {
 // bins.  The host (step_phases) sets bin64 when that bound exceeds 1e-3 bins (a narrow
 // range far from 0, very many bins): such a spec is binned in fp64 like the fp64 kernels
 // (a scalar branch per second, taken the same way by every wave).
-template <typename R>
+// B64: bin in fp64 (the fp64 kernels; fp32 kernels built for a bin64 spec, OUT_B64); the
+// per-second loops take the choice at compile time, hist_bin_rt (the fixup, the sequential
+// kernel) at run time
+template <typename R, bool B64 = (sizeof(R) == 8)>
 __device__ __forceinline__ int hist_bin(const StatsView& sv, R res)
 {
-    if (sizeof(R) == 8 || sv.bin64) {
+    if constexpr (sizeof(R) == 8 || B64) {
         const double x = ((double)res - sv.lo) * sv.scale;
         return x < 0.0 ? 0 : (x >= (double)(sv.n_bins - 1) ? (int)sv.n_bins - 1 : (int)x);
     } else {
         return (int)__builtin_amdgcn_fmed3f(fmaf((float)res, sv.scale_f, sv.off_f), 0.0f, (float)(sv.n_bins - 1));
     }
+}
+template <typename R>
+__device__ __forceinline__ int hist_bin_rt(const StatsView& sv, R res)
+{
+    return sv.bin64 ? hist_bin<R, true>(sv, res) : hist_bin<R>(sv, res);
 }
 
 struct Samp {
@@ -1197,9 +1205,13 @@ __device__ __forceinline__ PP lds_fence(PP p)
     }
 }
 
-// Every a * b + c of the chain is one fma in pvmodel.py's order of operations (the summations
-// keep their order, each product enters exactly): an fp64 rounding fewer per pair, within
-// 1e-16 relative of the separate multiply and add (the kernels build with -ffp-contract=off).
+// The a * b + c of the chain after DISC's polynomials are one fma each, in pvmodel.py's order
+// of operations (the summations keep their order, each product enters exactly): an fp64
+// rounding fewer per pair, within 1e-16 relative of the separate multiply and add (the
+// kernels build with -ffp-contract=off); fp64 C2 trace loop -5 % VALU.  DISC's polynomials
+// keep the multiply-add form: fused as well, the trace kernel took 122 VGPRs instead of 110,
+// i.e. two waves per SIMD beside a 146-VGPR walk wave instead of three (measured: alone
+// 2.74 against 2.89 ms, in the pipeline 3.05 against 2.94 ms).
 template <typename PP, typename LT>
 __device__ __forceinline__ double pv_power_d(PP p, const double* g, double csi, LT lt)
 {
@@ -1211,13 +1223,13 @@ __device__ __forceinline__ double pv_power_d(PP p, const double* g, double csi, 
     const double am = g[G_AM], kt2 = kt * kt, kt3 = kt2 * kt;
     double a, b, cc;
     if (kt <= 0.6) {
-        a = fma(-2.222, kt3, fma(2.286, kt2, fma(-1.56, kt, 0.512)));
-        b = fma(0.962, kt, 0.37);
-        cc = fma(-2.048, kt2, fma(0.932, kt, -0.28));
+        a = 0.512 - 1.56 * kt + 2.286 * kt2 - 2.222 * kt3;
+        b = 0.37 + 0.962 * kt;
+        cc = -0.28 + 0.932 * kt - 2.048 * kt2;
     } else {
-        a = fma(11.56, kt3, fma(-27.49, kt2, fma(21.77, kt, -5.743)));
-        b = fma(31.9, kt3, fma(66.05, kt2, fma(-118.5, kt, 41.4)));
-        cc = fma(73.81, kt3, fma(-222.0, kt2, fma(184.2, kt, -47.01)));
+        a = -5.743 + 21.77 * kt - 27.49 * kt2 + 11.56 * kt3;
+        b = 41.4 - 118.5 * kt + 66.05 * kt2 + 31.9 * kt3;
+        cc = -47.01 + 184.2 * kt - 222.0 * kt2 + 73.81 * kt3;
     }
     double ex;
     if constexpr (__is_same(LT, decltype(nullptr))) ex = exp_tab(cc * am, (const double*)g_pv_tab);
@@ -1465,8 +1477,12 @@ struct Acc {
 enum : int {
     OUT_ANY = 0,      // any combination of trace fields and statistics
     OUT_TRACE3 = 1,   // exactly pv, meter, residual traces (the trace-mode hot path)
-    OUT_STATS = 2     // statistics only, no trace
+    OUT_STATS = 2,    // statistics only, no trace
+    // flags on OUT_ANY / OUT_STATS (fp32 kernels): OUT_B64 bins in fp64 (a histogram spec whose
+    // fp32 bin position is not accurate enough, StatsView::bin64); OUT_BRT decides at run time
+    OUT_B64 = 8, OUT_BRT = 16
 };
+constexpr int out_base(int out) { return out & 7; }
 
 // held: a guard-band second whose pv / residual fixup_kernel replaces; it enters
 // the sums here (fixup_kernel adds the exact difference) but not the maximum or
@@ -1477,13 +1493,13 @@ template <typename R, int OUT = OUT_ANY, bool PACK = false>
 __device__ __forceinline__ void emit(const TraceView& tr, const StatsView& sv, uint32_t* lds_hist, uint64_t o,
                                      uint8_t cov, R csi, R pv, R meter, R res, Acc& acc, bool ok, bool held = false)
 {
-    if constexpr (OUT == OUT_TRACE3) {
+    if constexpr (out_base(OUT) == OUT_TRACE3) {
         __builtin_nontemporal_store(pv, reinterpret_cast<R*>(tr.pv) + o);
         __builtin_nontemporal_store(meter, reinterpret_cast<R*>(tr.meter) + o);
         __builtin_nontemporal_store(res, reinterpret_cast<R*>(tr.residual) + o);
         return;
     }
-    if constexpr (OUT == OUT_ANY) {
+    if constexpr (out_base(OUT) == OUT_ANY) {
         trace_store<R>(tr.csi, o, csi);
         trace_store<R>(tr.pv, o, pv);
         trace_store<R>(tr.meter, o, meter);
@@ -1498,7 +1514,7 @@ __device__ __forceinline__ void emit(const TraceView& tr, const StatsView& sv, u
             if (!held) acc.mx = fmax(acc.mx, (double)res);
         }
         if (sv.hist && !held) {
-            const int bin = hist_bin<R>(sv, res);
+            const int bin = (OUT & OUT_BRT) ? hist_bin_rt<R>(sv, res) : hist_bin<R, sizeof(R) == 8 || (OUT & OUT_B64) != 0>(sv, res);
             if constexpr (PACK) atomicAdd(&lds_hist[bin >> 1], 1u << ((bin & 1) << 4));
             else atomicAdd(&lds_hist[bin], 1u);
         }
