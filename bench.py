@@ -279,6 +279,9 @@ def parse():
 
 SECONDARY = {   # --secondary: the other BASELINE.json configs, each in a child process of its own
     "c2_fp64": ["--precision", "fp64", "--steps", "10", "--warmup", "3"],
+    # the headline at HIP's default of 4 hardware queues (the pipelines' streams have queues of
+    # their own, PipelineConfig.queues = "dedicated": no result depends on GPU_MAX_HW_QUEUES)
+    "c2_q4": ["--hw-queues", "4", "--steps", "20", "--warmup", "5"],
     "c3": ["--workload", "c3", "--steps", "4", "--warmup", "1"],
     # C4 / C5 at N = 1 keep 3 / 5 batches in flight: whole rounds of them (6 / 5 timed batches)
     "c4": ["--workload", "c4", "--steps", "6", "--warmup", "1"],
@@ -305,7 +308,7 @@ def secondary_lines(args):
         if args.secondary != "all" and name not in args.secondary.split(","):
             continue
         cmd = [sys.executable, os.path.abspath(__file__), "--no-cpu-baseline", "--secondary", "none"] + extra
-        if getattr(args, "hw_queues_given", False):
+        if getattr(args, "hw_queues_given", False) and "--hw-queues" not in extra:
             cmd += ["--hw-queues", str(args.hw_queues)]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
