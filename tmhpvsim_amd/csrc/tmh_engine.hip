@@ -1773,9 +1773,19 @@ __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t rs, uint32_t of
 #ifndef TMH_ROW_LDS_WAVES
 #define TMH_ROW_LDS_WAVES 6
 #endif
-#ifndef TMH_EXP_TILE_ORDER
-#define TMH_EXP_TILE_ORDER 0   // expand_kernel tile order: 0 launch order, 1 / 2 XCD-aware (A/B builds)
+// expand_kernel's tile order: 0 launch order, 1 / 2 XCD-aware (below).  Order 1 for the
+// per-site kernels (C5: 4.20 against 3.995e10 live chain-s/s, same box), launch order for
+// the rest (C2: order 1 2.17 against 2.39e11); TMH_EXP_TILE_ORDER sets one order for every
+// instantiation (A/B builds).
+template <typename R, int OUT, bool SITES>
+constexpr int exp_tile_order()
+{
+#ifdef TMH_EXP_TILE_ORDER
+    return TMH_EXP_TILE_ORDER;
+#else
+    return SITES ? 1 : 0;
 #endif
+}
 template <typename R, int OUT, bool SITES>
 constexpr int exp_wg()
 {
@@ -2187,25 +2197,30 @@ __global__ __launch_bounds__((exp_wg<R, OUT, SITES>()), (exp_waves<R, OUT, SITES
         const uint32_t m = k / CB, qt = T >> 3, rt = T & 7u, big = rt * (qt + 1);
         const uint32_t xm = m < big ? m / (qt + 1) : rt + (m - big) / max(qt, 1u);
         const uint32_t b = xm + 8u * (m - (xm * qt + min(xm, rt)));
-#if TMH_EXP_TILE_ORDER == 0
-        const uint32_t bs = blockIdx.x, cs = blockIdx.y;   // launch order (A/B builds)
-#elif TMH_EXP_TILE_ORDER == 2
-        // order 2: the tiles listed class by class (time blocks b = x mod 8), chain block major
-        // inside a class (consecutive workgroups of an XCD: different time blocks, as in launch
-        // order, so the trace rows written at a time spread over the HBM channels); XCD x's
-        // contiguous range of that list is (nearly) class x: 1/8 of the rows per L2
-        const uint32_t kbig = big * CB;   // tiles of the rt classes with qt + 1 blocks
-        const uint32_t x2 = k < kbig ? k / (CB * (qt + 1)) : rt + (k - kbig) / max(CB * qt, 1u);
-        const uint32_t cum = x2 <= rt ? x2 * CB * (qt + 1) : kbig + (x2 - rt) * CB * qt;
-        const uint32_t nbx = qt + (x2 < rt ? 1u : 0u), i2 = k - cum;
-        const uint32_t bs = __builtin_amdgcn_readfirstlane(x2 + 8u * (i2 % nbx)),
-                       cs = __builtin_amdgcn_readfirstlane(i2 / nbx);
-        (void)b;
-#else
-        // (uniform, but computed by VALU integer division: readfirstlane keeps them in SGPRs, so
-        // the row pointer and the tile's block loads stay scalar)
-        const uint32_t bs = __builtin_amdgcn_readfirstlane(b), cs = __builtin_amdgcn_readfirstlane(k % CB);
-#endif
+        constexpr int ORD = exp_tile_order<R, OUT, SITES>();
+        uint32_t bs, cs;
+        if constexpr (ORD == 0) {   // launch order
+            bs = blockIdx.x;
+            cs = blockIdx.y;
+            (void)b;
+        } else if constexpr (ORD == 2) {
+            // order 2: the tiles listed class by class (time blocks b = x mod 8), chain block major
+            // inside a class (consecutive workgroups of an XCD: different time blocks, as in launch
+            // order, so the trace rows written at a time spread over the HBM channels); XCD x's
+            // contiguous range of that list is (nearly) class x: 1/8 of the rows per L2
+            const uint32_t kbig = big * CB;   // tiles of the rt classes with qt + 1 blocks
+            const uint32_t x2 = k < kbig ? k / (CB * (qt + 1)) : rt + (k - kbig) / max(CB * qt, 1u);
+            const uint32_t cum = x2 <= rt ? x2 * CB * (qt + 1) : kbig + (x2 - rt) * CB * qt;
+            const uint32_t nbx = qt + (x2 < rt ? 1u : 0u), i2 = k - cum;
+            bs = __builtin_amdgcn_readfirstlane(x2 + 8u * (i2 % nbx));
+            cs = __builtin_amdgcn_readfirstlane(i2 / nbx);
+            (void)b;
+        } else {
+            // (uniform, but computed by VALU integer division: readfirstlane keeps them in SGPRs, so
+            // the row pointer and the tile's block loads stay scalar)
+            bs = __builtin_amdgcn_readfirstlane(b);
+            cs = __builtin_amdgcn_readfirstlane(k % CB);
+        }
         constexpr int TPW = exp_tpw<R, OUT, SITES>();
         if constexpr (TPW == 1) tile(bs, cs);
         else {   // time blocks bs TPW .. bs TPW + TPW - 1 (x counts super-blocks of TPW blocks)
@@ -2308,11 +2323,15 @@ __global__ __launch_bounds__(256) void state_move_kernel(StateView src, StateVie
 // residual are overwritten; the statistics get the exact differences of the
 // sums (fp32 values in fp64 differ exactly, so the corrections add up in any
 // order), the final residual's maximum and histogram count (the expansion left
-// these seconds out of both).  One work-item per (record, second of its block):
-// the kernel's duration is one second's recomputation (a latency-bound fp64 chain),
-// not a record's mask of them in a row.  Grid-stride over the records.
+// these seconds out of both).  One wave per FIX_RPW records (one mask word per lane):
+// the wave compacts their set bits (a prefix sum of the words' popcounts) and runs one
+// flagged second per lane, so the kernel's duration is one second's recomputation (a
+// latency-bound fp64 chain) and the waves that run it are full.  (Round 4 gave every
+// (record, second) a work-item: ~1 flagged second in 20 per wave, 95 us per C2 batch.)
+// Grid-stride over the record groups.
+constexpr uint32_t FIX_RPW = 16;
 template <bool SITES>
-__global__ __launch_bounds__(256) void fixup_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
+__global__ __launch_bounds__(64) void fixup_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
                                                     int64_t W0, uint32_t nsteps, int64_t utc0,
                                                     const double* __restrict__ tab64, const float* __restrict__ tab32,
                                                     const double* __restrict__ sun,
@@ -2323,32 +2342,57 @@ __global__ __launch_bounds__(256) void fixup_kernel(KParams kp, DrawParams dp, S
 {
     const uint32_t nrec = min(*sg.nfix, sg.fixcap);
     const int ne = (int)min(*n_events, ev_cap_dev(nsteps));
-    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < (uint64_t)BLOCK_STEPS * nrec;
-         t += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t i = (uint32_t)(t % BLOCK_STEPS);   // second of the record's block
-        const FixRec& fr = sg.fix[t / BLOCK_STEPS];
-        const uint32_t w = i >> 5;
-        const uint32_t mw = w == 0 ? fr.mask.x : (w == 1 ? fr.mask.y : (w == 2 ? fr.mask.z : fr.mask.w));
-        if (!((mw >> (i & 31)) & 1u)) continue;
-        const uint32_t c = fr.c;
-        if (c >= n || fr.b >= sg.nblk) continue;   // (never appended: the expansion records live chains only)
-        const BlockDesc db = desc[fr.b];
-        const uint32_t j = fr.b * BLOCK_STEPS + i;
-        float pv32, meter, pv;
-        if (!redo_second<SITES>(kp, dp, st, sg, n, c, chain0, W0, utc0, j, db, fr.jr, events, ne, tab64, tab32, sun,
-                                pv32, meter, pv))
-            continue;
-        const float res = meter - pv, res32 = meter - pv32;   // second_body's residual
-        const size_t o = (size_t)j * tr.ld + c;
-        if (tr.pv) reinterpret_cast<float*>(tr.pv)[o] = pv;
-        if (tr.residual) reinterpret_cast<float*>(tr.residual)[o] = res;
-        if (sv.acc) {
-            atomicAdd(&sg.corr[c], (double)pv - (double)pv32);
-            atomicAdd(&sg.corr[(size_t)n + c], (double)res - (double)res32);
-            __hip_atomic_fetch_max(sg.acc_mx + c, max_key((double)res), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t lane = threadIdx.x;   // one wave per workgroup
+    for (uint32_t r0 = blockIdx.x * FIX_RPW; r0 < nrec; r0 += gridDim.x * FIX_RPW) {   // wave-uniform
+        const uint32_t rw = r0 + (lane >> 2);
+        uint32_t word = 0;
+        if (rw < nrec) {
+            const uint4 m = sg.fix[rw].mask;
+            const uint32_t w = lane & 3;
+            word = w == 0 ? m.x : (w == 1 ? m.y : (w == 2 ? m.z : m.w));
         }
-        if (sv.hist) {
-            atomicAdd((unsigned long long*)&sv.hist[hist_bin_rt<float>(sv, res)], 1ull);
+        uint32_t cum = __popc(word);   // inclusive prefix sum over the wave's words
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t u = __shfl_up(cum, d, 64);
+            if (lane >= (uint32_t)d) cum += u;
+        }
+        const uint32_t total = __builtin_amdgcn_readfirstlane(__shfl(cum, 63, 64));
+        for (uint32_t k0 = 0; k0 < total; k0 += 64) {   // wave-uniform
+            const uint32_t k = k0 + lane;
+            // the word holding flagged second k: the first q with cum[q] > k (every lane
+            // takes part in the shuffles; lanes past the total search for nothing)
+            uint32_t lo = 0;
+#pragma unroll
+            for (uint32_t h = 32; h; h >>= 1)
+                if (__shfl(cum, (int)(lo + h - 1), 64) <= k) lo += h;
+            const uint32_t wq = __shfl(word, (int)lo, 64);
+            const uint32_t cq = __shfl(cum, (int)lo, 64);
+            if (k >= total) continue;
+            uint32_t m = wq;
+            for (uint32_t rank = k - (cq - __popc(wq)); rank; --rank) m &= m - 1;   // drop the lower set bits
+            const uint32_t i = (lo & 3) * 32 + (uint32_t)(__ffs(m) - 1);   // second of the record's block
+            const FixRec& fr = sg.fix[r0 + (lo >> 2)];
+            const uint32_t c = fr.c;
+            if (c >= n || fr.b >= sg.nblk) continue;   // (never appended: the expansion records live chains only)
+            const BlockDesc db = desc[fr.b];
+            const uint32_t j = fr.b * BLOCK_STEPS + i;
+            float pv32, meter, pv;
+            if (!redo_second<SITES>(kp, dp, st, sg, n, c, chain0, W0, utc0, j, db, fr.jr, events, ne, tab64, tab32, sun,
+                                    pv32, meter, pv))
+                continue;
+            const float res = meter - pv, res32 = meter - pv32;   // second_body's residual
+            const size_t o = (size_t)j * tr.ld + c;
+            if (tr.pv) reinterpret_cast<float*>(tr.pv)[o] = pv;
+            if (tr.residual) reinterpret_cast<float*>(tr.residual)[o] = res;
+            if (sv.acc) {
+                atomicAdd(&sg.corr[c], (double)pv - (double)pv32);
+                atomicAdd(&sg.corr[(size_t)n + c], (double)res - (double)res32);
+                __hip_atomic_fetch_max(sg.acc_mx + c, max_key((double)res), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (sv.hist) {
+                atomicAdd((unsigned long long*)&sv.hist[hist_bin_rt<float>(sv, res)], 1ull);
+            }
         }
     }
 }
@@ -3313,15 +3357,15 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     }
     if (!(phases & PH_COMMIT)) return TMH_OK;
     if (!f64 && eng->kp.with_pv) {   // the fp32 guard-band seconds, in fp64
-        // one work-item per (record, second): records are ~1.3e-3 of the (chain, block)s, so
-        // ~n nblk / 3,000 workgroups of 256 cover them in one pass (C2: ~900); grid-stride past
-        // 16,384 (C3: 1 M chains x 675 blocks)
-        const uint32_t gx = (uint32_t)std::min<uint64_t>(16384, std::max<uint64_t>(64, (uint64_t)n_chains * sg.nblk / 3000));
+        // one wave per FIX_RPW records: records are ~1.3e-3 of the (chain, block)s, so
+        // ~n nblk / 10,000 one-wave workgroups cover them in one pass (C2: ~280); grid-stride
+        // past 65,535 (C3: 1 M chains x 675 blocks)
+        const uint32_t gx = (uint32_t)std::min<uint64_t>(65535, std::max<uint64_t>(64, (uint64_t)n_chains * sg.nblk / 10000));
         if (eng->kp.sites)
-            hipLaunchKernelGGL(fixup_kernel<true>, dim3(gx), dim3(256), 0, s, eng->kp, eng->dp, v, chain0, n_chains, step0,
+            hipLaunchKernelGGL(fixup_kernel<true>, dim3(gx), dim3(64), 0, s, eng->kp, eng->dp, v, chain0, n_chains, step0,
                                n_steps, utc0, pv.tab64, pv.tab32, pv.sun, pv.events, pv.n_events, pv.desc, sg, tv, sv);
         else
-            hipLaunchKernelGGL(fixup_kernel<false>, dim3(gx), dim3(256), 0, s, eng->kp, eng->dp, v, chain0, n_chains, step0,
+            hipLaunchKernelGGL(fixup_kernel<false>, dim3(gx), dim3(64), 0, s, eng->kp, eng->dp, v, chain0, n_chains, step0,
                                n_steps, utc0, pv.tab64, pv.tab32, pv.sun, pv.events, pv.n_events, pv.desc, sg, tv, sv);
         if (int rc = hip_check(hipGetLastError(), "fixup_kernel launch")) return rc;
     }
