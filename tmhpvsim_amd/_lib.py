@@ -164,13 +164,34 @@ def check(rc):
     return rc
 
 
+_streams = []   # (device, handle) of the streams cu_stream created
+
+
+def _destroy_streams():
+    """At interpreter exit: drain and destroy the streams cu_stream created, before the
+    HIP runtime's own teardown (a CU-masked stream still alive when the runtime is
+    finalised crashed the process's exit under rocprofv3's kernel trace)."""
+    import torch
+    while _streams:
+        dev, h = _streams.pop()
+        try:
+            torch.cuda.synchronize(dev)
+            load().tmh_stream_destroy(h)
+        except Exception:   # exit path: nothing to report to
+            pass
+
+
 def cu_stream(cu_first, cu_count, device):
     """A torch stream over a HIP stream restricted to CU-mask bits cu_first ..
     cu_first + cu_count - 1 (tmh_stream_create_cus; cu_count 0 = all CUs).  The
-    stream lives as long as the process."""
+    stream lives until the interpreter exits (destroyed then, `_destroy_streams`)."""
+    import atexit
     import torch
     h = C.c_void_p()
     check(load().tmh_stream_create_cus(cu_first, cu_count, C.byref(h)))
+    if not _streams:
+        atexit.register(_destroy_streams)   # registered after torch's handlers, so it runs before them (LIFO)
+    _streams.append((device, h.value))
     return torch.cuda.ExternalStream(h.value, device=device)
 
 
@@ -181,7 +202,7 @@ def dedicated_stream(device):
     stream of the process -- torch's stream pool included -- and a queue runs its
     packets in order across the streams sharing it; a CU-masked stream always gets a
     queue of its own, so the pipeline's streams never wait behind each other's kernels
-    whatever GPU_MAX_HW_QUEUES is.  Lives as long as the process."""
+    whatever GPU_MAX_HW_QUEUES is.  Destroyed at interpreter exit (cu_stream)."""
     import torch
     ncu = torch.cuda.get_device_properties(device).multi_processor_count
     return cu_stream(0, ncu, device)
