@@ -2721,8 +2721,10 @@ struct tmh_engine {
             pool.pop_back();
             return e;
         }
+        // timing only: no system-scope fence (an L2 writeback + invalidate at every record,
+        // which the kernels beside the timed one would pay for too)
         hipEvent_t e = nullptr;
-        (void)hipEventCreate(&e);
+        (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
         return e;
     }
     // returns the start event of a timed region (nullptr when not profiling)
