@@ -107,6 +107,7 @@ struct SegView {                   // P1 -> P2 scratch
     long long* acc_fx;             // [3][n], zeroed with nfix / corr before each expansion
     long long* acc_mx;             // [n]
     double fx_scale, fx_inv;       // 2^k with 9,001 W x n_steps x 2^k < 2^62
+    uint32_t* brec;                // [nblk][n] the record holding each block's start (block_rec_kernel)
 };
 
 // double <-> int64 key with the same order (max of keys = key of the max)
@@ -1738,6 +1739,34 @@ __global__ __launch_bounds__(256) void overflow_settle_kernel(uint32_t n, SegVie
     sg.count[c] = min(sg.count[c], sg.cap);
 }
 
+// The record holding each block's start, for the expansion's tiles (a tile reads one
+// coalesced word instead of a binary search of ~9 dependent, lane-scattered record loads
+// at its start): the first record whose next-call step lies past the block start, or the
+// chain's last record (expand_tile's rule).  One work-item per (chain, BREC_G blocks): a
+// binary search for the first block, then a forward scan, the records' next-call steps
+// being nondecreasing.  Off the critical path: after the walk, on its stream.
+constexpr uint32_t BREC_G = 32;
+__global__ __launch_bounds__(256) void block_rec_kernel(uint32_t n, int64_t W0, SegView sg)
+{
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const uint32_t b0 = blockIdx.y * BREC_G, b1 = min(b0 + BREC_G, sg.nblk);
+    const int last = (int)sg.count[c] - 1;
+    const int32_t s00 = (int32_t)(W0 + (int64_t)b0 * BLOCK_STEPS);
+    int lo = 0, hi = last;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (rec_at(sg, c, mid).y > s00) hi = mid;
+        else lo = mid + 1;
+    }
+    int32_t y = lo < last ? rec_at(sg, c, lo).y : 0;
+    for (uint32_t b = b0; b < b1; ++b) {
+        const int32_t s0 = (int32_t)(W0 + (int64_t)b * BLOCK_STEPS);
+        while (lo < last && y <= s0) y = rec_at(sg, c, ++lo).y;
+        sg.brec[(size_t)b * n + c] = (uint32_t)lo;
+    }
+}
+
 // ------------------------------------------------------------ P2: expand
 // one trace store: a buffer resource on a wave-uniform base (SGPRs) plus the lane's
 // 32-bit byte offset, non-temporal (the trace is written once); no per-lane 64-bit
@@ -1895,13 +1924,8 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
     {
         uint32_t cw[4] = {0u, 0u, 0u, 0u};
         if (alive) {   // segment containing the block start: first record with next-call step > start
-            int lo = 0, hi = (int)sg.count[c] - 1;
-            const int last = hi;
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (rec_at(sg, c, mid).y > s0i) hi = mid;
-                else lo = mid + 1;
-            }
+            int lo = (int)sg.brec[(size_t)b * n + c];   // block_rec_kernel
+            const int last = (int)sg.count[c] - 1;
             // covered iff step < x of the segment holding it: [start, min(x, y)) per segment
             int2 r = rec_at(sg, c, lo);
             int32_t a = s0i;
@@ -2692,6 +2716,8 @@ size_t scratch_layout(uint32_t n, uint32_t n_steps, void* base, SegView* v, size
     o += align_up((size_t)n * 3 * 8);
     if (v) v->acc_mx = (long long*)(b + o);
     o += align_up((size_t)n * 8);
+    if (v) v->brec = (uint32_t*)(b + o);
+    o += align_up((size_t)nblk * n * 4);
     return o;
 }
 
@@ -3299,6 +3325,7 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     else { if (q) WALK(true, 16); else WALK(false, 16); }
 #undef WALK
     hipLaunchKernelGGL(overflow_settle_kernel, dim3(cb), dim3(256), 0, s, n_chains, sg);
+    hipLaunchKernelGGL(block_rec_kernel, dim3(cb, (sg.nblk + BREC_G - 1) / BREC_G), dim3(256), 0, s, n_chains, step0, sg);
     eng->close(TMH_K_SEGMENTS, t_seg, s);
     if (int rc = hip_check(hipGetLastError(), "segments kernel launch")) return rc;
     }
