@@ -129,6 +129,7 @@ struct FixRec {
     uint32_t jr;                   // segment record index at the block's last step
     uint32_t pad;
     uint4 mask;                    // bit i: second b * 128 + i lies in a guard band
+    uint4 cov;                     // bit i: second b * 128 + i is covered (the tile's covered bits)
 };
 
 // The window-start values a walk takes from the PREVIOUS window's walk instead of
@@ -858,19 +859,24 @@ __device__ __forceinline__ void load_fast_noise(const StateView& st, uint32_t c,
 
 // One second of a chain at window step j, rebuilt outside the expansion: the
 // sampler state (window-start state + desc_for(j) over the fp64 draw tables, as
-// a block start does), the covered bit (segment records) and the step's Philox
-// words.  fixup_kernel uses it for the fp32 expansion's guard-band seconds
+// a block start does), the covered bit (the tile's, from its FixRec) and the step's
+// Philox words.  fixup_kernel uses it for the fp32 expansion's guard-band seconds
 // (pv_power_f: DISC's kt = 0.6 split, the inverter's Pso cut-in): `pv32` is the
 // second as the fp32 expansion emitted it (the same fp32 arithmetic on the same
 // values), `pv64` the fp64 kernel's second, whose branch falls as in the fp64
-// reference.
+// reference.  need32 = false (no statistics to correct): the fp32 second is not
+// recomputed, since a recorded second is a guard-band second by construction (the
+// expansion's `held` is this `risky`), and the meter comes from its Philox word alone.
 template <bool SITES>
 __device__ __forceinline__ bool redo_second(const KParams& kp, const DrawParams& dp, const StateView& st,
                                             const SegView& sg, uint32_t n, uint32_t c, uint64_t chain0, int64_t W0,
-                                            int64_t utc0, uint32_t j, const BlockDesc& db, uint32_t jr_end,
+                                            int64_t utc0, uint32_t j, const BlockDesc& db, bool covered, bool need32,
                                             const int2* events, int ne, const double* tab64, const float* tab32,
                                             const double* sun, float& pv32, float& meter32, float& pv64)
 {   // returns whether the fp32 second lies in a guard band (then pv64 is set)
+    double row64[ROW];   // issued first: independent of the samplers' chain of loads
+#pragma unroll
+    for (int i = 0; i < ROW; ++i) row64[i] = tab64[(size_t)j * ROW + i];
     const int64_t step = W0 + (int64_t)j;
     const BlockDesc d = desc_advance(db, W0, utc0, events, ne, step);   // db: the block's descriptor
     Samp s;   // the fp32 kernels' samplers: fast noise copies
@@ -888,9 +894,6 @@ __device__ __forceinline__ bool redo_second(const KParams& kp, const DrawParams&
     sx.b[S_CLEAR_NOISE] = st.sb[S_CLEAR_NOISE][c];
     sx.a[S_CLEAR_NOISE] = st.sa[S_CLEAR_NOISE][c];
     exact_noise_at(d, dp, st, sg, n, c, chain0, W0, first_minute(utc0, W0), events, tab64, sx);
-    uint32_t k = jr_end;   // the segment holding the step: first next-call step > step, at or before the block's last
-    while (k > 0 && (int64_t)rec_at(sg, c, k - 1).y > step) --k;
-    const bool covered = step < (int64_t)rec_at(sg, c, k).x;
     const uint64_t gch = chain0 + gid(kp.ids, c);   // the step's noise and meter words (TAG_NOISE4 / TAG_METER4)
     const uint32_t wn = word_of(keyed_block(kp.seed, gch, (uint64_t)step >> 2, TAG_NOISE4, 0), (uint32_t)step & 3u);
     const uint32_t wm = word_of(keyed_block(kp.seed, gch, (uint64_t)step >> 2, TAG_METER4, 0), (uint32_t)step & 3u);
@@ -901,8 +904,8 @@ __device__ __forceinline__ bool redo_second(const KParams& kp, const DrawParams&
         ls.tl_doy = -1;
         lane_anchor(ls, sun + (size_t)(j / BLOCK_STEPS * BLOCK_STEPS) * SUN_W);
     }
-    bool risky;
-    {   // fp32, as expand_kernel<float>
+    bool risky = true;
+    if (need32) {   // fp32, as expand_kernel<float>
         FSamp<float> f;
         to_real(f, s);
         float row[ROW32];
@@ -915,17 +918,17 @@ __device__ __forceinline__ bool redo_second(const KParams& kp, const DrawParams&
         second_body<float>(kp, kp.pvf, row, flp, f, covered, noise_z<float>(wn), meter_w<float>(wm), csi, pv32, m, r,
                            risky);
         meter32 = m;
+        if (!risky) return false;
+    } else {
+        meter32 = meter_w<float>(wm);   // second_body's meter
+        pv32 = 0.0f;
     }
-    if (!risky) return false;
     {   // fp64, as expand_kernel<double>
         FSamp<double> f;
         to_real(f, sx);
-        double row[ROW];
-#pragma unroll
-        for (int i = 0; i < ROW; ++i) row[i] = tab64[(size_t)j * ROW + i];
-        if constexpr (SITES) lane_row<double>(ls, sun + (size_t)j * SUN_W, kp.module, row);
+        if constexpr (SITES) lane_row<double>(ls, sun + (size_t)j * SUN_W, kp.module, row64);
         double csi, pv, m, r;
-        second_body<double>(kp, kp.pvf, row, 0u, f, covered, noise_z<double>(wn), 0.0, csi, pv, m, r,
+        second_body<double>(kp, kp.pvf, row64, 0u, f, covered, noise_z<double>(wn), 0.0, csi, pv, m, r,
                             risky);
         pv64 = (float)pv;
     }
@@ -1843,7 +1846,7 @@ constexpr int PVF_VGPR = 0;   // leading PVF fields pinned in VGPRs in the fp32 
 //  fp32 statistics / other outputs (C3, C4): 6 = 80 VGPRs (the 16-bit-pair LDS histogram,
 //    8 KB, + 12 KB staging: 8 workgroups per CU; +6 % over 5 waves);
 //  fp64 single-site: 4 = at most 128 VGPRs (the trace kernel takes 110, no VGPR spills since the
-//    round-4 PV-constant and table changes; 5 waves = 96 VGPRs spill 11 and run the same);
+//    round-4 PV-constant and table changes; 5 waves = 96 VGPRs spill 14 and run 6 % slower, round 5);
 //  per-chain sites (C5): 2 (a few spills) is 35 % faster than 1
 template <typename R, int OUT, bool SITES>
 constexpr int exp_waves()
@@ -2153,7 +2156,10 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
         const bool held_any = (hm.x | hm.y | hm.z | hm.w) != 0;
         if (live && held_any) {   // (chain, block, seconds) for fixup_kernel (outside the loop: no registers held across it)
             const uint32_t k = atomicAdd(sg.nfix, 1u);
-            if (k < sg.fixcap) sg.fix[k] = FixRec{c, b, jr, 0u, hm};
+            if (k < sg.fixcap)
+                sg.fix[k] = FixRec{c, b, jr, 0u, hm,
+                                   make_uint4(cov_lds[0][threadIdx.x], cov_lds[1][threadIdx.x], cov_lds[2][threadIdx.x],
+                                              cov_lds[3][threadIdx.x])};
         }
     }
     if (live && sv.acc) {   // the block's sums into the chain's fixed-point window totals (order-free)
@@ -2401,9 +2407,11 @@ __global__ __launch_bounds__(64) void fixup_kernel(KParams kp, DrawParams dp, St
             if (c >= n || fr.b >= sg.nblk) continue;   // (never appended: the expansion records live chains only)
             const BlockDesc db = desc[fr.b];
             const uint32_t j = fr.b * BLOCK_STEPS + i;
+            const uint32_t cw = (lo & 3) == 0 ? fr.cov.x : ((lo & 3) == 1 ? fr.cov.y : ((lo & 3) == 2 ? fr.cov.z : fr.cov.w));
+            const bool covered = (cw >> (i & 31)) & 1u;
             float pv32, meter, pv;
-            if (!redo_second<SITES>(kp, dp, st, sg, n, c, chain0, W0, utc0, j, db, fr.jr, events, ne, tab64, tab32, sun,
-                                    pv32, meter, pv))
+            if (!redo_second<SITES>(kp, dp, st, sg, n, c, chain0, W0, utc0, j, db, covered, sv.acc != nullptr, events, ne,
+                                    tab64, tab32, sun, pv32, meter, pv))
                 continue;
             const float res = meter - pv, res32 = meter - pv32;   // second_body's residual
             const size_t o = (size_t)j * tr.ld + c;
