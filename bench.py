@@ -224,6 +224,10 @@ def parse():
     ap.add_argument("--commit-stream", type=int, default=None,
                     help="gated schedule: each batch's fixup + commit on a stream of their own beside the next "
                          "expansion (1) or after its expansion on the expansion stream (0, the default)")
+    ap.add_argument("--first-split", type=int, default=None,
+                    help="gated schedule: the run's first batch in this many consecutive windows of whole hours, "
+                         "so the first expansion waits for a part of the first walk only (the pipeline's fill); "
+                         "default 1 (off; 2 measured slower for c2, DESIGN.md round 5)")
     ap.add_argument("--compact", type=int, default=None,
                     help="multi-window stats workloads: run each window after the first on the chains still "
                          "live (faulted chains, e.g. C5's markov AssertionError, drop out); default 1 for c5")
@@ -256,7 +260,7 @@ def parse():
                               build_priority=a.build_priority,
                               commit_stream=None if a.commit_stream is None else bool(a.commit_stream),
                               walk_order=bool(a.walk_order), walk_cus=a.walk_cus, other_cus=a.other_cus,
-                              timeline=a.timeline, queues=a.queues)
+                              timeline=a.timeline, queues=a.queues, first_split=a.first_split)
     for k in ("mode", "window", "pipeline", "walks", "build_ahead", "build_on", "walk_priority", "compact",
               "commit_stream"):
         setattr(a, k, getattr(a.cfg, k))
@@ -488,7 +492,9 @@ def main():
     for name, kk in (("expand", _lib.K_EXPAND), ("segments", _lib.K_SEGMENTS),
                      ("candidates", _lib.K_CANDIDATES), ("tmh_step", _lib.K_STEP)):
         ms, cnt = _lib.profile_read(sim._eng, kk)
-        phases[name] = ms / cnt if cnt else None
+        # per launch, below made per batch (x windows).  One-window batches: the total over
+        # the batches, since the gated schedule's first batch runs as first_split windows
+        phases[name] = (ms / cnt if nwin > 1 else ms / args.steps) if cnt else None
     # the dominant kernel alone: one more batch with nothing beside it (after the timed
     # region, not part of `value`): its duration without the pipelined walks sharing the CUs
     one_step(args.warmup + args.steps)
@@ -588,6 +594,7 @@ def main():
                    "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"), "walks_in_flight": pipe.W, "walk_order": bool(args.walk_order), "walk_cus": args.walk_cus or "all", "other_cus": args.other_cus if args.walk_cus else "all",
                    "walk_chains_per_row": args.walk_cpr, "queues": args.queues, "walk_lanes": args.walk_lanes or "auto", "build_ahead": pipe.A,
                    "commit_stream": bool(args.commit_stream),
+                   "first_batch_windows": len(pipe.split) if (pipe.split and pipe.gated()) else 1,
                    "compacted_windows": bool(args.compact and args.mode == "stats" and nwin > 1)},
         "roofline": roof,
         "chain_seconds_total": chain_seconds, "chain_seconds_live": live,

@@ -23,6 +23,8 @@ if [ "$WHAT" = c2 ]; then
   f=$(find gpurun_out/prof_$TAG -name '*kernel_stats.csv' | head -1)
   cp "$f" gpurun_out/kstats_$TAG.csv
   python3 scripts/kstats.py gpurun_out/kstats_$TAG.csv | head -14 | tee gpurun_out/kstats_$TAG.txt
+  t=$(find gpurun_out/prof_$TAG -name '*kernel_trace.csv' | head -1)
+  python3 scripts/kstats_launches.py "$t" expand_kernel | tee -a gpurun_out/kstats_$TAG.txt
   rm -rf gpurun_out/prof_$TAG
 else
   bash scripts/pmc_workload.sh ${TAG}_c3 c3 1048576 86400 fp32 stats faithful -- --workload c3 --steps 1 --warmup 1 || exit 1

@@ -187,6 +187,35 @@ def test_bench_gated_schedule_equals_tmh_run(prec):
         del ref, r
 
 
+@pytest.mark.parametrize("prec", ["fp32", "fp64"])
+def test_gated_first_batch_split_equals_tmh_run(prec):
+    """The gated schedule's first batch of each run as two half-day windows
+    (`first_split=2`, a bench.py A/B option: the windows' walks chained through the
+    previous window's scratch, their expansions in order, the second window's trace rows
+    from row 43,200): two runs (batches 0-1, then 2-4), so batches 0 and 2 are split and
+    batch 1 is not; each equals a separate tmh_run of the same chains bit for bit."""
+    from tmhpvsim_amd.pipeline import BatchPipeline, pipeline_defaults
+    n, secs = 4096, 86400
+    cfg = pipeline_defaults("c2", prec, first_split=2)
+    sim = _sim(n, prec)
+    pipe = BatchPipeline(sim, n, secs, cfg, lambda k: 3_000_000 + k * n, torch.device("cuda:0"))
+    assert pipe.gated() and pipe.split == [(0, 43200), (43200, 43200)]
+    pipe.run(0, 2)
+    pipe.run(2, 3)
+    pipe.sync()
+    for k in (0, 1, 2):
+        cx = pipe.ctxs[k]
+        assert cx.chain0 == 3_000_000 + k * n
+        ref = _sim(n, prec, chain0=cx.chain0)
+        r = ref.run(secs, trace=("csi",) + FIELDS)
+        torch.cuda.synchronize()
+        for f in FIELDS:
+            assert _same(cx.trace[f], r[f]), (k, f)
+        sim.state = cx.state
+        np.testing.assert_array_equal(sim.status(), ref.status())
+        del ref, r
+
+
 def test_stats_pipeline_c3_shape_equals_batches():
     """The stats schedule bench.py's C3 line runs (pipeline_defaults("c3"): two contexts,
     one walk in flight, so the staggered schedule: construction ahead on the expansion

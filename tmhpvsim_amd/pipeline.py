@@ -43,6 +43,8 @@ class PipelineConfig:
     other_cus: str = "all"       # with walk_cus: the other streams on all CUs or the rest
     compact: bool = False        # multi-window stats batches: later windows on the live chains only
     timeline: bool = False       # gated: HIP events around every build, walk and expansion
+    first_split: int = 1         # gated: the run's first batch in this many consecutive windows (its walk
+                                 # is the pipeline's fill; the windows' walks run ahead of their expansions)
     queues: str = "dedicated"    # "dedicated": normal-priority streams on hardware queues of their own
                                  # (_lib.dedicated_stream); "shared": plain streams (GPU_MAX_HW_QUEUES pool)
     hist_bins: int = 4096
@@ -86,6 +88,10 @@ def pipeline_defaults(workload, precision="fp32", seconds=None, window=None, wal
         # 1.94e11 chain-s/s vs 1.82e11 on the expansion stream with high-priority walks
         build_on="walk" if workload == "c2" else "expand",
         walk_priority="normal" if workload == "c2" else "high",
+        # (first_split 2 for C2 -- the run's first batch as two half-day windows -- starts the
+        # first expansion after half a day's walk, but the second half's draws and walk then
+        # run beside that expansion, the next batch's walk and three constructions: the first
+        # batch ends 0.6 ms later, 2.39-2.44 against 2.46-2.47e11, round 5, same box)
         compact=bool(c5 if compact is None else compact),
     )
     for k, v in overrides.items():
@@ -211,6 +217,20 @@ class BatchPipeline:
             self.bst_p = C.c_void_p(self.bst.cuda_stream)
         self.A = cfg.build_ahead
         self.tl = {}   # timeline: per-batch HIP timing events (build done, walk start / end, expansion start / end)
+        # gated schedule, the run's first batch in consecutive windows of whole hours (first_split):
+        # their plans + scratch, and the events chaining each window's walk to the previous one's
+        self.split = []
+        if nwin == 1 and cfg.first_split > 1 and sim.path == "time_parallel":
+            h = secs // cfg.first_split // 3600 * 3600
+            if h > 0:
+                bounds = [i * h for i in range(cfg.first_split)] + [secs]
+                self.split = [(a, b - a) for a, b in zip(bounds[:-1], bounds[1:])]
+                self.sbufs = [(torch.empty(L.tmh_plan_bytes(k), dtype=torch.uint8, device=device),
+                               torch.empty(L.tmh_engine_scratch_bytes(sim._eng, n, k), dtype=torch.uint8, device=device))
+                              for _, k in self.split]
+                self.swalked = [torch.cuda.Event() for _ in self.split]
+                self.splanned = [torch.cuda.Event() for _ in self.split]
+                self.sdone = None   # the last split batch's expansions are done (its buffers are free)
 
     # ------------------------------------------------------------------ helpers
     @property
@@ -398,6 +418,76 @@ class BatchPipeline:
             _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_COMMIT, ep))
             cx.expanded.record(es)
 
+    # the run's first batch in consecutive windows (first_split): as engine.run_windows, each
+    # window's draws + walk chained to the previous window's walk (tmh_walk_part with its
+    # scratch as prev), the expansions in order behind them on the expansion stream
+    def s_build(self, j):
+        L, sim = self.L, self.sim
+        cx = self.ctx_of(j)
+        cx.chain0 = self.chain0_of(j)
+        bst, bp = self.bst, self.bst_p
+        if cx.expanded is not None:
+            bst.wait_event(cx.expanded)
+        if self.sdone is not None:   # a previous run's split batch still reading the window buffers
+            bst.wait_event(self.sdone)
+        _lib.check(L.tmh_init(sim._eng, self._p(cx.state), cx.chain0, self.n, None, bp))
+        (s0, k), (plan, scr) = self.split[0], self.sbufs[0]
+        _lib.check(L.tmh_plan(sim._eng, s0, k, self._p(plan), bp))
+        _lib.check(L.tmh_walk_part(sim._eng, self._p(cx.state), cx.chain0, self.n, s0, k, self._p(plan),
+                                   self._p(scr), scr.numel(), None, 0, _lib.WALK_DRAWS, bp))
+        cx.done.record(bst)
+        self.tl_mark("built", j, bst)
+        for w in range(1, len(self.split)):   # the later windows' plans, after the first window's draws
+            (s0, k), (plan, _) = self.split[w], self.sbufs[w]
+            _lib.check(L.tmh_plan(sim._eng, s0, k, self._p(plan), bp))
+            self.splanned[w].record(bst)
+
+    def s_walk(self, j):
+        L, sim = self.L, self.sim
+        cx = self.ctx_of(j)
+        wst = self.wsts[j % self.W]
+        wp = C.c_void_p(wst.cuda_stream)
+        wst.wait_event(cx.done)
+        self.tl_mark("walk0", j, wst)
+        for w, ((s0, k), (plan, scr)) in enumerate(zip(self.split, self.sbufs)):
+            parts, ps, pk = _lib.WALK_SEGMENTS, None, 0
+            if w > 0:
+                wst.wait_event(self.splanned[w])
+                parts = _lib.WALK_DRAWS | _lib.WALK_SEGMENTS
+                ps, pk = self._p(self.sbufs[w - 1][1]), self.split[w - 1][1]
+            _lib.check(L.tmh_walk_part(sim._eng, self._p(cx.state), cx.chain0, self.n, s0, k, self._p(plan),
+                                       self._p(scr), scr.numel(), ps, pk, parts, wp))
+            self.swalked[w].record(wst)
+        cx.walked.record(wst)
+        self.tl_mark("walk1", j, wst)
+
+    def s_expand(self, j):
+        L = self.L
+        cx = self.ctx_of(j)
+        es, ep = self.estream, self.eptr
+        esz = self.torch.finfo(self.sim.real).bits // 8   # the trace rows of window w start at row s0
+        last = len(self.split) - 1
+        for w, ((s0, k), (plan, scr)) in enumerate(zip(self.split, self.sbufs)):
+            es.wait_event(self.swalked[w])
+            if w == 0:
+                self.tl_mark("exp0", j, es)
+            tr = _lib.Trace(None, None, *((cx.trace[f].data_ptr() + s0 * self.n * esz) if f in cx.trace else None
+                                          for f in ("pv", "meter", "residual")), self.n)
+            args_ = (self.sim._eng, self._p(cx.state), cx.chain0, self.n, s0, k, None, C.byref(tr),
+                     C.byref(cx.st) if cx.st is not None else None, self._p(plan), self._p(scr), scr.numel())
+            if w < last:
+                _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_KERNEL | _lib.EXPAND_COMMIT, ep))
+            else:
+                _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_KERNEL, ep))
+                self.tl_mark("exp1", j, es)
+                _lib.check(L.tmh_expand_part(*args_, _lib.EXPAND_COMMIT, ep))
+        if cx.expanded is None:
+            cx.expanded = self.torch.cuda.Event()
+        cx.expanded.record(es)
+        if self.sdone is None:
+            self.sdone = self.torch.cuda.Event()
+        self.sdone.record(es)
+
     def run_gated(self, k0, cnt):
         """W walks in flight: when the walk of batch k ends, the expansion of k, the walk
         of k + W (on k's walk stream) and the construction of k + A are released together."""
@@ -409,16 +499,25 @@ class BatchPipeline:
             # order's (four windy chains); the wind order for the rest, which run beside expansions
             if cfg.walk_order:
                 _lib.check(L.tmh_set_walk_order(sim._eng, 0 if (j == k0 and W > 1) else 1))
-            self.g_build(j, None)
+            if j == k0 and self.split:
+                self.s_build(j)
+            else:
+                self.g_build(j, None)
         for j in range(k0, min(k0 + W, end)):
-            self.g_walk(j)
+            if j == k0 and self.split:
+                self.s_walk(j)
+            else:
+                self.g_walk(j)
         for k in range(k0, end):
             gate = self.ctx_of(k).walked
             if k + A < end:
                 self.g_build(k + A, gate)
             if k + W < end:
                 self.g_walk(k + W)
-            self.g_expand(k)
+            if k == k0 and self.split:
+                self.s_expand(k)
+            else:
+                self.g_expand(k)
 
     def gated(self):
         """Whether `run` takes the gated schedule (one-window, staggered batches)."""
