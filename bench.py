@@ -282,7 +282,7 @@ def parse():
 
 
 SECONDARY = {   # --secondary: the other BASELINE.json configs, each in a child process of its own
-    "c2_fp64": ["--precision", "fp64", "--steps", "10", "--warmup", "3"],
+    "c2_fp64": ["--precision", "fp64", "--steps", "20", "--warmup", "5"],
     # the headline at HIP's default of 4 hardware queues (the pipelines' streams have queues of
     # their own, PipelineConfig.queues = "dedicated": no result depends on GPU_MAX_HW_QUEUES)
     "c2_q4": ["--hw-queues", "4", "--steps", "20", "--warmup", "5"],

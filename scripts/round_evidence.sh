@@ -37,6 +37,6 @@ else
     timeout -k 10 600 python -u bench.py --workload $wl > gpurun_out/bench_${TAG}_$1.json 2> gpurun_out/bench_${TAG}_$1.err || exit 1
     cat gpurun_out/bench_${TAG}_$1.json
   done
-  timeout -k 10 300 python -u bench.py --precision fp64 --steps 10 --warmup 3 > gpurun_out/bench_${TAG}_c2_fp64.json 2> gpurun_out/bench_${TAG}_c2_fp64.err || exit 1
+  timeout -k 10 300 python -u bench.py --precision fp64 --steps 20 --warmup 5 > gpurun_out/bench_${TAG}_c2_fp64.json 2> gpurun_out/bench_${TAG}_c2_fp64.err || exit 1
   cat gpurun_out/bench_${TAG}_c2_fp64.json
 fi

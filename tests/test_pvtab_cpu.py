@@ -22,9 +22,12 @@ def fma(a, b, c):
 
 
 def coefs():
+    """(centers, coefficient rows) of ndtri64's pieces, parsed from the header"""
     src = open(MATH_H).read()
-    body = re.search(r"NDTRI_COEF\[NDTRI_DEG \+ 1\] = \{[^\n]*\n(.*?)\};", src, re.S).group(1)
-    return [float(x) for x in re.findall(r"[-+0-9.eE]+", body)]
+    centers = re.search(r"NDTRI_CENTER\[NDTRI_PIECES\] = \{([^}]*)\};", src).group(1)
+    body = re.search(r"NDTRI_COEF\[NDTRI_PIECES\]\[NDTRI_DEG \+ 1\] = \{[^\n]*\n(.*?)\}\};", src, re.S).group(1)
+    rows = [[float(x) for x in re.findall(r"[-+]?[0-9][-+0-9.eE]*", r)] for r in body.split("},")]
+    return [float(x) for x in centers.split(",")], rows
 
 
 TAB = [(1.0 / (1.0 + (i + 0.5) / LOG_TAB), math.log(1.0 + (i + 0.5) / LOG_TAB)) for i in range(LOG_TAB)]
@@ -62,10 +65,12 @@ def ndtri64(w, c):
     ww = -log_tab(4.0 * p * (1.0 - p))
     if not ww < 6.25:
         return None                      # the device takes ocml's quantile here
-    u = ww - 3.125
-    f = c[22]
-    for k in range(21, -1, -1):
-        f = fma(f, u, c[k])
+    centers, rows = c
+    q = (1 if ww >= 2.0 else 0) + (1 if ww >= 4.0 else 0)   # the lane's piece
+    u = ww - centers[q]
+    f = rows[q][-1]
+    for k in range(len(rows[q]) - 2, -1, -1):
+        f = fma(f, u, rows[q][k])
     return (1.4142135623730950488 * x) * f
 
 
@@ -83,8 +88,14 @@ def test_exp_tab_accuracy():
 
 def test_ndtri64_accuracy_and_coefficients():
     c = coefs()
-    assert len(c) == 23 and abs(c[0] - 1.6536545626831027) < 1e-15   # degree 0 first: sqrt(pi) / 2 at w = 3.125
-    ws = np.concatenate([np.random.default_rng(3).integers(0, 2 ** 32, 6000), [2 ** 31 - 1, 2 ** 31, 2 ** 31 + 1]])
+    centers, rows = c
+    assert centers == [1.0, 3.0, 5.125] and [len(r) for r in rows] == [14, 14, 14]
+    # degree 0 first: f at each piece's center
+    assert abs(rows[1][0] - 1.6235420064648298) < 1e-15 and abs(rows[0][0] - 1.1273743936892275) < 1e-15
+    rng = np.random.default_rng(3)
+    # uniform words, plus 3,000 in the lower tail (p < 0.031: the pieces from w' = 2 and 4 on)
+    ws = np.concatenate([rng.integers(0, 2 ** 32, 6000), 2 ** 32 - 1 - rng.integers(0, 2 ** 27, 1500),
+                         rng.integers(0, 2 ** 27, 1500), [2 ** 31 - 1, 2 ** 31, 2 ** 31 + 1]])
     n, worst = 0, 0.0
     for w in ws:
         z = ndtri64(int(w), c)
@@ -93,4 +104,4 @@ def test_ndtri64_accuracy_and_coefficients():
         ref = float(ndtri((int(w) + 0.5) * 2.0 ** -32))
         worst = max(worst, abs(z - ref) / max(abs(ref), 1e-300))
         n += 1
-    assert n > 0.99 * len(ws) and worst <= 2e-15, (n, worst)
+    assert n > 0.95 * len(ws) and worst <= 2e-15, (n, worst)

@@ -2850,7 +2850,10 @@ static int pv_tab_upload(int device)
         lt[2 * i + 1] = std::log(c);
     }
     for (int i = 0; i < EXP_TAB; ++i) lt[EXP_OFF + i] = std::exp2(i * (1.0 / EXP_TAB));
-    for (int i = 0; i <= NDTRI_DEG; ++i) lt[NDTRI_OFF + i] = NDTRI_COEF[i];
+    for (int q = 0; q < NDTRI_PIECES; ++q) {
+        lt[NDTRI_OFF + NDTRI_STRIDE * q] = NDTRI_CENTER[q];
+        for (int i = 0; i <= NDTRI_DEG; ++i) lt[NDTRI_OFF + NDTRI_STRIDE * q + 1 + i] = NDTRI_COEF[q][i];
+    }
     if (int rc = hip_check(hipSetDevice(device), "hipSetDevice")) return rc;
     return hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_pv_tab), lt, sizeof lt), "hipMemcpyToSymbol(g_pv_tab)");
 }

@@ -373,12 +373,13 @@ __device__ __noinline__ double pow_d(double x, double y) { return pow(x, y); }
 // needs 1e-12 relative.  13 VALU instead of ocml log's ~90.  Zero, negative, NaN,
 // infinite and subnormal x take ocml's log (and its -inf / NaN).
 // g_pv_tab: t[2 i] = 1 / c_i, t[2 i + 1] = log c_i, then exp_tab's 2^(i / 64) at
-// t[EXP_OFF + i], then ndtri64's coefficients at t[NDTRI_OFF + k] (degree k); written
+// t[EXP_OFF + i], then ndtri64's three pieces at t[NDTRI_OFF + NDTRI_STRIDE q] (the piece's
+// center, then its coefficients, degree 0 first); written
 // once per engine from the host (tmh_engine_create); every fp64
 // PV evaluation reads these same values (the expansion from an LDS copy), so the kernels
 // agree bit for bit.
-constexpr int LOG_TAB = 128, EXP_TAB = 64, EXP_OFF = 2 * LOG_TAB, NDTRI_OFF = EXP_OFF + EXP_TAB, NDTRI_DEG = 22,
-              PV_TAB = NDTRI_OFF + NDTRI_DEG + 1;
+constexpr int LOG_TAB = 128, EXP_TAB = 64, EXP_OFF = 2 * LOG_TAB, NDTRI_OFF = EXP_OFF + EXP_TAB, NDTRI_DEG = 13,
+              NDTRI_PIECES = 3, NDTRI_STRIDE = NDTRI_DEG + 2, PV_TAB = NDTRI_OFF + NDTRI_PIECES * NDTRI_STRIDE;
 __device__ double g_pv_tab[PV_TAB];
 typedef __attribute__((address_space(3))) const double LdsD;
 
@@ -407,35 +408,27 @@ __device__ __forceinline__ double log_tab(double x, TP t)
 // ---- fp64 normal quantile of a 32-bit word (the per-second noise, noise_z<double>) ----
 // p = (w + 1/2) 2^-32, x = 2p - 1 (exact), ndtri(p) = sqrt(2) erfinv(x) = sqrt(2) x f(w')
 // with w' = -log(1 - x^2) = -log(4 p (1 - p)) and, for w' < 6.25 (p in ~[5e-4, 1 - 5e-4],
-// 99.9 % of the draws), f a degree-22 polynomial in w' - 3.125 (Giles' form, "Approximating
-// the erfinv function", refitted: scripts/fit_ndtri_f64.py, <= 4.2e-16 relative in an fp64
-// Horner evaluation); the rest take ocml's quantile out of line (ndtri_fast).  About 40 VALU
-// instead of ocml's ~150 and a call.  The coefficients come from the table (an LDS copy in
-// the expansion, read through `tab_fence` in chunks so they are loaded shortly before use).
-constexpr double NDTRI_COEF[NDTRI_DEG + 1] = {   // degree 0 first (the host copies them into g_pv_tab)
-    1.6536545626831027,
-    0.2401581824255897,
-    -0.006033670871427011,
-    -0.0007407025341669402,
-    0.0001867342080212427,
-    -1.3882523361276876e-05,
-    -1.3654691796592068e-06,
-    4.2347877672780653e-07,
-    -2.907038666019143e-08,
-    -4.112633104297614e-09,
-    1.0512202440121784e-09,
-    -5.4154417754696635e-11,
-    -1.2977505202014966e-11,
-    2.6335724924608484e-12,
-    -8.106594456438496e-14,
-    -4.0554139746886e-14,
-    6.581955305929239e-15,
-    2.166994626283574e-17,
-    -1.290702354613073e-16,
-    1.1125794759379464e-17,
-    1.1027771591500033e-18,
-    -1.6787330615256773e-19,
-    -2.362369698566107e-22};
+// 99.9 % of the draws), f a degree-13 polynomial in w' - c_q on the lane's piece q of
+// [0, 2), [2, 4), [4, 6.25) (Giles' form, "Approximating the erfinv function", refitted in
+// pieces: scripts/fit_ndtri_f64.py, <= 3.1e-16 relative in an fp64 Horner evaluation; round 4
+// used one piece of degree 22, 9 fmas more per daylight second at 4.2e-16); the rest take
+// ocml's quantile out of line (ndtri_fast).  The piece is chosen per lane by table offset,
+// not by branch.  The coefficients come from the table (an LDS copy in the expansion, read
+// through `tab_fence` in chunks so they are loaded shortly before use).
+constexpr double NDTRI_CENTER[NDTRI_PIECES] = {1.0, 3.0, 5.125};
+constexpr double NDTRI_COEF[NDTRI_PIECES][NDTRI_DEG + 1] = {   // degree 0 first (the host copies them into g_pv_tab)
+    {1.1273743936892275, 0.24783287028621095, 0.004250709244840092, -0.002376369955580531, 0.00010012177598503247,
+     3.820187251368197e-05, -4.275584236922046e-06, -5.652253874123589e-07, 1.2231291266949573e-07,
+     6.040592330213068e-09, -3.017929272010491e-09, 1.5906520115066905e-11, 6.298924235630103e-11,
+     -3.2253159972831256e-12},
+    {1.6235420064648298, 0.24163040416615827, -0.0057381352210059446, -0.0008361817769086462, 0.0001950613244170301,
+     -1.2716422648914508e-05, -1.7480021231028974e-06, 4.499854856199944e-07, -2.3688647408781946e-08,
+     -5.467350086581866e-09, 1.110687588033803e-09, -3.117460148479959e-11, -1.7262109450729976e-11,
+     2.5158500392913756e-12},
+    {2.1064123296343875, 0.21189284366397468, -0.007210971340179456, 0.00015540013139557572, 4.64226024498019e-05,
+     -9.737631064560686e-06, 9.675017285744816e-07, -1.947519718448861e-08, -1.048456228150318e-08,
+     1.8905557238598573e-09, -1.415734465250556e-10, -5.179746543640047e-12, 2.839759278393376e-12,
+     -3.365321693201019e-13}};
 
 template <typename TP>
 __device__ __forceinline__ TP tab_fence(TP t)
@@ -455,13 +448,14 @@ __device__ __forceinline__ double ndtri64(uint32_t w, TP t)
     const double x = 2.0 * p - 1.0;
     const double ww = -log_tab(4.0 * p * (1.0 - p), t);
     if (__builtin_expect(!(ww < 6.25), 0)) return ndtri_fast(p);
-    const double u = ww - 3.125;
+    const int q = NDTRI_OFF + NDTRI_STRIDE * ((ww >= 2.0 ? 1 : 0) + (ww >= 4.0 ? 1 : 0));   // the lane's piece
     t = tab_fence(t);
-    double f = t[NDTRI_OFF + 22];
+    const double u = ww - t[q];
+    double f = t[q + 1 + NDTRI_DEG];
 #pragma unroll
-    for (int k = 21; k >= 0; --k) {
+    for (int k = NDTRI_DEG - 1; k >= 0; --k) {
         if (k % 6 == 5) t = tab_fence(t);
-        f = fma(f, u, t[NDTRI_OFF + k]);
+        f = fma(f, u, t[q + 1 + k]);
     }
     return (1.4142135623730950488 * x) * f;
 }
