@@ -2,7 +2,8 @@
 import csv
 import sys
 
-for r in csv.DictReader(open(sys.argv[1])):
+rows = list(csv.DictReader(open(sys.argv[1])))
+for r in rows[:int(sys.argv[2]) if len(sys.argv) > 2 else len(rows)]:
     name = r["Name"]
     short = name.split("(")[0] if not name.startswith("void") else name.split("(")[1].split(")")[-1] if False else name
     short = name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]

@@ -22,7 +22,7 @@ if [ "$WHAT" = c2 ]; then
       -o run -- python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline > "$ROOT/gpurun_out/prof_$TAG.json" 2>&1 ) || exit 1
   f=$(find gpurun_out/prof_$TAG -name '*kernel_stats.csv' | head -1)
   cp "$f" gpurun_out/kstats_$TAG.csv
-  python3 scripts/kstats.py gpurun_out/kstats_$TAG.csv | head -14 | tee gpurun_out/kstats_$TAG.txt
+  python3 scripts/kstats.py gpurun_out/kstats_$TAG.csv 14 | tee gpurun_out/kstats_$TAG.txt
   t=$(find gpurun_out/prof_$TAG -name '*kernel_trace.csv' | head -1)
   python3 scripts/kstats_launches.py "$t" expand_kernel | tee -a gpurun_out/kstats_$TAG.txt
   rm -rf gpurun_out/prof_$TAG

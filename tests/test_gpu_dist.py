@@ -42,3 +42,24 @@ def test_simulate_stats_two_ranks_equal_one(tmp_path):
         np.testing.assert_array_equal(got["energy_fx"], want["energy_fx"])   # integer energy sums: bit for bit
         for k in ("energy_pv", "energy_meter", "energy_residual"):
             assert float(got[k]) == float(want[k])
+
+
+def test_simulate_stats_rccl_one_rank_equals_direct(tmp_path):
+    """The RCCL all-reduce of the statistics (dist.all_reduce_stats: the int64 histogram and
+    energy limbs in one SUM, the peak in a MAX) executed on the GPU: one rank over the
+    `nccl` backend (RCCL; the test box has one GPU), whose node totals equal the
+    unsharded run bit for bit."""
+    from tmhpvsim_amd.dist import simulate_stats
+    n_total, n_steps = 321, 2 * 3600
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE="1", RANK="0",
+               LOCAL_RANK="0")
+    p = subprocess.Popen([sys.executable, os.path.join(HERE, "_dist_gpu_worker.py"), str(n_total), str(n_steps),
+                          str(tmp_path), "nccl"], env=env)
+    assert p.wait(timeout=240) == 0
+    one, bad1 = simulate_stats(n_total, "2019-09-05 06:00:00", n_steps, tz="Europe/Berlin", device="cuda:0",
+                               window=7200)
+    got = np.load(tmp_path / "rank0.npz")
+    assert int(got["bad"]) == bad1
+    np.testing.assert_array_equal(got["hist"], one["hist"].cpu().numpy())
+    np.testing.assert_array_equal(got["energy_fx"], one["energy_fx"].cpu().numpy())
+    assert float(got["peak_residual"]) == float(one["peak_residual"])

@@ -1747,8 +1747,10 @@ __global__ __launch_bounds__(256) void overflow_settle_kernel(uint32_t n, SegVie
 // at its start): the first record whose next-call step lies past the block start, or the
 // chain's last record (expand_tile's rule).  One work-item per (chain, BREC_G blocks): a
 // binary search for the first block, then a forward scan, the records' next-call steps
-// being nondecreasing.  Off the critical path: after the walk, on its stream.
-constexpr uint32_t BREC_G = 32;
+// being nondecreasing.  After the walk, on its stream (so the expansion's wait for the walk
+// includes it): 32 blocks per work-item took 122 us per C2 batch, a latency chain of ~60
+// dependent loads; 8 blocks, ~23.
+constexpr uint32_t BREC_G = 8;
 __global__ __launch_bounds__(256) void block_rec_kernel(uint32_t n, int64_t W0, SegView sg)
 {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;

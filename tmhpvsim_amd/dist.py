@@ -96,7 +96,7 @@ def all_reduce_stats(tot: dict, group=None) -> dict:
     packed = limbs.to(dev).reshape(6) if hist is None else torch.cat([limbs.to(dev).reshape(6), hist.to(torch.int64)])
     packed = packed.clone()
     peak = torch.as_tensor(tot["peak_residual"], dtype=torch.float64, device=dev).reshape(1).clone()
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    if dist.is_available() and dist.is_initialized():   # (a one-rank group too: the collective runs)
         dist.all_reduce(packed, op=dist.ReduceOp.SUM, group=group)
         dist.all_reduce(peak, op=dist.ReduceOp.MAX, group=group)
     return totals_from(packed[:6].reshape(2, 3), peak[0], packed[6:] if hist is not None else None, device=dev)
