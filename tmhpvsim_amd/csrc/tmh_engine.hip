@@ -3399,10 +3399,12 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     }
     if (!(phases & PH_COMMIT)) return TMH_OK;
     if (!f64 && eng->kp.with_pv) {   // the fp32 guard-band seconds, in fp64
-        // one wave per FIX_RPW records: records are ~1.3e-3 of the (chain, block)s, so
-        // ~n nblk / 10,000 one-wave workgroups cover them in one pass (C2: ~280); grid-stride
-        // past 65,535 (C3: 1 M chains x 675 blocks)
-        const uint32_t gx = (uint32_t)std::min<uint64_t>(65535, std::max<uint64_t>(64, (uint64_t)n_chains * sg.nblk / 10000));
+        // one wave per FIX_RPW records, one workgroup per group of the record capacity (up to
+        // 65,535, grid-stride past it: C3): the groups past the count exit at once.  (A grid
+        // sized for ~1.3e-3 records per (chain, block) left a quarter of the C2 workgroups two
+        // groups in a row -- 2.0e-3 are recorded, ~1 flagged second each, diagnostic run r05 --
+        // and the kernel two redo latencies long.)
+        const uint32_t gx = (uint32_t)std::min<uint64_t>(65535, ((uint64_t)sg.fixcap + FIX_RPW - 1) / FIX_RPW);
         if (eng->kp.sites)
             hipLaunchKernelGGL(fixup_kernel<true>, dim3(gx), dim3(64), 0, s, eng->kp, eng->dp, v, chain0, n_chains, step0,
                                n_steps, utc0, pv.tab64, pv.tab32, pv.sun, pv.events, pv.n_events, pv.desc, sg, tv, sv);
