@@ -154,8 +154,8 @@ def parse():
                          "(Europe/Berlin wall clock, stats, 30-day windows); c5: the lat/lon sweep (65,536 sites x 1 "
                          "week, markov cc with per-site tables, per-site PV geometry, stats mode, day windows)")
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=8)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--chains", type=int, default=None,
                     help="c2: chains per GPU (4096, weak scaling); c3 / c4 / c5: chains of the whole node, "
                          "sharded over the GPUs (1048576 / 16384 / 65536, strong scaling)")
