@@ -602,6 +602,8 @@ def main():
         # whole-pipeline rate: trace bytes of all batches / wall time (kernels overlap across batches)
         "effective_trace_gbs": (TB * n * secs / (elapsed / args.steps) / 1e9) if args.mode == "trace" else None,
         "faulted_chains": bad,
+        # the loaded library's build stamp (tmh_build_stamp; _lib.load refuses a stale in-tree library)
+        "lib_stamp": _lib.loaded_stamp(),
     }
     if proxy > 1:
         line["proxy_world"] = proxy
@@ -627,6 +629,7 @@ def main():
                             "walk_ms": wdur, "walk_start_after_build_ms": bwait}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args, kw)
+    pipe.close()   # drain and release the pipeline's dedicated streams
     if rank == 0 and world == 1 and args.secondary != "none":
         del pipe, run_batches, one_step   # the children need the memory
         torch.cuda.empty_cache()

@@ -142,6 +142,11 @@ typedef struct tmh_stats {
 
 int tmh_abi_version(void);
 const char* tmh_last_error(void);
+/* Provenance: "TMHSTAMP:" + the 16-hex-digit hash of the sources and compile flags
+ * this library was built from (tmhpvsim_amd/build.py build_stamp; "unstamped" for a
+ * build outside it).  The Python loader refuses an in-tree library whose stamp differs
+ * from its sources, so a stale binary is never tested or benchmarked. */
+const char* tmh_build_stamp(void);
 
 /* Chain state (structure of arrays, one element per chain per field). */
 size_t tmh_state_bytes(uint32_t n_chains);
@@ -186,7 +191,10 @@ int tmh_set_walk_order(struct tmh_engine* eng, int on);
  * anywhere like a plain stream but, being CU-masked, on a hardware queue of its own
  * (plain streams share GPU_MAX_HW_QUEUES queues round-robin, a queue running its
  * packets in order across them): the pipelines' streams (tmhpvsim_amd.pipeline).
- * *stream receives the hipStream_t; release it with tmh_stream_destroy. */
+ * *stream receives the hipStream_t; release it with tmh_stream_destroy.  The stream
+ * belongs to the calling thread's current device (hipSetDevice first).  A CU-masked
+ * stream is a blocking stream (it synchronises with the legacy null stream, as
+ * hipStreamCreate's default does); cu_count == 0 gives a non-blocking one. */
 int tmh_stream_create_cus(uint32_t cu_first, uint32_t cu_count, void** stream);
 int tmh_stream_destroy(void* stream);
 /* Compaction (batches whose chains fault, e.g. the reference's markov-mode

@@ -93,3 +93,25 @@ def test_no_cpu_fallback():
     from tmhpvsim_amd.engine import BatchedSim
     with pytest.raises(Exception):
         BatchedSim(4, "2019-09-05 00:00:00", device="cpu")
+
+
+def test_loaded_library_carries_the_sources_stamp():
+    """Provenance (round 6): the library exports the build stamp it was compiled with
+    (tmh_build_stamp), build.lib_stamp reads it from the file, and it equals the stamp of
+    the sources in the tree -- the loader refuses an in-tree library built from other
+    sources, so a stale pushed binary can neither be tested nor benchmarked."""
+    from tmhpvsim_amd import build
+    _lib.load()
+    assert _lib.loaded_stamp() == build.build_stamp() == build.lib_stamp()
+
+
+def test_loader_refuses_a_stale_library(monkeypatch):
+    from tmhpvsim_amd import build
+    L = _lib.load()
+    monkeypatch.delenv("TMHPVSIM_LIB", raising=False)
+    monkeypatch.delenv("TMHPVSIM_ALLOW_STALE", raising=False)
+    monkeypatch.setattr(build, "build_stamp", lambda: "0123456789abcdef")
+    with pytest.raises(_lib.StaleLibraryError, match="other sources"):
+        _lib._check_stamp(L)
+    monkeypatch.setenv("TMHPVSIM_ALLOW_STALE", "1")
+    _lib._check_stamp(L)   # diagnostics override

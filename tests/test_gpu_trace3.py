@@ -299,3 +299,42 @@ def test_c5_shape_compacted_group_equals_batches():
         assert torch.equal(cx.hist, s.hist), ci
         assert _same(cx.acc, s.chain_acc), ci
     assert faulted > n // 4, "the test needs chains that fault (markov AssertionError)"
+
+
+def test_pipelines_closed_in_turn_release_their_streams():
+    """Lifecycle (round 6): a long-lived process builds pipelines in turn (the GPU test
+    session, a pvsim service).  Each BatchPipeline owns dedicated CU-masked streams (a
+    hardware queue each); `close()` / the context manager drains and releases them, so
+    twelve pipelines built and closed one after another never hold more streams than
+    one pipeline does, and the last pipeline's batches still equal tmh_run bit for bit.
+    Reference: /root/reference/tmhpvsim/pvsim.py:86-101 (the long-lived process that owns
+    the model)."""
+    from tmhpvsim_amd import _lib
+    from tmhpvsim_amd.pipeline import BatchPipeline, pipeline_defaults
+    n, secs = 512, 3600
+    cfg = pipeline_defaults("c2", "fp32", seconds=secs)
+    sim = _sim(n, "fp32", steps=secs)
+    base = _lib.live_streams()
+    peak = per = 0
+    for i in range(12):
+        with BatchPipeline(sim, n, secs, cfg, lambda k, i=i: 20_000_000 + (i * 8 + k) * n, torch.device("cuda:0")) as pipe:
+            assert pipe.gated()
+            pipe.run(0, 6)
+            pipe.sync()
+            now = _lib.live_streams() - base
+            per = per or now
+            peak = max(peak, now)
+            assert now > 0, "the dedicated queues are CU-masked streams"
+            if i == 11:   # the last pipeline's batches against separate runs
+                last = {k % len(pipe.ctxs): k for k in range(6)}
+                for ci, k in sorted(last.items()):
+                    cx = pipe.ctxs[ci]
+                    ref = _sim(n, "fp32", chain0=cx.chain0, steps=secs)
+                    r = ref.run(secs, trace=("csi",) + FIELDS)
+                    torch.cuda.synchronize()
+                    for f in FIELDS:
+                        assert _same(cx.trace[f], r[f]), (k, f)
+        assert _lib.live_streams() == base, "close() released every stream the pipeline created"
+        with pytest.raises(RuntimeError, match="closed"):
+            pipe.run(0, 1)
+    assert peak == per, (peak, per)

@@ -60,7 +60,7 @@ class Stats(C.Structure):
                 ("hi", C.c_double), ("chain_acc", C.c_void_p)]
 
 
-EXPORTS = ["tmh_abi_version", "tmh_last_error", "tmh_state_bytes", "tmh_state_offsets", "tmh_plan_bytes",
+EXPORTS = ["tmh_abi_version", "tmh_last_error", "tmh_build_stamp", "tmh_state_bytes", "tmh_state_offsets", "tmh_plan_bytes",
            "tmh_scratch_bytes", "tmh_engine_scratch_bytes", "tmh_workspace_bytes", "tmh_engine_create", "tmh_engine_destroy", "tmh_engine_path",
            "tmh_init", "tmh_run", "tmh_plan", "tmh_step", "tmh_probe", "tmh_profile_enable", "tmh_profile_read",
            "tmh_set_shape_tables", "tmh_set_sites", "tmh_walk", "tmh_expand",
@@ -79,8 +79,40 @@ class TmhError(RuntimeError):
     pass
 
 
+class StaleLibraryError(ImportError):
+    pass
+
+
+def loaded_stamp():
+    """The build stamp compiled into the loaded library ("unstamped" without one)."""
+    L = load()
+    if not hasattr(L, "tmh_build_stamp"):
+        return "unstamped"
+    raw = L.tmh_build_stamp().decode()
+    return raw.split(":", 1)[1] if raw.startswith("TMHSTAMP:") else raw
+
+
+def _check_stamp(L):
+    """The in-tree library must carry the stamp of the sources beside it (build.build_stamp):
+    a stale pushed binary is refused instead of being tested or benchmarked silently.
+    A library named by TMHPVSIM_LIB (same-box A/B builds of other sources) is not checked;
+    TMHPVSIM_ALLOW_STALE=1 skips the check (diagnostics only)."""
+    if os.environ.get("TMHPVSIM_LIB") or os.environ.get("TMHPVSIM_ALLOW_STALE") == "1":
+        return
+    from .build import build_stamp
+    want = build_stamp()
+    have = None
+    if hasattr(L, "tmh_build_stamp"):
+        L.tmh_build_stamp.restype = C.c_char_p
+        raw = L.tmh_build_stamp().decode()
+        have = raw.split(":", 1)[1] if raw.startswith("TMHSTAMP:") else raw
+    if have != want:
+        raise StaleLibraryError(f"{LIB_PATH} was built from other sources (stamp {have}, sources {want}): "
+                                "rebuild it with `python -c 'import __graft_entry__ as g; g.build()'`")
+
+
 def load():
-    """Load libtmhpvsim.so (raises if it is missing: no fallback)."""
+    """Load libtmhpvsim.so (raises if it is missing or stale: no fallback)."""
     global _lib
     if _lib is not None:
         return _lib
@@ -93,6 +125,9 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
     L = C.CDLL(LIB_PATH)
+    _check_stamp(L)
+    if hasattr(L, "tmh_build_stamp"):
+        L.tmh_build_stamp.restype = C.c_char_p
     p, u32, u64, i64, sz = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int64, C.c_size_t
     L.tmh_abi_version.restype = C.c_int
     L.tmh_last_error.restype = C.c_char_p
@@ -164,13 +199,14 @@ def check(rc):
     return rc
 
 
-_streams = []   # (device, handle) of the streams cu_stream created
+_streams = []   # (device, handle) of the live streams cu_stream created (process-wide)
 
 
 def _destroy_streams():
-    """At interpreter exit: drain and destroy the streams cu_stream created, before the
-    HIP runtime's own teardown (a CU-masked stream still alive when the runtime is
-    finalised crashed the process's exit under rocprofv3's kernel trace)."""
+    """At interpreter exit: drain and destroy the streams cu_stream created that nobody
+    released (release_stream), before the HIP runtime's own teardown (a CU-masked stream
+    still alive when the runtime is finalised crashed the process's exit under
+    rocprofv3's kernel trace)."""
     import torch
     while _streams:
         dev, h = _streams.pop()
@@ -181,18 +217,41 @@ def _destroy_streams():
             pass
 
 
+def live_streams():
+    """How many streams cu_stream created are alive (not yet released)."""
+    return len(_streams)
+
+
 def cu_stream(cu_first, cu_count, device):
     """A torch stream over a HIP stream restricted to CU-mask bits cu_first ..
-    cu_first + cu_count - 1 (tmh_stream_create_cus; cu_count 0 = all CUs).  The
-    stream lives until the interpreter exits (destroyed then, `_destroy_streams`)."""
+    cu_first + cu_count - 1 of `device` (tmh_stream_create_cus; cu_count 0 = all CUs).
+    Created with `device` current (the HIP call builds the mask and the stream on the
+    current device).  Release it with release_stream (BatchPipeline.close does); what is
+    still alive at interpreter exit is destroyed then (_destroy_streams).  A CU-masked HIP
+    stream is blocking (it synchronises with the legacy null stream); the pipelines issue
+    nothing on the null stream."""
     import atexit
     import torch
+    dev = torch.device(device)
     h = C.c_void_p()
-    check(load().tmh_stream_create_cus(cu_first, cu_count, C.byref(h)))
-    if not _streams:
+    with torch.cuda.device(dev):
+        check(load().tmh_stream_create_cus(cu_first, cu_count, C.byref(h)))
+    if not _streams and not getattr(cu_stream, "_atexit", False):
         atexit.register(_destroy_streams)   # registered after torch's handlers, so it runs before them (LIFO)
-    _streams.append((device, h.value))
-    return torch.cuda.ExternalStream(h.value, device=device)
+        cu_stream._atexit = True
+    _streams.append((dev, h.value))
+    return torch.cuda.ExternalStream(h.value, device=dev)
+
+
+def release_stream(stream):
+    """Drain and destroy a stream cu_stream / dedicated_stream created (no-op for others)."""
+    for i, (dev, h) in enumerate(_streams):
+        if h == stream.cuda_stream:
+            stream.synchronize()
+            _streams.pop(i)
+            check(load().tmh_stream_destroy(h))
+            return True
+    return False
 
 
 def dedicated_stream(device):
@@ -202,7 +261,7 @@ def dedicated_stream(device):
     stream of the process -- torch's stream pool included -- and a queue runs its
     packets in order across the streams sharing it; a CU-masked stream always gets a
     queue of its own, so the pipeline's streams never wait behind each other's kernels
-    whatever GPU_MAX_HW_QUEUES is.  Destroyed at interpreter exit (cu_stream)."""
+    whatever GPU_MAX_HW_QUEUES is.  Released by release_stream (cu_stream)."""
     import torch
     ncu = torch.cuda.get_device_properties(device).multi_processor_count
     return cu_stream(0, ncu, device)

@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import os
+import re
 import shutil
 import subprocess
 
@@ -29,7 +30,6 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off"]
 def _code_only(text):
     """C / C++ source without comments and blank-line / trailing-space differences: what
     the compiler sees (a comment-only edit does not change the stamp)."""
-    import re
     out, i, n = [], 0, len(text)
     pat = re.compile(r'//[^\n]*|/\*.*?\*/|"(?:\\.|[^"\\])*"|\'(?:\\.|[^\'\\])*\'', re.S)
     for m in pat.finditer(text):
@@ -54,10 +54,24 @@ def build_stamp():
     return h.hexdigest()[:16]
 
 
+def lib_stamp(path=LIB):
+    """The build stamp compiled into a built library (tmh_build_stamp's string, read from
+    the file's bytes without loading it), or None for an unstamped or missing library."""
+    if not os.path.exists(path):
+        return None
+    m = re.search(rb"TMHSTAMP:([0-9a-f]{16})", open(path, "rb").read())
+    return m.group(1).decode() if m else None
+
+
 def build_lib(force=False, verbose=False):
-    if not force and os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(d) for d in DEPS):
+    """Compile libtmhpvsim.so unless the in-tree library already carries the stamp of
+    the current sources (a library built from other sources -- an older pushed binary,
+    an A/B build copied over it -- is rebuilt, whatever its mtime)."""
+    stamp = build_stamp()
+    if not force and lib_stamp() == stamp:
         return LIB
-    cmd = [hipcc(), f"--offload-arch={ARCH}"] + FLAGS + ["-I", os.path.join(ROOT, "include"), "-o", LIB + ".tmp"] + SRC
+    cmd = [hipcc(), f"--offload-arch={ARCH}"] + FLAGS + [f'-DTMH_BUILD_STAMP="TMHSTAMP:{stamp}"',
+                                                          "-I", os.path.join(ROOT, "include"), "-o", LIB + ".tmp"] + SRC
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

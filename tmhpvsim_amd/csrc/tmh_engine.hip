@@ -2800,6 +2800,11 @@ extern "C" {
 
 int tmh_abi_version(void) { return TMH_ABI_VERSION; }
 
+#ifndef TMH_BUILD_STAMP
+#define TMH_BUILD_STAMP "unstamped"   // tmhpvsim_amd/build.py defines "TMHSTAMP:<hash of the sources + flags>"
+#endif
+const char* tmh_build_stamp(void) { return TMH_BUILD_STAMP; }
+
 const char* tmh_last_error(void) { return g_err.c_str(); }
 
 size_t tmh_state_bytes(uint32_t n_chains)

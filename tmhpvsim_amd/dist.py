@@ -90,6 +90,9 @@ def all_reduce_stats(tot: dict, group=None) -> dict:
     import torch
     import torch.distributed as dist
 
+    if "energy_fx" not in tot:
+        raise KeyError("all_reduce_stats needs the exact energy limbs 'energy_fx' of chain_totals(); a totals dict "
+                       "of the pre-round-5 format (fp64 energies only) cannot be reduced partition-independently")
     limbs = tot["energy_fx"]
     hist = tot.get("hist")
     dev = limbs.device if hist is None else hist.device

@@ -114,6 +114,14 @@ class BatchPipeline:
         prio_lo, prio_hi = torch.cuda.Stream.priority_range()
         self._prio = lambda s: prio_hi if s == "high" else prio_lo
         pipe = self
+        # every stream this pipeline creates: close() drains them and releases the CU-masked
+        # ones (a long-lived process that builds pipelines in turn -- the GPU test session, a
+        # pvsim service -- would otherwise accumulate hardware queues until exit)
+        self._owned, self._closed = [], False
+
+        def own(st):
+            pipe._owned.append(st)
+            return st
 
         def mk(prio="normal"):
             # HIP maps plain streams round-robin onto GPU_MAX_HW_QUEUES hardware queues (4 by
@@ -124,8 +132,8 @@ class BatchPipeline:
             # at any GPU_MAX_HW_QUEUES.  (High-priority streams keep HIP's priority pool: the
             # CU-masked constructor takes no priority.)
             if cfg.queues == "dedicated" and prio != "high":
-                return _lib.dedicated_stream(device)
-            return torch.cuda.Stream(device, priority=pipe._prio(prio))
+                return own(_lib.dedicated_stream(device))
+            return own(torch.cuda.Stream(device, priority=pipe._prio(prio)))
         self._mk = mk
 
         class Ctx:   # one batch in flight: its own state, plan, scratch, outputs and HIP streams
@@ -209,10 +217,11 @@ class BatchPipeline:
             self.bst = mk(cfg.build_priority)
             if cfg.walk_cus:   # the walks on a share of every XCD's CUs (CU-masked streams)
                 ncu = torch.cuda.get_device_properties(device).multi_processor_count
-                self.wsts = [_lib.cu_stream(0, cfg.walk_cus, device) for _ in range(W)]
+                self.wsts = [own(_lib.cu_stream(0, cfg.walk_cus, device)) for _ in range(W)]
                 if cfg.other_cus == "rest":
-                    self.bst, self._cst = (_lib.cu_stream(cfg.walk_cus, ncu - cfg.walk_cus, device) for _ in range(2))
-                    self.estream = _lib.cu_stream(cfg.walk_cus, ncu - cfg.walk_cus, device)
+                    self.bst, self._cst = (own(_lib.cu_stream(cfg.walk_cus, ncu - cfg.walk_cus, device))
+                                           for _ in range(2))
+                    self.estream = own(_lib.cu_stream(cfg.walk_cus, ncu - cfg.walk_cus, device))
             self.eptr = C.c_void_p(self.estream.cuda_stream)
             self.bst_p = C.c_void_p(self.bst.cuda_stream)
         self.A = cfg.build_ahead
@@ -231,6 +240,26 @@ class BatchPipeline:
                 self.swalked = [torch.cuda.Event() for _ in self.split]
                 self.splanned = [torch.cuda.Event() for _ in self.split]
                 self.sdone = None   # the last split batch's expansions are done (its buffers are free)
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self):
+        """Drain every stream of the pipeline and release the CU-masked ones
+        (_lib.release_stream); the pipeline is unusable afterwards.  Idempotent."""
+        if self._closed:
+            return
+        self.torch.cuda.synchronize(self.dev)
+        for st in self._owned:
+            st.synchronize()
+            _lib.release_stream(st)
+        self._owned.clear()
+        self._closed = True
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
 
     # ------------------------------------------------------------------ helpers
     @property
@@ -531,6 +560,8 @@ class BatchPipeline:
         next batches on their own streams beside them, so the one-wave-per-SIMD walks
         overlap the expansion instead of running in lockstep with it.  The caller
         synchronises (the outputs of batch k sit in context k % pipeline)."""
+        if self._closed:
+            raise RuntimeError("BatchPipeline is closed")
         cfg = self.cfg
         if self.nwin > 1 and cfg.compact and cfg.mode == "stats" and self.sim.path == "time_parallel":
             P = len(self.ctxs)   # compacted windows: one group of batches (one per context) at a time
@@ -568,7 +599,11 @@ class BatchPipeline:
 
     def totals(self):
         """stats mode: the node-local totals over every context (histogram, energies, peak;
-        dist.chain_totals: every chain's accumulated seconds, exact integer energy sums)."""
+        dist.chain_totals: every chain's accumulated seconds, exact integer energy sums).
+        A context's per-chain accumulators keep adding over every batch run on it until
+        reset_stats(); the fixed-point grid holds |energy| < 2^42 W s per chain slot (~15
+        chain-years at 9 kW): past it chain_totals raises OverflowError, so reset between
+        runs longer than that."""
         from .dist import chain_totals
         hist = sum(cx.hist for cx in self.ctxs)
         return chain_totals(self.torch.cat([cx.acc for cx in self.ctxs], dim=1), hist)
