@@ -88,6 +88,40 @@ def test_probe_math():
     # and its min(csi, csimax) = v_med3_f32(csi, -inf, csimax): csimax on a NaN csi (measured on
     # MI355X, round 4), as fminf(NaN, csimax) gave
     np.testing.assert_array_equal(probe(10, 1.25, x), [1.25, -5.0, 0.5, 1.25, 1.25])
+    # round 6: the fp32 kernels' min(csi, csimax) as a plain v_min_f32 with the bound in an SGPR
+    # (pv_power_f<true>): the same results, csimax on a NaN csi
+    np.testing.assert_array_equal(probe(16, 1.25, x), [1.25, -5.0, 0.5, 1.25, 1.25])
+
+
+def test_probe_noise_table_quantile():
+    """Round 6: the fp32 kernels' per-second noise quantile from the segment table
+    (ndtri_t: a cubic per 1/32 octave of min(u, 1 - u), the log form below 2^-15) against
+    the fp64 quantile of the same 32-bit words: <= 6e-7 absolute on the table's range over
+    random words, every segment's ends, both halves and the word range's extremes; below
+    2^-15 it is round 5's log form (ndtri_w, probe 15) bit for bit, <= 1.5e-6 there.  Reference: the per-second noise
+    draw, /root/reference/tmhpvsim/clearskyindexmodel.py:146-147."""
+    from tmhpvsim_amd.engine import probe
+    rng = np.random.default_rng(11)
+    w = rng.integers(0, 2 ** 32, 200000, dtype=np.uint64)
+    # every segment's first and last words (both halves) and the log form's range (u < 2^-15)
+    e = np.arange(112, 126)
+    top = np.arange(32)
+    lo = (2.0 ** (e[:, None] - 127) * (1 + top[None, :] / 32.0)).ravel()
+    hi = (2.0 ** (e[:, None] - 127) * (1 + (top[None, :] + 1) / 32.0)).ravel()
+    words = np.concatenate([lo * 2.0 ** 32, hi * 2.0 ** 32 - 1]).astype(np.int64).clip(0, 2 ** 31 - 1)
+    words = np.concatenate([words, rng.integers(0, 2 ** 17, 5000), [0, 1, 2, 2 ** 31 - 2, 2 ** 31 - 1]])
+    words = np.concatenate([words, 2 ** 32 - 1 - words, w.astype(np.int64)]).astype(np.float64)
+    u = (words + 0.5) * 2.0 ** -32
+    ref = O.ndtri(u)
+    z = probe(14, 0, words)
+    err = np.abs(z - ref)
+    tab = np.minimum(u, 1 - u) >= 2.0 ** -15     # the table's range; below it the log form
+    assert err[tab].max() <= 6e-7, (err[tab].max(), words[tab][err[tab].argmax()])
+    zw = probe(15, 0, words)                     # round 5's form on the same words
+    np.testing.assert_array_equal(z[~tab], zw[~tab])
+    # the log form's own accuracy in the far tails (|z| > 4.1): <= 1.5e-6 absolute (3e-7 relative)
+    assert np.abs(zw - ref).max() <= 1.5e-6 and err.max() <= 1.5e-6, (np.abs(zw - ref).max(), err.max())
+    assert (np.sign(z[np.abs(ref) > 1e-6]) == np.sign(ref[np.abs(ref) > 1e-6])).all()
 
 
 # ------------------------------------------------------------------ reference fixtures

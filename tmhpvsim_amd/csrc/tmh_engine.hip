@@ -389,6 +389,28 @@ __global__ __launch_bounds__(256) void geom_kernel(GParams gp, int64_t step0, ui
     o32[G_RB + G32] = (float)(g[G_RB] - g[G_TERM2]);   // sky = dhi (term2 + AI (Rb - term2))
 }
 
+// The kind of each four-step group (first row j with (step0 + j) % 4 == 0, j + 3 < n) of a
+// window on the four-step grid, ORed into its first fp32 row's flags: FL_G_NIGHT (four night
+// seconds), FL_G_DAY (four daylight seconds with DISC valid); either only when seconds 1-3
+// carry no boundary event.  Other windows and partial groups get neither bit.
+__global__ __launch_bounds__(256) void group_kind_kernel(int64_t step0, uint32_t n, float* tab32)
+{
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x, j = 4 * g;
+    if ((step0 & 3) != 0 || j + 3 >= n) return;
+    uint32_t f[4], ev = 0, all = ~0u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        f[q] = __float_as_uint(tab32[(size_t)(j + q) * ROW32 + G_FLAGS + G32]);
+        all &= f[q];
+        if (q > 0) ev |= f[q] & (FL_DAY | FL_HOUR | FL_MIN);
+    }
+    const uint32_t anyn = (f[0] | f[1] | f[2] | f[3]) & FL_NIGHT;
+    uint32_t k = 0;
+    if (!ev && (all & FL_NIGHT)) k = FL_G_NIGHT;
+    else if (!ev && !anyn && (all & FL_DISCOK)) k = FL_G_DAY;
+    if (k) tab32[(size_t)j * ROW32 + G_FLAGS + G32] = __uint_as_float(f[0] | k);
+}
+
 // Compact the window's day/hour boundary steps, in order (one workgroup).
 // Every such boundary is also a minute boundary (local second 0 = UTC second 0
 // for whole-minute offsets), so only one row per minute is inspected.
@@ -1777,17 +1799,19 @@ __global__ __launch_bounds__(256) void block_rec_kernel(uint32_t n, int64_t W0, 
 // 32-bit byte offset, non-temporal (the trace is written once); no per-lane 64-bit
 // address arithmetic.  0x00020000: gfx9 raw-buffer dword 3.  Offsets past
 // num_records are dropped by the range check (lanes past the last chain)
+// a non-temporal trace store at lane byte offset `off` (range-checked) plus the row's
+// wave-uniform offset `soff` (the store's scalar offset)
 template <typename R>
-__device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t rs, uint32_t off, R v)
+__device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t soff, R v)
 {
     if constexpr (sizeof(R) == 8)
     {
         typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
         const uint64_t u = (uint64_t)__double_as_longlong(v);
-        __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)u, (uint32_t)(u >> 32)}, rs, (int)off, 0, 2 /* nt */);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)u, (uint32_t)(u >> 32)}, rs, (int)off, (int)soff, 2 /* nt */);
     }
     else
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (int)off, 0, 2 /* nt */);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (int)off, (int)soff, 2 /* nt */);
 }
 
 // One work-item per (chain, block of 128 seconds).  The boundary draws come
@@ -1870,7 +1894,8 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
                                             const BlockDesc* __restrict__ desc, const SegView& sg,
                                             const TraceView& tr, const StatsView& sv, uint32_t* lds_hist,
                                             uint32_t (*cov_lds)[WGT], R (*min_lds)[WGT], uint4* held_lds,
-                                            const PV64* pv_lds, const double* pv_lds_tab, float* row_lds)
+                                            const PV64* pv_lds, const double* pv_lds_tab, float* row_lds,
+                                            const float4* nd_lds)
 {
     // TMH_ROW_LDS: the tile's fp32 geometry rows copied to LDS once (coalesced vector loads),
     // read back per second with broadcast ds_reads instead of per-second scalar loads
@@ -1978,7 +2003,11 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
         __syncthreads();
     }
     __amdgpu_buffer_rsrc_t rs_pv, rs_m, rs_r;
-    uint32_t voff = live ? c * (uint32_t)sizeof(R) : 0x80000000u;
+    // the lane's byte offset in a trace row (lanes past the last chain at 2^31: outside the
+    // resource's range, so their stores are dropped without an exec mask); the row's offset
+    // within the block goes in the stores' scalar offset (range checks use the lane offset
+    // only), so a second's stores cost no VALU for addressing
+    const uint32_t voff = live ? c * (uint32_t)sizeof(R) : 0x80000000u;
     const uint32_t rowb = (uint32_t)(tr.ld * sizeof(R));
     if constexpr (out_base(OUT) == OUT_TRACE3) {
         const size_t bo = (size_t)j0 * tr.ld * sizeof(R);
@@ -2000,8 +2029,69 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
     // per-chain sites: some lane's site sees daylight in this block (else every second of the
     // wave is night: no noise block, no geometry)
     const bool wave_day = !SITES || __builtin_amdgcn_ballot_w64(live && !blk_night) != 0;
-    auto second = [&](uint32_t j, uint32_t un, uint32_t um, auto ff) __attribute__((always_inline)) {
+    // _next_day / _next_hour / _next_min at step j (flags fl): the pushes of the day and hour
+    // draws (event table) and of the block's staged minute draws
+    auto apply_events = [&](uint32_t j, uint32_t fl) __attribute__((always_inline)) {
+        if (fl & (FL_DAY | FL_HOUR)) {            // _next_day, _next_hour (rare: loads waited here)
+            const size_t eo = (size_t)evi * 4 * n;
+            if (live) {
+                if (fl & FL_DAY) fpush(fs, S_CLEAR_DAY, (R)evd[eo + 2 * (size_t)n]);
+                if (fl & FL_HOUR) {
+                    fpush(fs, S_CC, (R)evd[eo]);
+                    fpush(fs, S_CLEAR_DAY, (R)evd[eo + 3 * (size_t)n]);
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(0);
+            ++evi;
+        }
+        if (fl & FL_MIN) {                         // _next_min: staged minute draws
+            const int32_t mi = ((int32_t)j - (int32_t)fm) / 60;
+            const int32_t k = mi - mA;   // wave-uniform
+            const int32_t kk = min(k, 1);
+            R ncl = min_lds[2 * kk][threadIdx.x], ncr = min_lds[2 * kk + 1][threadIdx.x];
+            if (k >= 2) {   // a third boundary in the block (its first within 8 s of the start): rare
+                if (live) {
+                    const R* mt = reinterpret_cast<const R*>(sg.mtab) + (size_t)(2 * mi) * n + c;
+                    ncl = mt[0];
+                    ncr = mt[n];
+                }
+                __builtin_amdgcn_s_waitcnt(0);   // wait here, not at the join every minute
+            }
+            fpush(fs, S_CLOUDY_NOISE, ncl);
+            fpush(fs, S_CLEAR_NOISE, ncr);
+        }
+    };
+    // the second's outputs: NaN on a faulted lane, the guard-band bit, the trace stores or
+    // the statistics (jb = j - j0, wave-uniform)
+    auto finish = [&](uint32_t j, uint32_t jb, bool covered, R csi, R pv, R meter, R res, bool held, auto ff)
+        __attribute__((always_inline)) {
         constexpr bool FF = decltype(ff)::value;
+        const bool ok = FF || (int32_t)j < fault_eff;
+        held = held && ok && live;   // lanes past the last chain run on uninitialised samplers: never held
+        if constexpr (sizeof(R) == 4) {
+            if (held) {   // jb is wave-uniform: the word and the bit are scalars
+                uint32_t* hw = reinterpret_cast<uint32_t*>(&held_lds[threadIdx.x]) + (jb >> 5);
+                *hw |= 1u << (jb & 31);
+            }
+        }
+        if constexpr (!FF) {
+            csi = ok ? csi : R(NAN);
+            pv = ok ? pv : R(NAN);
+            meter = ok ? meter : R(NAN);
+            res = ok ? res : R(NAN);
+        }
+        const uint8_t cov = ok ? (covered ? 1 : 0) : 255;
+        if constexpr (out_base(OUT) == OUT_TRACE3) {
+            const uint32_t so = jb * rowb;
+            row_store(rs_pv, voff, so, pv);
+            row_store(rs_m, voff, so, meter);
+            row_store(rs_r, voff, so, res);
+        } else if (live) {
+            emit<R, OUT, exp_hist_pack<R, OUT, SITES>()>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter,
+                                                         res, acc, ok, held);
+        }
+    };
+    auto second = [&](uint32_t j, uint32_t un, uint32_t um, auto ff) __attribute__((always_inline)) {
         R row[row_w<R>()];
         uint32_t fl;
         if constexpr (ROWL) {
@@ -2015,42 +2105,7 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
             rowp += RW;
             fl = sizeof(R) == 8 ? (uint32_t)(double)rowp[G_FLAGS - RW] : __float_as_uint(row[G_FLAGS + G32]);
         }
-        const bool ok = FF || (int32_t)j < fault_eff;
-        if (fl & (FL_DAY | FL_HOUR)) {            // _next_day, _next_hour (rare: loads waited here)
-            const size_t eo = (size_t)evi * 4 * n;
-            if (live) {
-                if (fl & FL_DAY) {
-                    fs.b[S_CLEAR_DAY] = fs.a[S_CLEAR_DAY];
-                    fs.a[S_CLEAR_DAY] = (R)evd[eo + 2 * (size_t)n];
-                }
-                if (fl & FL_HOUR) {
-                    fs.b[S_CC] = fs.a[S_CC];
-                    fs.a[S_CC] = (R)evd[eo];
-                    fs.b[S_CLEAR_DAY] = fs.a[S_CLEAR_DAY];
-                    fs.a[S_CLEAR_DAY] = (R)evd[eo + 3 * (size_t)n];
-                }
-            }
-            __builtin_amdgcn_s_waitcnt(0);
-            ++evi;
-        }
-        if (fl & FL_MIN) {                         // _next_min: staged minute draws
-            const int32_t mi = ((int32_t)j - (int32_t)fm) / 60;
-            fs.b[S_CLOUDY_NOISE] = fs.a[S_CLOUDY_NOISE];
-            fs.b[S_CLEAR_NOISE] = fs.a[S_CLEAR_NOISE];
-            const int32_t k = mi - mA;   // wave-uniform
-            const int32_t kk = min(k, 1);
-            R ncl = min_lds[2 * kk][threadIdx.x], ncr = min_lds[2 * kk + 1][threadIdx.x];
-            if (k >= 2) {   // a third boundary in the block (its first within 8 s of the start): rare
-                if (live) {
-                    const R* mt = reinterpret_cast<const R*>(sg.mtab) + (size_t)(2 * mi) * n + c;
-                    ncl = mt[0];
-                    ncr = mt[n];
-                }
-                __builtin_amdgcn_s_waitcnt(0);   // wait here, not at the join every minute
-            }
-            fs.a[S_CLOUDY_NOISE] = ncl;
-            fs.a[S_CLEAR_NOISE] = ncr;
-        }
+        apply_events(j, fl);
         const uint32_t jb = j - j0;   // wave-uniform
         if ((jb & 31) == 0) cov_w = cov_lds[jb >> 5][threadIdx.x];
         const bool covered = (cov_w >> (jb & 31)) & 1u;
@@ -2081,31 +2136,43 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
                 second_body<R>(kp, pkv, row, flp, fs, covered, ndtri64(un, (LdsD*)pv_lds_tab), meter_w<R>(um), csi, pv,
                                meter, res, held, p, (LdsD*)pv_lds_tab);
             } else {
-                second_body<R>(kp, pkv, row, flp, fs, covered, noise_z<R>(un), meter_w<R>(um), csi, pv, meter, res, held);
+                second_body<R, !SITES && !ROWL>(kp, pkv, row, flp, fs, covered, noise_lds<R>(un, nd_lds), meter_w<R>(um),
+                                                csi, pv, meter, res, held);
             }
         }
-        held = held && ok && live;   // lanes past the last chain run on uninitialised samplers: never held
-        if constexpr (sizeof(R) == 4) {
-            if (held) {   // jb is wave-uniform: the word and the bit are scalars
-                uint32_t* hw = reinterpret_cast<uint32_t*>(&held_lds[threadIdx.x]) + (jb >> 5);
-                *hw |= 1u << (jb & 31);
-            }
+        finish(j, jb, covered, csi, pv, meter, res, held, ff);
+    };
+    // fp32 single-site kernels (C2 trace, C3 / C4 statistics): four-second groups whose kind the
+    // plan gives on the group's first row (geom_kernel: FL_G_NIGHT, FL_G_DAY -- every second
+    // night, or every second daylight with DISC valid, and no boundary event after the first
+    // second; a window start on the four-step grid makes every minute, hour and day boundary
+    // a group's first second).  Such a group applies its first second's events once and runs
+    // four straight-line seconds with no flag tests; a night second is its meter alone (no
+    // row loads).  Other groups (sunrise, sunset, DISC's zenith limit) take the per-second path.
+    constexpr bool FASTG = sizeof(R) == 4 && !SITES && !ROWL && out_base(OUT) != OUT_ANY;
+    auto night4 = [&](uint32_t j, const U4& pm, auto ff) __attribute__((always_inline)) {
+        const uint32_t w[4] = {pm.x, pm.y, pm.z, pm.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const R meter = meter_w<R>(w[q]);
+            finish(j + q, j + q - j0, false, R(0), R(0), meter, meter, false, ff);
         }
-        if constexpr (!FF) {
-            csi = ok ? csi : R(NAN);
-            pv = ok ? pv : R(NAN);
-            meter = ok ? meter : R(NAN);
-            res = ok ? res : R(NAN);
-        }
-        const uint8_t cov = ok ? (covered ? 1 : 0) : 255;
-        if constexpr (out_base(OUT) == OUT_TRACE3) {
-            row_store(rs_pv, voff, pv);
-            row_store(rs_m, voff, meter);
-            row_store(rs_r, voff, res);
-            voff += rowb;
-        } else if (live) {
-            emit<R, OUT, exp_hist_pack<R, OUT, SITES>()>(tr, sv, lds_hist, (uint64_t)j * tr.ld + c, cov, csi, pv, meter,
-                                                         res, acc, ok, held);
+    };
+    auto day4 = [&](uint32_t j, const U4& pn, const U4& pm, auto ff) __attribute__((always_inline)) {
+        const uint32_t wn[4] = {pn.x, pn.y, pn.z, pn.w}, wm[4] = {pm.x, pm.y, pm.z, pm.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            R row[ROW32];
+#pragma unroll
+            for (int i = 0; i < ROW32; ++i) row[i] = rowp[i];
+            rowp += RW;
+            const uint32_t jb = j + q - j0;
+            const bool covered = (cov_w >> (jb & 31)) & 1u;
+            R csi, pv, meter, res;
+            bool held = false;
+            second_body<R, true>(kp, pkv, row, FL_DISCOK, fs, covered, noise_lds<R>(wn[q], nd_lds), meter_w<R>(wm[q]),
+                                 csi, pv, meter, res, held);
+            finish(j + q, jb, covered, csi, pv, meter, res, held, ff);
         }
     };
     // The per-second draws: the meter's and the noise's streams, one Philox block per four
@@ -2119,6 +2186,23 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
             for (; j + 4 <= j1; j += 4) {
                 const uint64_t g = (uint64_t)(W0 + j) >> 2;
                 const U4 pm = keyed_block(kp.seed, chain, g, TAG_METER4, 0);
+                if constexpr (FASTG) {
+                    const uint32_t fl0 = __float_as_uint((float)rowp[G_FLAGS + G32]);   // the group's first row
+                    if (!kp.with_pv || (fl0 & FL_G_NIGHT)) {
+                        apply_events(j, fl0);
+                        if (((j - j0) & 31) == 0) cov_w = cov_lds[(j - j0) >> 5][threadIdx.x];
+                        rowp += 4 * RW;
+                        night4(j, pm, ff);
+                        continue;
+                    }
+                    if (fl0 & FL_G_DAY) {
+                        const U4 pn = keyed_block(kp.seed, chain, g, TAG_NOISE4, 0);
+                        apply_events(j, fl0);
+                        if (((j - j0) & 31) == 0) cov_w = cov_lds[(j - j0) >> 5][threadIdx.x];
+                        day4(j, pn, pm, ff);
+                        continue;
+                    }
+                }
                 bool need = out_base(OUT) == OUT_ANY || !kp.with_pv || (SITES && wave_day);
                 if (!need && !SITES) {   // any daylight second among the four (scalar loads of their flags)
                     uint32_t nf = FL_NIGHT;
@@ -2198,11 +2282,15 @@ __global__ __launch_bounds__((exp_wg<R, OUT, SITES>()), (exp_waves<R, OUT, SITES
     __shared__ PV64 pv_lds[1];   // (176 + 16 bytes in the fp32 kernels: unused)
     __shared__ __attribute__((aligned(16))) double pv_tab[sizeof(R) == 8 || SITES ? PV_TAB : 2];
     __shared__ __attribute__((aligned(16))) float row_lds[TMH_ROW_LDS && sizeof(R) == 4 && !SITES ? BLOCK_STEPS * ROW32 : 1];
+    // fp32: the noise quantile's table (ndtri_t), 8 KB, copied once per workgroup
+    __shared__ float4 nd_tab[sizeof(R) == 4 ? ND32_N : 1];
     if constexpr (sizeof(R) == 8 || SITES) {
         if (threadIdx.x < PV64_N) reinterpret_cast<double*>(pv_lds)[threadIdx.x] = reinterpret_cast<const double*>(&kp.pv64)[threadIdx.x];
         for (uint32_t i = threadIdx.x; i < PV_TAB; i += blockDim.x) pv_tab[i] = g_pv_tab[i];
-        __syncthreads();
     }
+    if constexpr (sizeof(R) == 4)
+        for (uint32_t i = threadIdx.x; i < ND32_N; i += blockDim.x) nd_tab[i] = g_nd32_tab[i];
+    __syncthreads();
     constexpr bool PACK = exp_hist_pack<R, OUT, SITES>();
     const uint32_t nw = PACK ? (sv.n_bins + 1) / 2 : sv.n_bins;   // 16-bit bin pairs, or bins
     if (sv.hist) {
@@ -2212,7 +2300,7 @@ __global__ __launch_bounds__((exp_wg<R, OUT, SITES>()), (exp_waves<R, OUT, SITES
     auto tile = [&](uint32_t b, uint32_t cblk) __attribute__((always_inline)) {
         expand_tile<R, OUT, SITES, WGT>(b, cblk, kp, dp, st, chain0, n, W0, nsteps, utc0, tab64, tab32, sun, events,
                                         n_events, desc, sg, tr, sv, lds_hist, cov_lds, min_lds, held_lds, pv_lds, pv_tab,
-                                        row_lds);
+                                        row_lds, nd_tab);
     };
     {   // grid: x = time block, y = chain block; XCD-aware tile order (speed only): the
         // hardware deals workgroups round-robin over the 8 XCDs in launch order (x fastest),
@@ -2534,6 +2622,17 @@ __global__ void probe_kernel(int fn, double a, const double* x, double* out, uin
         case 11: v = ndtri64((uint32_t)x[i], (const double*)g_pv_tab); break;
         case 12: v = log_tab(x[i], (const double*)g_pv_tab); break;
         case 13: v = exp_tab(x[i], (const double*)g_pv_tab); break;
+        // the fp32 per-second noise quantile of a 32-bit word: the table form the kernels use
+        // (ndtri_t, g_nd32_tab) and round 5's log form (ndtri_w)
+        case 14: v = (double)ndtri_t((uint32_t)x[i], (const float4*)g_nd32_tab); break;
+        case 15: v = (double)ndtri_w((uint32_t)x[i]); break;
+        case 16: {   // pv_power_f<true>'s min(csi, csimax): v_min_f32 with the bound in an SGPR
+            float c;
+            const float b = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint((float)a)));
+            asm("v_min_f32 %0, %1, %2" : "=v"(c) : "s"(b), "v"((float)x[i]));
+            v = (double)c;
+            break;
+        }
         default: v = NAN;
     }
     out[i] = v;
@@ -2846,6 +2945,81 @@ size_t tmh_engine_scratch_bytes(const struct tmh_engine* eng, uint32_t n_chains,
     return scratch_layout(n_chains, n_steps, nullptr, nullptr, tmh_engine_scratch_rbytes(eng));
 }
 
+// fp64 standard normal quantile on the host, lower half (p <= 0.5): Acklam's rational
+// approximation (1.2e-9 relative) polished by two Halley steps on libm's erfc (to ~1 ulp);
+// only the fp32 noise table is built from it
+static double host_ndtri_lower(double p)
+{
+    static const double a[6] = {-3.969683028665376e+01, 2.209460984245205e+02, -2.759285104469687e+02,
+                                1.383577518672690e+02, -3.066479806614716e+01, 2.506628277459239e+00};
+    static const double b[5] = {-5.447609879822406e+01, 1.615858368580409e+02, -1.556989798598866e+02,
+                                6.680131188771972e+01, -1.328068155288572e+01};
+    static const double c[6] = {-7.784894002430293e-03, -3.223964580411365e-01, -2.400758277161838e+00,
+                                -2.549732539343734e+00, 4.374664141464968e+00, 2.938163982698783e+00};
+    static const double d[4] = {7.784695709041462e-03, 3.224671290700398e-01, 2.445134137142996e+00,
+                                3.754408661907416e+00};
+    double x;
+    if (p < 0.02425) {
+        const double q = std::sqrt(-2.0 * std::log(p));
+        x = (((((c[0] * q + c[1]) * q + c[2]) * q + c[3]) * q + c[4]) * q + c[5]) /
+            ((((d[0] * q + d[1]) * q + d[2]) * q + d[3]) * q + 1.0);
+    } else {
+        const double q = p - 0.5, r = q * q;
+        x = (((((a[0] * r + a[1]) * r + a[2]) * r + a[3]) * r + a[4]) * r + a[5]) * q /
+            (((((b[0] * r + b[1]) * r + b[2]) * r + b[3]) * r + b[4]) * r + 1.0);
+    }
+    for (int it = 0; it < 2; ++it) {
+        const double e = 0.5 * std::erfc(-x * 0.70710678118654752440) - p;
+        const double u = e * 2.50662827463100050242 * std::exp(0.5 * x * x);
+        x = x - u / (1.0 + 0.5 * x * u);
+    }
+    return x;
+}
+
+// g_nd32_tab (ndtri_t): per segment (exponent e, top ND32_S mantissa bits) the cubic in the
+// low ND32_SHIFT bits r that interpolates the fp64 quantile at the four Chebyshev nodes of
+// the segment, solved in x = r 2^-18 (well conditioned) and scaled to r exactly (powers of
+// two), then rounded to fp32.  Deterministic host arithmetic: every engine and process
+// uploads the same bits.
+static int nd32_tab_upload()
+{
+    std::vector<float> t(4 * (size_t)ND32_N, 0.0f);
+    const double PI = 3.14159265358979323846;
+    for (int i = 0; i < ND32_N; ++i) {
+        const int e = ND32_EMIN + (i >> ND32_S), top = i & ((1 << ND32_S) - 1);
+        if (e >= 126) continue;   // uf >= 0.5 (rounded up): z = 0
+        double xk[4], yk[4];
+        for (int k = 0; k < 4; ++k) {
+            xk[k] = 0.5 * (1.0 + std::cos(PI * (2 * k + 1) / 8.0));
+            const double m = (double)top * (double)(1 << ND32_SHIFT) + xk[k] * (double)(1 << ND32_SHIFT);
+            yk[k] = host_ndtri_lower(std::ldexp(1.0 + m * 0x1p-23, e - 127));
+        }
+        double A[4][5];   // Vandermonde in x, Gaussian elimination with partial pivoting
+        for (int k = 0; k < 4; ++k) {
+            double v = 1.0;
+            for (int j = 0; j < 4; ++j) {
+                A[k][j] = v;
+                v *= xk[k];
+            }
+            A[k][4] = yk[k];
+        }
+        for (int col = 0; col < 4; ++col) {
+            int piv = col;
+            for (int r = col + 1; r < 4; ++r)
+                if (std::fabs(A[r][col]) > std::fabs(A[piv][col])) piv = r;
+            for (int j = 0; j < 5; ++j) std::swap(A[col][j], A[piv][j]);
+            for (int r = 0; r < 4; ++r) {
+                if (r == col) continue;
+                const double f = A[r][col] / A[col][col];
+                for (int j = col; j < 5; ++j) A[r][j] -= f * A[col][j];
+            }
+        }
+        for (int j = 0; j < 4; ++j) t[4 * (size_t)i + j] = (float)std::ldexp(A[j][4] / A[j][j], -ND32_SHIFT * j);
+    }
+    return hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_nd32_tab), t.data(), t.size() * sizeof(float)),
+                     "hipMemcpyToSymbol(g_nd32_tab)");
+}
+
 // the table of log_tab / exp_tab / ndtri64 (g_pv_tab) on `device`: the same host values
 // for every engine and process, so every kernel's fp64 PV agrees bit for bit
 static int pv_tab_upload(int device)
@@ -2862,7 +3036,8 @@ static int pv_tab_upload(int device)
         for (int i = 0; i <= NDTRI_DEG; ++i) lt[NDTRI_OFF + NDTRI_STRIDE * q + 1 + i] = NDTRI_COEF[q][i];
     }
     if (int rc = hip_check(hipSetDevice(device), "hipSetDevice")) return rc;
-    return hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_pv_tab), lt, sizeof lt), "hipMemcpyToSymbol(g_pv_tab)");
+    if (int rc = hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_pv_tab), lt, sizeof lt), "hipMemcpyToSymbol(g_pv_tab)")) return rc;
+    return nd32_tab_upload();
 }
 
 int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, struct tmh_engine** out)
@@ -2944,6 +3119,11 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
         f.pacoc = (float)(iv[0] > 0.0 ? iv[0] : 0.0);
         f.eps0 = (float)(k.sqrt6 * 0.001);
         f.eps1 = (float)(k.sqrt6 * (0.0015 * 8));
+        if (f.eps0 != EPS0F || f.eps1 != EPS1F) {   // the fp32 kernels' literals (second_body)
+            delete e;
+            return fail(TMH_E_INVAL, "fp32 noise-scale literals differ from the host's (%a, %a)", (double)f.eps0,
+                        (double)f.eps1);
+        }
         PV64& d = k.pv64;   // the same forms in fp64 (ln, not log2: pv_power_d's log is natural)
         d.tk = k.tmod_k + m[TMH_MOD_TEMP_DT] * 1e-3;
         d.temp_air = k.temp_air;
@@ -3214,6 +3394,7 @@ int tmh_plan(struct tmh_engine* eng, int64_t step0, uint32_t n_steps, void* plan
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(geom_kernel, dim3((n_steps + 255) / 256), dim3(256), 0, s, eng->gp, step0, n_steps, pv.tab64,
                        pv.tab32, pv.sun);
+    hipLaunchKernelGGL(group_kind_kernel, dim3((n_steps / 4 + 255) / 256 + 1), dim3(256), 0, s, step0, n_steps, pv.tab32);
     hipLaunchKernelGGL(events_kernel, dim3(1), dim3(1024), 0, s, pv.tab32, step0, n_steps, eng->gp.clock.utc0,
                        pv.events, ev_cap(n_steps), pv.n_events);
     const uint32_t nb = nblk_of(n_steps);
@@ -3511,7 +3692,7 @@ int tmh_debug_walk_prof(unsigned long long* host, uint32_t waves)
 
 int tmh_probe(int fn, double a, const double* x, double* out, uint32_t n, void* stream)
 {
-    if (fn >= 11 && fn <= 13) {   // the table functions need the table on the current device
+    if (fn >= 11 && fn <= 14) {   // the table functions need the tables on the current device
         int dev = 0;
         if (int rc = hip_check(hipGetDevice(&dev), "hipGetDevice")) return rc;
         if (int rc = pv_tab_upload(dev)) return rc;

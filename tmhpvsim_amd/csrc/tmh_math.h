@@ -198,6 +198,34 @@ __device__ __forceinline__ float ndtri_w(uint32_t w)
     return 1.41421356237309505f * (p * x);
 }
 
+// ---- fp32 normal quantile of a 32-bit word from a table (the per-second noise, round 6) ----
+// u = (w + 1/2) 2^-32, t = min(w, ~w) (u -> min(u, 1 - u)), uf = the fp32 value of (t + 1/2) 2^-32
+// (as ndtri_w forms it).  uf's exponent e and its top ND32_S mantissa bits pick a segment of
+// 1/32 octave; ndtri(uf) there is a cubic in the segment's low 18 mantissa bits r, its
+// coefficients in g_nd32_tab (written by the host at engine creation: Chebyshev-node
+// interpolation of the fp64 quantile, then rounded to fp32; tmh_engine.hip nd32_tab_upload).
+// The index is (bits >> 18) & 511: e in [112, 127] (u in [2^-15, 2)), so 16 octaves of which
+// e = 112..125 are used and e = 126 (uf rounded up to 0.5) holds zeros; u < 2^-15 (6e-5 of
+// the draws) takes ndtri_w.  Measured against scipy's ndtri on every segment (numpy
+// emulation of the fp32 Horner): <= 4.6e-7 absolute, the fp32 rounding of |z| ~ 4.
+// 13 VALU (3 FMA for the cubic) instead of ndtri_w's ~25 with a log and a tail branch
+// taken by a fifth of the waves.
+constexpr int ND32_S = 5, ND32_SHIFT = 23 - ND32_S, ND32_N = 512, ND32_EMIN = 112;
+__device__ float4 g_nd32_tab[ND32_N];
+
+template <typename TP>   // TP: const float4* (g_nd32_tab or an LDS copy)
+__device__ __forceinline__ float ndtri_t(uint32_t w, TP tab)
+{
+    const uint32_t m = w ^ (uint32_t)((int32_t)w >> 31);   // min(w, ~w)
+    const uint32_t bits = __float_as_uint(fmaf((float)m, 0x1p-32f, 0x1p-33f));
+    const float4 c = tab[(bits >> ND32_SHIFT) & (uint32_t)(ND32_N - 1)];
+    const float r = (float)(bits & ((1u << ND32_SHIFT) - 1u));
+    float q = fmaf(fmaf(fmaf(c.w, r, c.z), r, c.y), r, c.x);   // ndtri(min(u, 1 - u)) <= 0
+    q = __uint_as_float(__float_as_uint(q) ^ (w & 0x80000000u));   // the upper half by symmetry
+    if (__builtin_expect(bits < ((uint32_t)ND32_EMIN << 23), 0)) q = ndtri_w(w);   // the far tails
+    return q;
+}
+
 __device__ __noinline__ void gamma_pq(double a, double x, double lga, double& P, double& Q)
 {
     if (x <= 0.0) {

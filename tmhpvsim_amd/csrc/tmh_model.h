@@ -20,6 +20,10 @@ namespace tmh {
 //   Bvmpo = bvmpo + mbvmp (1 - Ee)                        nmbvmp = -mbvmp, bvmpo1 = bvmpo + mbvmp
 //   delta log2(Ee) = n k / q (tcell + 273.15) ln(Ee)     nkq = n k / q ln 2, nkq273 = 273.15 nkq
 //   A - B, B, C of the SNL inverter, affine in vmp:       (ab1, ab0), (b1, b0), (c1, c0)
+// sqrt(0.1 * 60) (0.001 + 0.0015 * 8 cc) of clearskyindexmodel.py:146-147 in fp32: model constants,
+// so literals in the kernels (the host checks they equal its PVF::eps0 / eps1)
+constexpr double SQRT6 = 2.449489742783178;
+constexpr float EPS0F = (float)(SQRT6 * 0.001), EPS1F = (float)(SQRT6 * (0.0015 * 8));
 struct PVF {
     float tk, temp_air, fd, nmbvmp, bvmpo1, nkq, nkq273, impo_c0;   // the first PVF_VGPR: pinned in VGPRs
     float impo_c1, aimp, vmpo, c2ns, c3ns;
@@ -73,7 +77,11 @@ struct GParams {
 
 // FL_DISCOK: DISC's zenith test passes (pvlib irradiance.disc max_zenith, the row's
 // G_DISCOK as a flag bit, so the fp32 chain tests a scalar instead of a float per lane)
-enum : uint32_t { FL_DAY = 1, FL_HOUR = 2, FL_MIN = 4, FL_NIGHT = 8, FL_DISCOK = 16 };
+// FL_G_NIGHT / FL_G_DAY (fp32 rows, on the first row of a four-step group of a window whose
+// start is on the four-step grid; group_kind_kernel): the group's four seconds are all night,
+// or all daylight with DISC valid, and its seconds 1-3 carry no boundary event, so the fp32
+// single-site expansion runs the group as straight-line code (expand_tile, FASTG)
+enum : uint32_t { FL_DAY = 1, FL_HOUR = 2, FL_MIN = 4, FL_NIGHT = 8, FL_DISCOK = 16, FL_G_NIGHT = 32, FL_G_DAY = 64 };
 // clock/geometry table row (TMH_GEOM_FIELDS = 20)
 enum {
     G_MINF = 0, G_HOURF = 1, G_DAYF = 2, G_FLAGS = 3, G_COSZ = 4, G_CSIMAX = 5, G_GHICS = 6,
@@ -1315,13 +1323,19 @@ constexpr float KT_GUARD = 4e-6f, PDC_GUARD = 1e-4f;
 // fp32 constants rounded once on the host (KParams::pvf) and the hardware
 // exp / log; within 1e-5 of the fp64 oracle.  `risky`: the second
 // lies in a guard band and must be recomputed in fp64.
+// UROW: the row is wave-uniform (the single-site kernels' scalar loads), so the clamp's bound
+// is an SGPR operand of a plain v_min_f32
+template <bool UROW = false>
 __device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float csi, bool discok, bool& risky)
 {
     // min(csi, csimax) as a median with -inf: no canonicalising max of the row's value first.
     // On a NaN csi it returns csimax, as fminf did (tmh_probe fn 10, test_probe_math); a NaN
     // csi occurs only on lanes whose outputs are masked anyway (faulted chains, lanes past the
     // last chain).
-    const float c = __builtin_amdgcn_fmed3f(csi, -INFINITY, g[G_CSIMAX]);
+    float c;
+    if constexpr (UROW)   // v_min_f32 directly (the compiler's minnum first canonicalises the row value: one op more)
+        asm("v_min_f32 %0, %1, %2" : "=v"(c) : "s"(g[G_CSIMAX]), "v"(csi));
+    else c = __builtin_amdgcn_fmed3f(csi, -INFINITY, g[G_CSIMAX]);
     const float ghi = c * g[G_GHICS];
     const float kt = fminf(fmaxf(ghi * g[G_I0H], 0.0f), 1.0f);
     // DISC Kn: coefficient sets split at kt = 0.6 (compile-time constants, no
@@ -1368,9 +1382,16 @@ __device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float 
 }
 
 // ------------------------------------------------------------ fused per-second body
+// The kernels' sampler pairs (InterpolatedSampler, clearskyindexmodel.py:12-40) in the
+// compute precision.  R = double: (before b, after a), interpolated exactly as the
+// reference (f a + (1 - f) b).  R = float (round 6): the after value a and the
+// difference d = a - b (held in b[k]), so the interpolation is one FMA, a - (1 - f) d,
+// with the row's fp32 1 - f; a push (b <- a, a <- v) is d = v - a, a = v.  Every fp32
+// kernel forms d from the same fp32 values (to_real, set_fast_noise, fpush), so the
+// sequential and time-parallel fp32 paths agree bit for bit.
 template <typename R>
 struct FSamp {
-    R b[6], a[6];
+    R b[6], a[6];   // R = float: b[k] holds a[k] - before
 };
 
 template <typename R>
@@ -1378,24 +1399,35 @@ __device__ __forceinline__ void to_real(FSamp<R>& f, const Samp& s)
 {
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-        f.b[k] = (R)s.b[k];
         f.a[k] = (R)s.a[k];
+        if constexpr (sizeof(R) == 8) f.b[k] = s.b[k];
+        else f.b[k] = (float)s.a[k] - (float)s.b[k];
     }
+}
+
+// push a new after value (InterpolatedSampler.next, clearskyindexmodel.py:34-37)
+template <typename R>
+__device__ __forceinline__ void fpush(FSamp<R>& f, int k, R v)
+{
+    if constexpr (sizeof(R) == 8) f.b[k] = f.a[k];
+    else f.b[k] = v - f.a[k];
+    f.a[k] = v;
 }
 
 // fp32: the noise samplers hold the fast draws (minute_noise_fast), not the state's fp64 ones
 template <typename R>
 __device__ __forceinline__ void set_fast_noise(FSamp<R>& f, float2 cloudy, float2 clear)
 {
-    f.b[S_CLOUDY_NOISE] = cloudy.x;
     f.a[S_CLOUDY_NOISE] = cloudy.y;
-    f.b[S_CLEAR_NOISE] = clear.x;
+    f.b[S_CLOUDY_NOISE] = cloudy.y - cloudy.x;
     f.a[S_CLEAR_NOISE] = clear.y;
+    f.b[S_CLEAR_NOISE] = clear.y - clear.x;
 }
 
 template <typename R>
 __device__ __forceinline__ R rinterp(const FSamp<R>& f, int k, R frac)
 {
+    static_assert(sizeof(R) == 8, "the fp32 samplers interpolate from the row's (1 - f) (rinterp_row)");
     return frac * f.a[k] + (R(1) - frac) * f.b[k];
 }
 
@@ -1406,8 +1438,7 @@ __device__ __forceinline__ R rinterp_row(const FSamp<R>& f, int k, const R* row,
     if constexpr (sizeof(R) == 8) return rinterp(f, k, row[fi]);
     else {
         const int pc = fi == G_MINF ? G32_MINF_C : (fi == G_HOURF ? G32_HOURF_C : G32_DAYF_C);
-        // a multiply and an FMA (2 fast-rate ops) rather than a packed multiply and an add
-        return fmaf(row[pc + 1], f.a[k], row[pc] * f.b[k]);
+        return fmaf(-row[pc], f.b[k], f.a[k]);   // a - (1 - f) (a - b): one FMA
     }
 }
 
@@ -1417,9 +1448,19 @@ __device__ __forceinline__ R rinterp_row(const FSamp<R>& f, int k, const R* row,
 template <typename R>
 __device__ __forceinline__ R noise_z(uint32_t w)
 {
-    // fp64: ndtri64 (<= ~1e-15 relative, far inside the fp64 bar)
+    // fp64: ndtri64 (<= ~1e-15 relative, far inside the fp64 bar); fp32: the table quantile
+    // (ndtri_t, <= 4.6e-7 absolute) read from global memory -- the expansion reads the same
+    // values from its LDS copy, so every fp32 kernel draws the same z
     if constexpr (sizeof(R) == 8) return ndtri64(w, (const double*)g_pv_tab);
-    else return ndtri_w(w);
+    else return ndtri_t(w, (const float4*)g_nd32_tab);
+}
+
+// the same quantile from the expansion's LDS copy of the fp32 table (the fp64 kernels' is ndtri64's)
+template <typename R>
+__device__ __forceinline__ R noise_lds(uint32_t w, const float4* nd_lds)
+{
+    if constexpr (sizeof(R) == 8) return noise_z<R>(w);
+    else return ndtri_t(w, nd_lds);
 }
 
 template <typename R>
@@ -1435,7 +1476,7 @@ __device__ __forceinline__ R meter_w(uint32_t w)
 // risky (fp32 only): pv lies in pv_power_f's guard band; the caller recomputes
 // the second in fp64 (pv_fp64_*) and replaces pv and res
 // (fp64: p64 / lt as pv_power_d's; the defaults read the kernel arguments and ocml's log)
-template <typename R, typename P64 = decltype(nullptr), typename LT = decltype(nullptr)>
+template <typename R, bool UROW = false, typename P64 = decltype(nullptr), typename LT = decltype(nullptr)>
 __device__ __forceinline__ void second_body(const KParams& kp, const PVF& pk, const R* row, uint32_t fl,
                                             const FSamp<R>& fs, bool covered, R z, R meter_in, R& csi, R& pv, R& meter,
                                             R& res, bool& risky, P64 p64 = nullptr, LT lt = nullptr)
@@ -1444,7 +1485,7 @@ __device__ __forceinline__ void second_body(const KParams& kp, const PVF& pk, co
     const R cloudcover = rinterp_row(fs, S_CC, row, G_HOURF);   // == interp() bit for bit when R = double
     R eps;
     if constexpr (sizeof(R) == 8) eps = z * (R(kp.sqrt6) * (R(0.001) + R(0.0015 * 8) * cloudcover)) + R(0);
-    else eps = z * fmaf(pk.eps1, cloudcover, pk.eps0);   // fp32: the scale as one FMA (z is never 0)
+    else eps = z * fmaf(cloudcover, EPS1F, EPS0F);   // fp32: the scale as one FMA on literals (z is never 0)
     // both branches' factors, then a select on values (a select on the sampler
     // index would make the compiler index the sampler arrays dynamically: scratch)
     const R a_clear = rinterp_row(fs, S_CLEAR_DAY, row, G_DAYF), a_cloudy = rinterp_row(fs, S_CLOUDY_HOUR, row, G_HOURF);
@@ -1456,7 +1497,7 @@ __device__ __forceinline__ void second_body(const KParams& kp, const PVF& pk, co
         else
             pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power_d(p64, row, csi, lt) : R(0);
     }
-    else pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power_f(pk, row + G32, csi, (fl & FL_DISCOK) != 0, risky) : 0.0f;
+    else pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power_f<UROW>(pk, row + G32, csi, (fl & FL_DISCOK) != 0, risky) : 0.0f;
     meter = meter_in;
     res = meter - pv;
 }

@@ -314,28 +314,53 @@ class BatchPipeline:
     def compact_batches(self, ks, init=True):
         """Compacted multi-window statistics batches (C5), one per context, advanced window
         by window together: every window after the first runs on the chains still live
-        (tmh_live_chains -> one host read of the counts per window for the whole group ->
-        tmh_state_move gather, tmh_set_chain_ids, tmh_plan + tmh_step, scatter).  The
-        chain ids are engine state read at each launch, so the contexts' launches are
-        issued one context at a time while their streams run concurrently."""
+        (tmh_live_chains -> tmh_state_move gather, tmh_set_chain_ids, tmh_step, scatter).
+        The chain ids are engine state read at each launch, so the contexts' launches are
+        issued one context at a time while their streams run concurrently.
+
+        Round 6: no host drain per window.  Each context's live count goes to pinned host
+        memory behind an event on its own stream, and the host waits for that context's
+        count only, just before issuing its next window -- the other contexts' windows keep
+        the GPU busy meanwhile (round 5 synchronised every context's stream at every window,
+        so all of them drained before any next window was issued).  The window's plan
+        (chain-independent: the same clock / geometry table for every batch of the group)
+        is built once per window on a plan stream, into one of three rotating buffers,
+        instead of once per context."""
         L, sim, n, secs, win = self.L, self.sim, self.n, self.secs, self.win
+        torch = self.torch
         cxs = [self.ctx_of(k) for k in ks]
         assert len({id(c) for c in cxs}) == len(cxs), "one batch per context"
         if init:
             for k, cx in zip(ks, cxs):
                 cx.chain0 = self.chain0_of(k)
                 _lib.check(L.tmh_init(sim._eng, self._p(cx.state), cx.chain0, n, None, cx.sptr))
-        for s0 in range(0, secs, win):
-            w = min(win, secs - s0)
-            nls = [n] * len(cxs)
-            if s0 > 0:
-                for cx in cxs:
-                    _lib.check(L.tmh_live_chains(sim._eng, self._p(cx.state), n, None, self._p(cx.ids),
-                                                 self._p(cx.nlive), cx.sptr))
-                for i, cx in enumerate(cxs):
-                    cx.stream.synchronize()            # n_live was written on the batch's stream
-                    nls[i] = int(cx.nlive.item())
-            for nl, cx in zip(nls, cxs):
+        wins = [(s0, min(win, secs - s0)) for s0 in range(0, secs, win)]
+        NP = 3
+        if getattr(self, "_cplans", None) is None:   # the group's plan buffers and stream
+            self._cplans = [torch.empty(L.tmh_plan_bytes(win), dtype=torch.uint8, device=self.dev) for _ in range(NP)]
+            self._cplan_ev = [torch.cuda.Event() for _ in range(NP)]
+            self._cpst = self._mk()
+        for cx in cxs:
+            if getattr(cx, "nlive_host", None) is None:
+                cx.nlive_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+                cx.counted = torch.cuda.Event()
+                cx.wdone = [torch.cuda.Event() for _ in range(NP)]
+                cx.wdone_used = [False] * NP
+        pst = self._cpst
+        for wi, (s0, w) in enumerate(wins):
+            b = wi % NP
+            plan = self._cplans[b]
+            for cx in cxs:   # the buffer's previous window is done on every context
+                if cx.wdone_used[b]:
+                    pst.wait_event(cx.wdone[b])
+            _lib.check(L.tmh_plan(sim._eng, s0, w, self._p(plan), C.c_void_p(pst.cuda_stream)))
+            self._cplan_ev[b].record(pst)
+            for cx in cxs:
+                nl = n
+                if wi > 0:
+                    cx.counted.synchronize()           # this context's count only
+                    nl = int(cx.nlive_host[0])
+                cx.stream.wait_event(self._cplan_ev[b])
                 sp, cur = self._p(cx.state), cx.state
                 try:
                     if nl < n:
@@ -345,15 +370,21 @@ class BatchPipeline:
                                                         self._p(cx.nlive), nl, 0, cx.sptr))
                             _lib.check(L.tmh_set_chain_ids(sim._eng, self._p(cx.ids), n))
                     if nl:
-                        _lib.check(L.tmh_plan(sim._eng, s0, w, self._p(cx.plan), cx.sptr))
                         _lib.check(L.tmh_step(sim._eng, self._p(cur), cx.chain0, nl, s0, w, None, C.byref(cx.tr),
-                                              C.byref(cx.st), self._p(cx.plan), self._p(cx.scratch),
+                                              C.byref(cx.st), self._p(plan), self._p(cx.scratch),
                                               cx.scratch.numel(), cx.sptr))
                     if nl and cur is cx.work:
                         _lib.check(L.tmh_state_move(sim._eng, self._p(cx.work), nl, sp, n, self._p(cx.ids),
                                                     self._p(cx.nlive), nl, 1, cx.sptr))
                 finally:
                     _lib.check(L.tmh_set_chain_ids(sim._eng, None, 0))
+                cx.wdone[b].record(cx.stream)
+                cx.wdone_used[b] = True
+                if wi + 1 < len(wins):   # the next window's live chains, counted behind this window
+                    _lib.check(L.tmh_live_chains(sim._eng, sp, n, None, self._p(cx.ids), self._p(cx.nlive), cx.sptr))
+                    with torch.cuda.stream(cx.stream):
+                        cx.nlive_host.copy_(cx.nlive, non_blocking=True)
+                    cx.counted.record(cx.stream)
 
     # ------------------------------------------------------------------ round 1's staggered schedule
     def _build(self, k):      # construction of batch k's chains, its plan and draws
