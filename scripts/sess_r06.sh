@@ -33,6 +33,19 @@ print("value %.4g ms/step %.4f kernel %.4f alone %s frac %.3f stamp %s" % (d["va
       r.get("alone", {}).get("kernel_ms"), r.get("frac") or 0, d.get("lib_stamp")))
 PY
       done ;;
+    ab:*)   # ab:<reps>:<VAR>: alternate bench runs with VAR=1 / VAR=0 (C2 defaults)
+      rest="${step#ab:}"; reps="${rest%%:*}"; var="${rest#*:}"
+      for i in $(seq 1 $reps); do
+        for v in 1 0; do
+          env $var=$v timeout -k 10 400 python bench.py --secondary none --no-cpu-baseline > gpurun_out/ab_${TAG}_${v}_$i.json 2> gpurun_out/ab_${TAG}_${v}_$i.err || { echo "bench failed"; tail -5 gpurun_out/ab_${TAG}_${v}_$i.err; exit 1; }
+          python - "gpurun_out/ab_${TAG}_${v}_$i.json" "$var=$v" <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+r = d["roofline"]
+print("%s value %.4g ms/step %.4f kernel %.4f alone %.4f" % (sys.argv[2], d["value"], d["ms_per_step"], r["kernel_ms"], r["alone"]["kernel_ms"]))
+PY
+        done
+      done ;;
     prof)
       ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OLDPWD/gpurun_out/prof_$TAG" -o run -- \
           python3 "$OLDPWD/bench.py" --secondary none --no-cpu-baseline > "$OLDPWD/gpurun_out/prof_$TAG.log" 2>&1 ) || { echo "rocprof failed"; exit 1; }

@@ -34,6 +34,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <type_traits>
@@ -409,6 +410,41 @@ __global__ __launch_bounds__(256) void group_kind_kernel(int64_t step0, uint32_t
     if (!ev && (all & FL_NIGHT)) k = FL_G_NIGHT;
     else if (!ev && !anyn && (all & FL_DISCOK)) k = FL_G_DAY;
     if (k) tab32[(size_t)j * ROW32 + G_FLAGS + G32] = __uint_as_float(f[0] | k);
+}
+
+// The window's 128-s blocks in the order the single-site expansion takes its tiles (round 6):
+// blocks with a daylight second first, then the all-night blocks, each class in time order
+// (a stable partition; one workgroup).  A night tile costs a tenth of a daylight one, so the
+// expansion's last tiles are short ones and its tail no longer waits for late daylight tiles.
+// A block is all night when every four-step group of it carries FL_G_NIGHT; windows off the
+// four-step grid (no group kinds) keep the time order.
+__global__ __launch_bounds__(1024) void block_order_kernel(const float* __restrict__ tab32, int64_t step0, uint32_t n,
+                                                           uint32_t* __restrict__ perm)
+{
+    __shared__ uint32_t cnt[1024];
+    const uint32_t t = threadIdx.x, nb = (n + BLOCK_STEPS - 1) / BLOCK_STEPS;
+    const uint32_t chunk = (nb + 1023) / 1024, lo = min(t * chunk, nb), hi = min(lo + chunk, nb);
+    auto night = [&](uint32_t b) {
+        if ((step0 & 3) != 0) return false;
+        const uint32_t j0 = b * BLOCK_STEPS, j1 = min(j0 + (uint32_t)BLOCK_STEPS, n);
+        if (j1 - j0 < BLOCK_STEPS) return false;   // a short last block: its tail groups carry no kind
+        for (uint32_t j = j0; j < j1; j += 4)
+            if (!(__float_as_uint(tab32[(size_t)j * ROW32 + G_FLAGS + G32]) & FL_G_NIGHT)) return false;
+        return true;
+    };
+    uint32_t d = 0;
+    for (uint32_t b = lo; b < hi; ++b) d += night(b) ? 0u : 1u;
+    cnt[t] = d;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {   // inclusive scan of the daylight counts
+        const uint32_t v = t >= off ? cnt[t - off] : 0;
+        __syncthreads();
+        cnt[t] += v;
+        __syncthreads();
+    }
+    const uint32_t nday = cnt[1023];
+    uint32_t od = cnt[t] - d, on = nday + (lo - od);   // this range's first daylight / night slots
+    for (uint32_t b = lo; b < hi; ++b) perm[night(b) ? on++ : od++] = b;
 }
 
 // Compact the window's day/hour boundary steps, in order (one workgroup).
@@ -1866,7 +1902,13 @@ constexpr bool exp_hist_pack()
 {
     return exp_wg<R, OUT, SITES>() * BLOCK_STEPS * exp_tpw<R, OUT, SITES>() <= 32768;
 }
-constexpr int PVF_VGPR = 0;   // leading PVF fields pinned in VGPRs in the fp32 single-site expansion
+#ifndef TMH_PVF_VGPR
+#define TMH_PVF_VGPR 0
+#endif
+constexpr int PVF_VGPR = TMH_PVF_VGPR;   // leading PVF fields pinned in VGPRs in the fp32 single-site expansion
+#ifndef TMH_EXP_WAVES_TRACE
+#define TMH_EXP_WAVES_TRACE 7
+#endif
 // min waves per SIMD (__launch_bounds__) of each expansion instantiation:
 //  fp32 single-site trace (C2): 7 = at most 72 VGPRs (alone -4 % vs 6, no VGPR spills);
 //  fp32 statistics / other outputs (C3, C4): 6 = 80 VGPRs (the 16-bit-pair LDS histogram,
@@ -1880,7 +1922,7 @@ constexpr int exp_waves()
 #ifndef TMH_EXP_WAVES_F64
 #define TMH_EXP_WAVES_F64 4
 #endif
-    return SITES ? 2 : (sizeof(R) == 8 ? TMH_EXP_WAVES_F64 : (out_base(OUT) == OUT_TRACE3 ? (TMH_ROW_LDS ? TMH_ROW_LDS_WAVES : 7) : 6));
+    return SITES ? 2 : (sizeof(R) == 8 ? TMH_EXP_WAVES_F64 : (out_base(OUT) == OUT_TRACE3 ? (TMH_ROW_LDS ? TMH_ROW_LDS_WAVES : TMH_EXP_WAVES_TRACE) : 6));
 }
 // One (128-second block b, chain block cblk) tile of the expansion: one work-item per
 // chain of the block (the expansion's unit of work, below).  The LDS staging areas are
@@ -2271,7 +2313,7 @@ __global__ __launch_bounds__((exp_wg<R, OUT, SITES>()), (exp_waves<R, OUT, SITES
                                                      const int2* __restrict__ events,
                                                      const uint32_t* __restrict__ n_events,
                                                      const BlockDesc* __restrict__ desc, SegView sg, TraceView tr,
-                                                     StatsView sv)
+                                                     StatsView sv, const uint32_t* __restrict__ bperm)
 {
     extern __shared__ uint32_t lds_hist[];
     constexpr int WGT = exp_wg<R, OUT, SITES>();   // threads per workgroup
@@ -2323,6 +2365,17 @@ __global__ __launch_bounds__((exp_wg<R, OUT, SITES>()), (exp_waves<R, OUT, SITES
             bs = blockIdx.x;
             cs = blockIdx.y;
             (void)b;
+            if (exp_tpw<R, OUT, SITES>() == 1 && bperm) {
+                // cost order (round 6): the tiles in chunks of TCH blocks of the plan's order
+                // (daylight blocks first), each chunk's tiles chain block by chain block, time
+                // block fastest -- so concurrent workgroups still write different trace rows, as
+                // in launch order, but the day tiles are all dealt before the night ones
+                constexpr uint32_t TCH = 16;
+                const uint32_t per = TCH * CB, ch = L / per, rr = L - ch * per;
+                const uint32_t cc = min(TCH, T - ch * TCH), y = rr / cc;
+                bs = bperm[ch * TCH + (rr - y * cc)];
+                cs = y;
+            }
         } else if constexpr (ORD == 2) {
             // order 2: the tiles listed class by class (time blocks b = x mod 8), chain block major
             // inside a class (consecutive workgroups of an XCD: different time blocks, as in launch
@@ -2721,6 +2774,7 @@ struct PlanView {
     uint32_t* n_events;
     BlockDesc* desc;
     double* sun;   // [n_steps][SUN_W]: the sun's place per step (per-chain sites)
+    uint32_t* bperm;   // [nblk]: the 128-s blocks, daylight blocks first (block_order_kernel)
 };
 
 size_t plan_layout(uint32_t n_steps, void* base, PlanView* v)
@@ -2739,6 +2793,8 @@ size_t plan_layout(uint32_t n_steps, void* base, PlanView* v)
     o += align_up((size_t)(nblk_of(n_steps) + 1) * sizeof(BlockDesc));
     if (v) v->sun = (double*)(b + o);
     o += align_up((size_t)n_steps * SUN_W * 8);
+    if (v) v->bperm = (uint32_t*)(b + o);
+    o += align_up((size_t)nblk_of(n_steps) * 4);
     return o;
 }
 
@@ -2845,6 +2901,10 @@ struct tmh_engine {
     uint32_t walk_lanes = 0;  // lanes per chain in the walk (tmh_set_walk_lanes; 0: by batch size)
     bool walk_order = true;   // walk rows windiest chain first (tmh_set_walk_order)
     int last_expand = -1;     // TMH_OUT_* of the last expansion launched (tmh_engine_last_expand)
+    // expansion tiles daylight blocks first (env TMH_EXP_COST_ORDER=1, A/B; measured slower in the C2
+    // pipeline, round 6: 1.55 against 1.42-1.45 ms per step, same box -- launch order mixes the
+    // store-bound night tiles with the VALU-bound day tiles over the launch)
+    bool cost_order = false;
     // kernel timing (tmh_profile_*): event pairs per kernel, read and recycled
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[TMH_K_COUNT];
@@ -3064,6 +3124,7 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
     if (device < 0 || device >= ndev) return fail(TMH_E_INVAL, "device %d out of range (%d devices)", device, ndev);
     tmh_engine* e = new (std::nothrow) tmh_engine;
     if (!e) return fail(TMH_E_NOMEM, "out of host memory");
+    if (const char* co = std::getenv("TMH_EXP_COST_ORDER")) e->cost_order = std::atoi(co) != 0;
     KParams& k = e->kp;
     memset(&k, 0, sizeof k);
     k.cc_mode = p->cc_mode;
@@ -3395,6 +3456,7 @@ int tmh_plan(struct tmh_engine* eng, int64_t step0, uint32_t n_steps, void* plan
     hipLaunchKernelGGL(geom_kernel, dim3((n_steps + 255) / 256), dim3(256), 0, s, eng->gp, step0, n_steps, pv.tab64,
                        pv.tab32, pv.sun);
     hipLaunchKernelGGL(group_kind_kernel, dim3((n_steps / 4 + 255) / 256 + 1), dim3(256), 0, s, step0, n_steps, pv.tab32);
+    hipLaunchKernelGGL(block_order_kernel, dim3(1), dim3(1024), 0, s, pv.tab32, step0, n_steps, pv.bperm);
     hipLaunchKernelGGL(events_kernel, dim3(1), dim3(1024), 0, s, pv.tab32, step0, n_steps, eng->gp.clock.utc0,
                        pv.events, ev_cap(n_steps), pv.n_events);
     const uint32_t nb = nblk_of(n_steps);
@@ -3537,6 +3599,8 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     const size_t hist_bins = stats && stats->hist ? stats->n_bins : 0;
     // x = time blocks, y = chain blocks; LDS: the histogram (16-bit bin pairs or bins)
     auto exp_grid = [&](uint32_t wg, uint32_t tpw) { return dim3((sg.nblk + tpw - 1) / tpw, (n_chains + wg - 1) / wg); };
+    // the tiles in cost order (block_order_kernel's plan permutation; TMH_EXP_COST_ORDER=1, A/B only)
+    const uint32_t* bperm = eng->cost_order ? pv.bperm : nullptr;
     auto exp_lds = [&](bool pack) { return pack ? (hist_bins + 1) / 2 * 4 : hist_bins * 4; };
     if (out == OUT_TRACE3 && tv.ld * (f64 ? 8u : 4u) * BLOCK_STEPS >= (1ull << 31))   // one block's rows: one buffer range
         return fail(TMH_E_INVAL, "trace ld %llu too large (a 128-step block of rows must stay under 2 GiB)",
@@ -3546,7 +3610,7 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
                        exp_grid(exp_wg<R, O, S>(), exp_tpw<R, O, S>()), dim3(exp_wg<R, O, S>()),                 \
                        exp_lds(exp_hist_pack<R, O, S>()), s,                                                      \
                        eng->kp, eng->dp, v, chain0, n_chains, step0, n_steps,   \
-                       utc0, pv.tab64, pv.tab32, pv.sun, pv.events, pv.n_events, pv.desc, sg, tv, sv)
+                       utc0, pv.tab64, pv.tab32, pv.sun, pv.events, pv.n_events, pv.desc, sg, tv, sv, bperm)
 #ifndef TMH_SITES_STATS
 #define TMH_SITES_STATS 1   // per-chain sites: the statistics-only instantiation (0: OUT_ANY for every output, A/B)
 #endif

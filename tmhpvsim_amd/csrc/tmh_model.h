@@ -25,9 +25,11 @@ namespace tmh {
 constexpr double SQRT6 = 2.449489742783178;
 constexpr float EPS0F = (float)(SQRT6 * 0.001), EPS1F = (float)(SQRT6 * (0.0015 * 8));
 struct PVF {
-    float tk, temp_air, fd, nmbvmp, bvmpo1, nkq, nkq273, impo_c0;   // the first PVF_VGPR: pinned in VGPRs
-    float impo_c1, aimp, vmpo, c2ns, c3ns;
-    float paco, pso, ab1, ab0, b1, b0, c1, c0;
+    // the addends of pv_power_f's affine maps first: the first PVF_VGPR fields can be pinned in
+    // VGPRs (a VOP3 FMA reads one SGPR, so a map with two SGPR constants costs a v_mov per use)
+    float temp_air, nkq273, impo_c0, bvmpo1, vmpo, ab0, b0, c0;
+    float tk, fd, nmbvmp, nkq, impo_c1, aimp, c2ns, c3ns;
+    float paco, pso, ab1, b1, c1;
     float pacoc;        // max(Paco, 0): the upper bound of the final clamp
     float eps0, eps1;   // sqrt(6) 0.001, sqrt(6) 0.0015 * 8: the noise scale is eps0 + eps1 cc
 };
