@@ -1293,20 +1293,36 @@ __device__ __forceinline__ double mov_dpp_f64(double v)
     return __hiloint2double(hi, lo);
 }
 
-// min over the G lanes of each group: quad_perm [1,0,3,2], [2,3,0,1], then
-// row_half_mirror (G >= 8: the other quad of the half row), row_mirror (G = 16).
-// The scan's distances are never NaN (+inf or |tot - 3600| of a finite total), so a
-// compare and a select are the minimum; fmin would first canonicalise both operands
-// (two more fp64 ops per step on the walk's latency chain).
 template <int G>
-__device__ __forceinline__ double grp_min_f64(double v)
+__device__ __forceinline__ int grp_min_i32(int v);
+
+template <int G>
+__device__ __forceinline__ uint32_t grp_min_u32(uint32_t v)
 {
-    auto mn = [](double a, double b) { return b < a ? b : a; };
-    v = mn(v, mov_dpp_f64<0xB1>(v));
-    v = mn(v, mov_dpp_f64<0x4E>(v));
-    if constexpr (G >= 8) v = mn(v, mov_dpp_f64<0x141>(v));
-    if constexpr (G >= 16) v = mn(v, mov_dpp_f64<0x140>(v));
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true));
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true));
+    if constexpr (G >= 8) v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true));
+    if constexpr (G >= 16) v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true));
     return v;
+}
+
+// np.argmin's first-index rule over the group's lanes (round 6): each lane holds its best
+// distance d >= 0 (or +inf) and that entry's index k.  The high words of non-negative
+// doubles order like the doubles, so the group minimum of the high words (32-bit DPP minima,
+// one instruction a step) leaves the candidates that share it; the minimum of their low
+// words leaves the lanes whose d equals the true minimum bit for bit, and the lowest k among
+// those is the argmin.  Returns the index, or -1 when no lane has a finite d (no possible
+// entry): the same result as an fp64 group minimum followed by the minimum index at it, with
+// 32-bit reductions only.
+template <int G>
+__device__ __forceinline__ int grp_argmin_f64(double bd, int bk, uint32_t mh)
+{
+    const uint64_t bits = (uint64_t)__double_as_longlong(bd);
+    const uint32_t hi = (uint32_t)(bits >> 32), lo = (uint32_t)bits;
+    if (mh >= 0x7FF00000u) return -1;   // group-uniform: every lane +inf
+    const bool cand = hi == mh;
+    const uint32_t ml = grp_min_u32<G>(cand ? lo : 0xFFFFFFFFu);
+    return grp_min_i32<G>(cand && lo == ml ? bk : INT_MAX);
 }
 
 template <int G>
@@ -1389,6 +1405,9 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
                                                           PrevView prev)
 {
     static_assert(G == 4 || G == 8 || G == 16, "lanes per chain");
+#ifdef TMH_WALK_SETPRIO
+    __builtin_amdgcn_s_setprio(TMH_WALK_SETPRIO);   // A/B builds: the walk's waves issue first on their SIMD
+#endif
     constexpr int NCH = WALK_REG / G;                              // register chunks
     constexpr int NFIX = (WALK_FIX + G - 1) / G < NCH ? (WALK_FIX + G - 1) / G : NCH;
     static_assert(NCH * G == WALK_REG, "WALK_REG: a multiple of 16");
@@ -1672,15 +1691,16 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
                 const int k = k0 + p;
                 if (k < L) scan(k, gsc[k], gsl[k]);
             }
-            return grp_min_f64<G>(bd);
+            // the group's minimum high word of the distances (grp_argmin_f64); >= +inf's: no entry possible
+            return grp_min_u32<G>((uint32_t)((uint64_t)__double_as_longlong(bd) >> 32));
         };
         auto draw = [&](int t) {   // try t's cloud length, keyed by (chain, call number, try)
             return pow_d(dp.alpha + dp.delta * keyed_u(dp.seed, chain0 + gid(dp.ids, c), ncall, TAG_CLOUD,
                                                        (uint32_t)(t >> 1), t & 1),
                          dp.expo);
         };
-        double dmin = attempt(x0 >= 0.0 ? x0 : draw(0));
-        if (!(dmin < INFINITY)) {   // group-uniform
+        uint32_t mh = attempt(x0 >= 0.0 ? x0 : draw(0));
+        if (mh >= 0x7FF00000u) {   // group-uniform: no possible entry
             for (;;) {
                 ++tries;
                 if (tries == 20) {   // reset_sigma (cloud_cover_binary.py:76-78); 300 (k+1) is exact
@@ -1693,11 +1713,11 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
                     L = nl;
                 }
                 if (tries == 40) break;
-                dmin = attempt(draw(tries));
-                if (dmin < INFINITY) break;
+                mh = attempt(draw(tries));
+                if (mh < 0x7FF00000u) break;
             }
         }
-        if (dmin < INFINITY) last = grp_min_i32<G>(bd == dmin ? bk : INT_MAX);
+        last = grp_argmin_f64<G>(bd, bk, mh);
         ++ncall;
         WPROF(2);
         if (last < 0) {   // assert not recurse (:91)
@@ -2192,6 +2212,15 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
     // four straight-line seconds with no flag tests; a night second is its meter alone (no
     // row loads).  Other groups (sunrise, sunset, DISC's zenith limit) take the per-second path.
     constexpr bool FASTG = sizeof(R) == 4 && !SITES && !ROWL && out_base(OUT) != OUT_ANY;
+    // TMH_ISA_MARKS (analysis builds only, scripts/isa_loop.py --groups): comment markers around
+    // the four-second group bodies, so the listing's instructions per group can be counted
+#ifdef TMH_ISA_MARKS
+#define TMH_MARK(s) asm volatile("; TMH_MARK " s)
+#else
+#define TMH_MARK(s) \
+    do {        \
+    } while (0)
+#endif
     auto night4 = [&](uint32_t j, const U4& pm, auto ff) __attribute__((always_inline)) {
         const uint32_t w[4] = {pm.x, pm.y, pm.z, pm.w};
 #pragma unroll
@@ -2227,21 +2256,29 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
         if (((W0 + j0) & 3) == 0) {
             for (; j + 4 <= j1; j += 4) {
                 const uint64_t g = (uint64_t)(W0 + j) >> 2;
+                TMH_MARK("meter begin");
                 const U4 pm = keyed_block(kp.seed, chain, g, TAG_METER4, 0);
+                TMH_MARK("meter end");
                 if constexpr (FASTG) {
                     const uint32_t fl0 = __float_as_uint((float)rowp[G_FLAGS + G32]);   // the group's first row
                     if (!kp.with_pv || (fl0 & FL_G_NIGHT)) {
                         apply_events(j, fl0);
                         if (((j - j0) & 31) == 0) cov_w = cov_lds[(j - j0) >> 5][threadIdx.x];
                         rowp += 4 * RW;
+                        TMH_MARK("night4 begin");
                         night4(j, pm, ff);
+                        TMH_MARK("night4 end");
                         continue;
                     }
                     if (fl0 & FL_G_DAY) {
+                        TMH_MARK("noise begin");
                         const U4 pn = keyed_block(kp.seed, chain, g, TAG_NOISE4, 0);
+                        TMH_MARK("noise end");
                         apply_events(j, fl0);
                         if (((j - j0) & 31) == 0) cov_w = cov_lds[(j - j0) >> 5][threadIdx.x];
+                        TMH_MARK("day4 begin");
                         day4(j, pn, pm, ff);
+                        TMH_MARK("day4 end");
                         continue;
                     }
                 }
