@@ -306,9 +306,11 @@ __device__ __forceinline__ double draw_cc(const KParams& kp, uint32_t c, Chain& 
 
 __device__ __forceinline__ int32_t ceil_thr(double x)
 {   // sec < x  <=>  sec < ceil(x) for integer sec (cloud_cover_binary.py:111-113)
-    if (!(x <= 2147483000.0)) return INT_MAX;
-    if (x < -2147483000.0) return INT_MIN + 1;
-    return (int32_t)ceil(x);
+    // branch-free (round 6: the walk's latency chain): above 2147483000 or NaN -> INT_MAX,
+    // below -2147483000 -> INT_MIN + 1, else ceil(x)
+    double y = x <= 2147483000.0 ? x : 2147483647.0;
+    y = y < -2147483000.0 ? -2147483647.0 : y;
+    return (int32_t)ceil(y);
 }
 
 __device__ __forceinline__ double* sig_c(const StateView& st, uint32_t c) { return st.sc + (size_t)c * CAP; }
