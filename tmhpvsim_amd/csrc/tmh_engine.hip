@@ -394,7 +394,7 @@ __global__ __launch_bounds__(256) void geom_kernel(GParams gp, int64_t step0, ui
 // window on the four-step grid, ORed into its first fp32 row's flags: FL_G_NIGHT (four night
 // seconds), FL_G_DAY (four daylight seconds with DISC valid); either only when seconds 1-3
 // carry no boundary event.  Other windows and partial groups get neither bit.
-__global__ __launch_bounds__(256) void group_kind_kernel(int64_t step0, uint32_t n, float* tab32)
+__global__ __launch_bounds__(256) void group_kind_kernel(int64_t step0, uint32_t n, float* tab32, double* tab64)
 {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x, j = 4 * g;
     if ((step0 & 3) != 0 || j + 3 >= n) return;
@@ -409,7 +409,10 @@ __global__ __launch_bounds__(256) void group_kind_kernel(int64_t step0, uint32_t
     uint32_t k = 0;
     if (!ev && (all & FL_NIGHT)) k = FL_G_NIGHT;
     else if (!ev && !anyn && (all & FL_DISCOK)) k = FL_G_DAY;
-    if (k) tab32[(size_t)j * ROW32 + G_FLAGS + G32] = __uint_as_float(f[0] | k);
+    if (k) {   // both rows: the fp32 and the fp64 single-site expansions read it
+        tab32[(size_t)j * ROW32 + G_FLAGS + G32] = __uint_as_float(f[0] | k);
+        tab64[(size_t)j * ROW + G_FLAGS] = (double)(f[0] | k);
+    }
 }
 
 // The window's 128-s blocks in the order the single-site expansion takes its tiles (round 6):
@@ -2216,7 +2219,7 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
     // a group's first second).  Such a group applies its first second's events once and runs
     // four straight-line seconds with no flag tests; a night second is its meter alone (no
     // row loads).  Other groups (sunrise, sunset, DISC's zenith limit) take the per-second path.
-    constexpr bool FASTG = sizeof(R) == 4 && !SITES && !ROWL && out_base(OUT) != OUT_ANY;
+    constexpr bool FASTG = !SITES && !ROWL && out_base(OUT) != OUT_ANY;
     // TMH_ISA_MARKS (analysis builds only, scripts/isa_loop.py --groups): comment markers around
     // the four-second group bodies, so the listing's instructions per group can be counted
 #ifdef TMH_ISA_MARKS
@@ -2238,16 +2241,24 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
         const uint32_t wn[4] = {pn.x, pn.y, pn.z, pn.w}, wm[4] = {pm.x, pm.y, pm.z, pm.w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            R row[ROW32];
+            R row[row_w<R>()];
 #pragma unroll
-            for (int i = 0; i < ROW32; ++i) row[i] = rowp[i];
+            for (int i = 0; i < row_w<R>(); ++i) row[i] = rowp[i];
             rowp += RW;
             const uint32_t jb = j + q - j0;
             const bool covered = (cov_w >> (jb & 31)) & 1u;
             R csi, pv, meter, res;
             bool held = false;
-            second_body<R, true>(kp, pkv, row, FL_DISCOK, fs, covered, noise_lds<R>(wn[q], nd_lds), meter_w<R>(wm[q]),
-                                 csi, pv, meter, res, held);
+            if constexpr (sizeof(R) == 8) {   // the PV constants from LDS (see second), the table quantile
+                uint32_t pa = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) PV64*)pv_lds;
+                asm volatile("" : "+v"(pa));
+                const __attribute__((address_space(3))) PV64* p = (const __attribute__((address_space(3))) PV64*)(uintptr_t)pa;
+                second_body<R>(kp, pkv, row, FL_DISCOK, fs, covered, ndtri64(wn[q], (LdsD*)pv_lds_tab),
+                               meter_w<R>(wm[q]), csi, pv, meter, res, held, p, (LdsD*)pv_lds_tab);
+            } else {
+                second_body<R, true>(kp, pkv, row, FL_DISCOK, fs, covered, noise_lds<R>(wn[q], nd_lds),
+                                     meter_w<R>(wm[q]), csi, pv, meter, res, held);
+            }
             finish(j + q, jb, covered, csi, pv, meter, res, held, ff);
         }
     };
@@ -2265,7 +2276,8 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
                 const U4 pm = keyed_block(kp.seed, chain, g, TAG_METER4, 0);
                 TMH_MARK("meter end");
                 if constexpr (FASTG) {
-                    const uint32_t fl0 = __float_as_uint((float)rowp[G_FLAGS + G32]);   // the group's first row
+                    const uint32_t fl0 = sizeof(R) == 8 ? (uint32_t)(double)rowp[G_FLAGS]   // the group's first row
+                                                        : __float_as_uint((float)rowp[G_FLAGS + G32]);
                     if (!kp.with_pv || (fl0 & FL_G_NIGHT)) {
                         apply_events(j, fl0);
                         if (((j - j0) & 31) == 0) cov_w = cov_lds[(j - j0) >> 5][threadIdx.x];
@@ -3497,7 +3509,8 @@ int tmh_plan(struct tmh_engine* eng, int64_t step0, uint32_t n_steps, void* plan
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(geom_kernel, dim3((n_steps + 255) / 256), dim3(256), 0, s, eng->gp, step0, n_steps, pv.tab64,
                        pv.tab32, pv.sun);
-    hipLaunchKernelGGL(group_kind_kernel, dim3((n_steps / 4 + 255) / 256 + 1), dim3(256), 0, s, step0, n_steps, pv.tab32);
+    hipLaunchKernelGGL(group_kind_kernel, dim3((n_steps / 4 + 255) / 256 + 1), dim3(256), 0, s, step0, n_steps, pv.tab32,
+                       pv.tab64);
     hipLaunchKernelGGL(block_order_kernel, dim3(1), dim3(1024), 0, s, pv.tab32, step0, n_steps, pv.bperm);
     hipLaunchKernelGGL(events_kernel, dim3(1), dim3(1024), 0, s, pv.tab32, step0, n_steps, eng->gp.clock.utc0,
                        pv.events, ev_cap(n_steps), pv.n_events);
