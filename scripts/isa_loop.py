@@ -77,6 +77,9 @@ def groups(kre):
               f"SALU {sal:4d} ({sal / per[name]:5.1f}/s)  mem {sum(1 for x in ins if x[:2] not in ('v_', 's_'))}")
         hist = collections.Counter(re.sub(r"_e(32|64)$", "", x) for x in v)
         print("         " + "  ".join(f"{k}:{n}" for k, n in hist.most_common(24)))
+        shist = collections.Counter(x for x in ins if x.startswith("s_") and x != "s_nop")
+        if shist:
+            print("   SALU  " + "  ".join(f"{k}:{n}" for k, n in shist.most_common(12)))
 
 
 def main():
