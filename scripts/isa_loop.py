@@ -1,7 +1,7 @@
 """Static instruction counts of a kernel's loop blocks (device assembly from hipcc -S).
 
 usage: python scripts/isa_loop.py [KERNEL_REGEX] [--hist] [-D MACRO ...]
-       python scripts/isa_loop.py --groups [KERNEL_REGEX]
+       python scripts/isa_loop.py --groups [KERNEL_REGEX] [-D MACRO ...]
 Default kernel: the fp32 trace-mode single-site expansion (expand_kernel<float, OUT_TRACE3, false>).
 Prints VGPR count and, per backward-branch loop, VALU / SALU / memory instruction counts.
 
@@ -53,8 +53,8 @@ def weight(op):
     return 4.2
 
 
-def groups(kre):
-    lines = asm(["TMH_ISA_MARKS"])
+def groups(kre, defines=()):
+    lines = asm(["TMH_ISA_MARKS", *defines])
     start = next(i for i, l in enumerate(lines) if re.match(r"^_Z\S*" + kre + r"\S*:", l))
     end = next(i for i in range(start, len(lines)) if lines[i].startswith(".Lfunc_end"))
     body = lines[start:end]
@@ -84,12 +84,12 @@ def groups(kre):
 
 def main():
     args = sys.argv[1:]
+    defines = [args[i + 1] for i, a in enumerate(args) if a == "-D"]
     if "--groups" in args:
-        pos = [a for a in args if not a.startswith("-")]
-        groups(pos[0] if pos else r"expand_kernelIfLi1ELb0E")
+        pos = [a for i, a in enumerate(args) if not a.startswith("-") and (i == 0 or args[i - 1] != "-D")]
+        groups(pos[0] if pos else r"expand_kernelIfLi1ELb0E", defines)
         return
     hist = "--hist" in args
-    defines = [args[i + 1] for i, a in enumerate(args) if a == "-D"]
     pos = [a for i, a in enumerate(args) if not a.startswith("-") and (i == 0 or args[i - 1] != "-D")]
     kre = pos[0] if pos else r"expand_kernelIfLi1ELb0E"
     lines = asm(defines)

@@ -1889,6 +1889,12 @@ __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t rs, uint32_t of
 #ifndef TMH_EXP_WG_STATS
 #define TMH_EXP_WG_STATS 512
 #endif
+#ifndef TMH_HELD_OR
+#define TMH_HELD_OR 0   // fp32 expansion: the guard-band bit as an unconditional LDS or (A/B builds; DESIGN round 6)
+#endif
+#ifndef TMH_DISC_LDS
+#define TMH_DISC_LDS 0   // fp32 single-site expansion: DISC's coefficient sets from an LDS table (disc_row; A/B builds)
+#endif
 #ifndef TMH_ROW_LDS
 #define TMH_ROW_LDS 0   // fp32 single-site expansion: the tile's geometry rows staged in LDS (A/B builds)
 #endif
@@ -1970,6 +1976,9 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
     // TMH_ROW_LDS: the tile's fp32 geometry rows copied to LDS once (coalesced vector loads),
     // read back per second with broadcast ds_reads instead of per-second scalar loads
     constexpr bool ROWL = TMH_ROW_LDS && sizeof(R) == 4 && !SITES;
+    // fp32: DISC's coefficient sets from the LDS table after the quantile's (the single-site
+    // second bodies; TMH_DISC_LDS=0 builds the constant-coefficient branches instead, for A/B)
+    const float4* disc_lds = sizeof(R) == 4 && TMH_DISC_LDS ? nd_lds + ND32_N : nullptr;
     const uint32_t c = cblk * blockDim.x + threadIdx.x;
     const bool live = c < n;
     const uint32_t j0 = b * BLOCK_STEPS, j1 = min(j0 + (uint32_t)BLOCK_STEPS, nsteps);
@@ -2139,10 +2148,13 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
         const bool ok = FF || (int32_t)j < fault_eff;
         held = held && ok && live;   // lanes past the last chain run on uninitialised samplers: never held
         if constexpr (sizeof(R) == 4) {
-            if (held) {   // jb is wave-uniform: the word and the bit are scalars
-                uint32_t* hw = reinterpret_cast<uint32_t*>(&held_lds[threadIdx.x]) + (jb >> 5);
+            // jb is wave-uniform: the word and the bit are scalars.  TMH_HELD_OR: every lane ors
+            // its bit or 0 into its word (one ds_or, no exec-mask branch around a rare store)
+            uint32_t* hw = reinterpret_cast<uint32_t*>(&held_lds[threadIdx.x]) + (jb >> 5);
+            if constexpr (TMH_HELD_OR)
+                __hip_atomic_fetch_or(hw, held ? 1u << (jb & 31) : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            else if (held)
                 *hw |= 1u << (jb & 31);
-            }
         }
         if constexpr (!FF) {
             csi = ok ? csi : R(NAN);
@@ -2207,7 +2219,7 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
                                meter, res, held, p, (LdsD*)pv_lds_tab);
             } else {
                 second_body<R, !SITES && !ROWL>(kp, pkv, row, flp, fs, covered, noise_lds<R>(un, nd_lds), meter_w<R>(um),
-                                                csi, pv, meter, res, held);
+                                                csi, pv, meter, res, held, nullptr, nullptr, disc_lds);
             }
         }
         finish(j, jb, covered, csi, pv, meter, res, held, ff);
@@ -2257,7 +2269,7 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
                                meter_w<R>(wm[q]), csi, pv, meter, res, held, p, (LdsD*)pv_lds_tab);
             } else {
                 second_body<R, true>(kp, pkv, row, FL_DISCOK, fs, covered, noise_lds<R>(wn[q], nd_lds),
-                                     meter_w<R>(wm[q]), csi, pv, meter, res, held);
+                                     meter_w<R>(wm[q]), csi, pv, meter, res, held, nullptr, nullptr, disc_lds);
             }
             finish(j + q, jb, covered, csi, pv, meter, res, held, ff);
         }
@@ -2379,13 +2391,17 @@ __global__ __launch_bounds__((exp_wg<R, OUT, SITES>()), (exp_waves<R, OUT, SITES
     __shared__ __attribute__((aligned(16))) double pv_tab[sizeof(R) == 8 || SITES ? PV_TAB : 2];
     __shared__ __attribute__((aligned(16))) float row_lds[TMH_ROW_LDS && sizeof(R) == 4 && !SITES ? BLOCK_STEPS * ROW32 : 1];
     // fp32: the noise quantile's table (ndtri_t), 8 KB, copied once per workgroup
-    __shared__ float4 nd_tab[sizeof(R) == 4 ? ND32_N : 1];
+    // (with TMH_DISC_LDS, DISC's coefficient sets after it: disc_row)
+    __shared__ float4 nd_tab[sizeof(R) == 4 ? ND32_N + (TMH_DISC_LDS ? DISC_TAB : 0) : 1];
     if constexpr (sizeof(R) == 8 || SITES) {
         if (threadIdx.x < PV64_N) reinterpret_cast<double*>(pv_lds)[threadIdx.x] = reinterpret_cast<const double*>(&kp.pv64)[threadIdx.x];
         for (uint32_t i = threadIdx.x; i < PV_TAB; i += blockDim.x) pv_tab[i] = g_pv_tab[i];
     }
     if constexpr (sizeof(R) == 4)
+    {
         for (uint32_t i = threadIdx.x; i < ND32_N; i += blockDim.x) nd_tab[i] = g_nd32_tab[i];
+        if (TMH_DISC_LDS && threadIdx.x < DISC_TAB) nd_tab[ND32_N + threadIdx.x] = disc_row(threadIdx.x);
+    }
     __syncthreads();
     constexpr bool PACK = exp_hist_pack<R, OUT, SITES>();
     const uint32_t nw = PACK ? (sv.n_bins + 1) / 2 : sv.n_bins;   // 16-bit bin pairs, or bins
@@ -3511,7 +3527,8 @@ int tmh_plan(struct tmh_engine* eng, int64_t step0, uint32_t n_steps, void* plan
                        pv.tab32, pv.sun);
     hipLaunchKernelGGL(group_kind_kernel, dim3((n_steps / 4 + 255) / 256 + 1), dim3(256), 0, s, step0, n_steps, pv.tab32,
                        pv.tab64);
-    hipLaunchKernelGGL(block_order_kernel, dim3(1), dim3(1024), 0, s, pv.tab32, step0, n_steps, pv.bperm);
+    if (eng->cost_order)   // the expansion reads the tile order only then
+        hipLaunchKernelGGL(block_order_kernel, dim3(1), dim3(1024), 0, s, pv.tab32, step0, n_steps, pv.bperm);
     hipLaunchKernelGGL(events_kernel, dim3(1), dim3(1024), 0, s, pv.tab32, step0, n_steps, eng->gp.clock.utc0,
                        pv.events, ev_cap(n_steps), pv.n_events);
     const uint32_t nb = nblk_of(n_steps);

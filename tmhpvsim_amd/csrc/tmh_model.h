@@ -1315,6 +1315,25 @@ __device__ __forceinline__ float disc_poly(const Cubic& p, float t)
     return v;
 }
 
+// The same coefficients as a table (round 6): the single-site expansion keeps it in LDS after
+// the noise quantile's and reads the lane's set, so DISC's kt split costs an address select
+// instead of divergent branches.  Rows {d3, d2, d1, d0} of a, b, c for kt <= 0.6, then for
+// kt > 0.6; the low set's missing leading terms are 0, and Horner through a zero leading term
+// gives disc_poly's value bit for bit (0 t + 0 = +-0, then +-0 t + d = d exactly, d != 0).
+constexpr int DISC_TAB = 6;
+__device__ __forceinline__ float4 disc_row(int i)
+{
+    const Cubic& p = i % 3 == 0 ? (i < 3 ? DISC_A_LO : DISC_A_HI)
+                                : (i % 3 == 1 ? (i < 3 ? DISC_B_LO : DISC_B_HI) : (i < 3 ? DISC_C_LO : DISC_C_HI));
+    const int deg = i == 1 ? 1 : (i == 2 ? 2 : 3);
+    const float d3 = deg >= 3 ? disc_shift(p, 3) : 0.0f, d2 = deg >= 2 ? disc_shift(p, 2) : 0.0f;
+    return make_float4(d3, d2, disc_shift(p, 1), disc_shift(p, 0));
+}
+__device__ __forceinline__ float disc_horner(const float4& d, float t)
+{
+    return fmaf(fmaf(fmaf(d.x, t, d.y), t, d.z), t, d.w);
+}
+
 // Guard band of the fp32 chain's two discontinuities (DISC's kt = 0.6 split and
 // the inverter's p_dc < Pso cut-in): a second whose fp32 kt or p_dc lies this
 // close to its threshold may have fallen on the other side than the fp64
@@ -1330,7 +1349,8 @@ constexpr float KT_GUARD = 4e-6f, PDC_GUARD = 1e-4f;
 // UROW: the row is wave-uniform (the single-site kernels' scalar loads), so the clamp's bound
 // is an SGPR operand of a plain v_min_f32
 template <bool UROW = false>
-__device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float csi, bool discok, bool& risky)
+__device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float csi, bool discok, bool& risky,
+                                            const float4* dtab = nullptr)
 {
     // min(csi, csimax) as a median with -inf: no canonicalising max of the row's value first.
     // On a NaN csi it returns csimax, as fminf did (tmh_probe fn 10, test_probe_math); a NaN
@@ -1345,11 +1365,20 @@ __device__ __forceinline__ float pv_power_f(const PVF& k, const float* g, float 
     // DISC Kn: coefficient sets split at kt = 0.6 (compile-time constants, no
     // SGPRs).  Both sets are evaluated and the results selected: cheaper than
     // selecting twelve coefficient pairs per lane.
+    // UROW with dtab (the single-site expansion): the lane's set from the LDS table (disc_row)
     const bool lo = kt <= 0.6f;
     const float t = kt - 0.6f;
-    const float a = lo ? disc_poly<3>(DISC_A_LO, t) : disc_poly<3>(DISC_A_HI, t);
-    const float b = lo ? disc_poly<1>(DISC_B_LO, t) : disc_poly<3>(DISC_B_HI, t);
-    const float cc = lo ? disc_poly<2>(DISC_C_LO, t) : disc_poly<3>(DISC_C_HI, t);
+    float a, b, cc;
+    if (UROW && dtab) {
+        const float4* d = dtab + (lo ? 0 : 3);
+        a = disc_horner(d[0], t);
+        b = disc_horner(d[1], t);
+        cc = disc_horner(d[2], t);
+    } else {
+        a = lo ? disc_poly<3>(DISC_A_LO, t) : disc_poly<3>(DISC_A_HI, t);
+        b = lo ? disc_poly<1>(DISC_B_LO, t) : disc_poly<3>(DISC_B_HI, t);
+        cc = lo ? disc_poly<2>(DISC_C_LO, t) : disc_poly<3>(DISC_C_HI, t);
+    }
     // exp(cc am) = exp2(cc * (am log2 e)): the fp32 row holds am log2 e (one rounding)
     const float dkn = fmaf(b, __builtin_amdgcn_exp2f(cc * g[G_AM]), a);
     float dni = (g[G_KNC] - dkn) * g[G_I0];
@@ -1483,7 +1512,8 @@ __device__ __forceinline__ R meter_w(uint32_t w)
 template <typename R, bool UROW = false, typename P64 = decltype(nullptr), typename LT = decltype(nullptr)>
 __device__ __forceinline__ void second_body(const KParams& kp, const PVF& pk, const R* row, uint32_t fl,
                                             const FSamp<R>& fs, bool covered, R z, R meter_in, R& csi, R& pv, R& meter,
-                                            R& res, bool& risky, P64 p64 = nullptr, LT lt = nullptr)
+                                            R& res, bool& risky, P64 p64 = nullptr, LT lt = nullptr,
+                                            const float4* dtab = nullptr)
 {
     risky = false;
     const R cloudcover = rinterp_row(fs, S_CC, row, G_HOURF);   // == interp() bit for bit when R = double
@@ -1501,7 +1531,7 @@ __device__ __forceinline__ void second_body(const KParams& kp, const PVF& pk, co
         else
             pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power_d(p64, row, csi, lt) : R(0);
     }
-    else pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power_f<UROW>(pk, row + G32, csi, (fl & FL_DISCOK) != 0, risky) : 0.0f;
+    else pv = (kp.with_pv && !(fl & FL_NIGHT)) ? pv_power_f<UROW>(pk, row + G32, csi, (fl & FL_DISCOK) != 0, risky, dtab) : 0.0f;
     meter = meter_in;
     res = meter - pv;
 }
