@@ -219,6 +219,9 @@ def parse():
     ap.add_argument("--build-ahead", type=int, default=None,
                     help="gated schedule: when the walk of batch k ends, the construction of batch k + A is "
                          "released (default A = walks + 2 with two or more walks, else walks + 1; needs --pipeline >= A + 1)")
+    ap.add_argument("--build-streams", type=int, default=None,
+                    help="gated schedule: the constructions on this many streams in turn (consecutive batches' "
+                         "constructions may then overlap)")
     ap.add_argument("--build-priority", default="normal", choices=["high", "normal"],
                     help="gated schedule: HIP stream priority of the construction stream")
     ap.add_argument("--commit-stream", type=int, default=None,
@@ -260,9 +263,10 @@ def parse():
                               build_priority=a.build_priority,
                               commit_stream=None if a.commit_stream is None else bool(a.commit_stream),
                               walk_order=bool(a.walk_order), walk_cus=a.walk_cus, other_cus=a.other_cus,
-                              timeline=a.timeline, queues=a.queues, first_split=a.first_split)
-    for k in ("mode", "window", "pipeline", "walks", "build_ahead", "build_on", "walk_priority", "compact",
-              "commit_stream"):
+                              timeline=a.timeline, queues=a.queues, first_split=a.first_split,
+                              build_streams=a.build_streams)
+    for k in ("mode", "window", "pipeline", "walks", "build_ahead", "build_streams", "build_on", "walk_priority",
+              "compact", "commit_stream"):
         setattr(a, k, getattr(a.cfg, k))
     # C5's compacted windows walk and expand in turn (latency-bound walk): 16 lanes per
     # chain (1.76e10 against 1.73e10 with the batch-size default, r02 same box)
@@ -592,7 +596,7 @@ def main():
                    "construction_on": args.build_on, "walk_priority": args.walk_priority,
                    "schedule": args.schedule if pipe.gated() else None,
                    "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"), "walks_in_flight": pipe.W, "walk_order": bool(args.walk_order), "walk_cus": args.walk_cus or "all", "other_cus": args.other_cus if args.walk_cus else "all",
-                   "walk_chains_per_row": args.walk_cpr, "queues": args.queues, "walk_lanes": args.walk_lanes or "auto", "build_ahead": pipe.A,
+                   "walk_chains_per_row": args.walk_cpr, "queues": args.queues, "walk_lanes": args.walk_lanes or "auto", "build_ahead": pipe.A, "build_streams": args.build_streams,
                    "commit_stream": bool(args.commit_stream),
                    "first_batch_windows": len(pipe.split) if (pipe.split and pipe.gated()) else 1,
                    "compacted_windows": bool(args.compact and args.mode == "stats" and nwin > 1)},
@@ -626,7 +630,12 @@ def main():
             if k0 in tl.get(key, {}):
                 fill[name] = t0ev.elapsed_time(tl[key][k0])
         line["timeline"] = {"fill": fill, "expansion_gap_ms": gaps, "walk_end_after_prev_expansion_ms": late,
-                            "walk_ms": wdur, "walk_start_after_build_ms": bwait}
+                            "walk_ms": wdur, "walk_start_after_build_ms": bwait,
+                            # every batch's marks from the timed region's start (ms): built, walk start /
+                            # end, expansion start / end
+                            "marks_ms": {key: [round(t0ev.elapsed_time(ev[k]), 4) if k in ev else None
+                                               for k in range(k0, k0 + args.steps)]
+                                         for key, ev in tl.items()}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args, kw)
     pipe.close()   # drain and release the pipeline's dedicated streams

@@ -1162,7 +1162,7 @@ __global__ __launch_bounds__(256) void chain_kernel(KParams kp, StateView st, ui
             sv.acc[g] += acc.pv;
             sv.acc[an + g] += acc.m;
             sv.acc[2 * an + g] += acc.r;
-            sv.acc[3 * an + g] = fmax(sv.acc[3 * an + g], acc.mx);
+            sv.acc[3 * an + g] = fmax(sv.acc[3 * an + g], acc.max());
         }
     }
     if (sv.hist) {
@@ -2361,7 +2361,7 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
         atomicAdd(fx + c, (unsigned long long)llrint(acc.pv * sg.fx_scale));
         atomicAdd(fx + (size_t)n + c, (unsigned long long)llrint(acc.m * sg.fx_scale));
         atomicAdd(fx + 2 * (size_t)n + c, (unsigned long long)llrint(acc.r * sg.fx_scale));
-        __hip_atomic_fetch_max(sg.acc_mx + c, max_key(acc.mx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_max(sg.acc_mx + c, max_key(acc.max()), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 

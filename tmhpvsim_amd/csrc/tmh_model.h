@@ -1546,6 +1546,11 @@ __device__ __forceinline__ void trace_store(void* p, uint64_t i, R v)
 
 struct Acc {
     double pv, m, r, mx;
+    // fp32 kernels: the residual maximum kept in fp32 (one v_max_f32 per second instead of an
+    // fp64 max and its operand canonicalisation); widening is exact and monotonic, so
+    // max(mx, mxf) equals the fp64 maximum of the widened residuals bit for bit
+    float mxf = -INFINITY;
+    __device__ double max() const { return fmax(mx, (double)mxf); }
 };
 
 // output specialisations of the time-parallel expansion (chosen on the host)
@@ -1583,10 +1588,18 @@ __device__ __forceinline__ void emit(const TraceView& tr, const StatsView& sv, u
     }
     if (ok) {
         if (sv.acc) {
-            acc.pv += (double)pv;
+            // a night second's literal pv = 0 adds nothing (acc.pv starts at +0 and sums values >= 0,
+            // so it is never -0 and acc.pv + 0 == acc.pv): no fp64 add for it
+            if (!(__builtin_constant_p(pv) && pv == R(0))) acc.pv += (double)pv;
             acc.m += (double)meter;
             acc.r += (double)res;
-            if (!held) acc.mx = fmax(acc.mx, (double)res);
+            if constexpr (sizeof(R) == 4) {   // v_max_f32 directly (fmaxf canonicalises both operands
+                float m;                         // first; res is never NaN here: ok lanes only), a select
+                asm("v_max_f32 %0, %1, %2" : "=v"(m) : "v"(acc.mxf), "v"(res));   // for held (no branch)
+                acc.mxf = held ? acc.mxf : m;
+            } else if (!held) {
+                acc.mx = fmax(acc.mx, (double)res);
+            }
         }
         if (sv.hist && !held) {
             const int bin = (OUT & OUT_BRT) ? hist_bin_rt<R>(sv, res) : hist_bin<R, sizeof(R) == 8 || (OUT & OUT_B64) != 0>(sv, res);

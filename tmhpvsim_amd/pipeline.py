@@ -31,6 +31,8 @@ class PipelineConfig:
     pipeline: int = 5            # contexts (batches in flight)
     walks: int = 2               # gated schedule: segment walks in flight
     build_ahead: int = 4         # gated: construction of batch k + A released when walk k ends
+    build_streams: int = 1       # gated: constructions on this many streams in turn (2: consecutive
+                                 # batches' constructions may overlap; their kernels are latency-bound)
     stagger: bool = True         # one-window batches software-pipelined (else one tmh_step each, in turn)
     schedule: str = "gated"      # "gated" or round 1's "stagger"
     build_on: str = "walk"       # stagger schedule: construction on the walk or the expansion stream
@@ -215,12 +217,15 @@ class BatchPipeline:
             self.estream = mk(cfg.expand_priority)
             self.wsts = [mk(cfg.walk_priority) for _ in range(W)]
             self.bst = mk(cfg.build_priority)
+            self.bsts = [self.bst] + [mk(cfg.build_priority) for _ in range(max(1, cfg.build_streams) - 1)]
             if cfg.walk_cus:   # the walks on a share of every XCD's CUs (CU-masked streams)
                 ncu = torch.cuda.get_device_properties(device).multi_processor_count
                 self.wsts = [own(_lib.cu_stream(0, cfg.walk_cus, device)) for _ in range(W)]
                 if cfg.other_cus == "rest":
                     self.bst, self._cst = (own(_lib.cu_stream(cfg.walk_cus, ncu - cfg.walk_cus, device))
                                            for _ in range(2))
+                    self.bsts = [self.bst] + [own(_lib.cu_stream(cfg.walk_cus, ncu - cfg.walk_cus, device))
+                                              for _ in range(max(1, cfg.build_streams) - 1)]
                     self.estream = own(_lib.cu_stream(cfg.walk_cus, ncu - cfg.walk_cus, device))
             self.eptr = C.c_void_p(self.estream.cuda_stream)
             self.bst_p = C.c_void_p(self.bst.cuda_stream)
@@ -434,7 +439,8 @@ class BatchPipeline:
         L, sim, cfg = self.L, self.sim, self.cfg
         cx = self.ctx_of(j)
         cx.chain0 = self.chain0_of(j)
-        bst, bp = self.bst, self.bst_p
+        bst = self.bsts[j % len(self.bsts)]
+        bp = C.c_void_p(bst.cuda_stream)
         if gate is not None:
             bst.wait_event(gate)
         if cx.expanded is not None:                        # the context's previous batch is committed
