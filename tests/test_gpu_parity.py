@@ -10,6 +10,8 @@ Bars (DESIGN.md "Parity"):
     in fp64 by fixup_kernel);
   * reference fixtures (injected uniforms): CSI within 1e-12 relative.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -562,9 +564,20 @@ def test_walk_lanes_invariance(window, markov, start):
     mp = ModelParams(cc_mode=CC_MARKOV, seed=0x7AB1E) if markov else None
     tab = site_shape_tables(n) if markov else None
     outs = []
-    for lanes, cpr, order in ((16, 1, 1), (16, 1, 0), (8, 1, 1), (4, 1, 1), (4, 3, 1), (4, 3, 0), (8, 2, 1)):
-        s = _sim(n, start, tz="Europe/Berlin", mp=mp, prec="fp32", kernel_path="time_parallel", horizon=steps,
-                 tables=tab)
+    # tp: the 8-lane walk's throughput variant (32 register entries, 4 waves per SIMD: C3's
+    # batches), forced on this small batch through the engine's row threshold
+    for lanes, cpr, order, tp in ((16, 1, 1, 0), (16, 1, 0, 0), (8, 1, 1, 0), (4, 1, 1, 0), (4, 3, 1, 0), (4, 3, 0, 0),
+                                  (8, 2, 1, 0), (8, 1, 1, 1), (8, 1, 0, 1)):
+        old = os.environ.get("TMH_WALK_TP_ROWS")
+        os.environ["TMH_WALK_TP_ROWS"] = "1" if tp else "4294967295"
+        try:
+            s = _sim(n, start, tz="Europe/Berlin", mp=mp, prec="fp32", kernel_path="time_parallel", horizon=steps,
+                     tables=tab)
+        finally:
+            if old is None:
+                del os.environ["TMH_WALK_TP_ROWS"]
+            else:
+                os.environ["TMH_WALK_TP_ROWS"] = old
         _lib.check(L.tmh_set_walk_lanes(s._eng, lanes))
         _lib.check(L.tmh_set_walk_chains_per_row(s._eng, cpr))
         _lib.check(L.tmh_set_walk_order(s._eng, order))   # rows windiest chain first, or in chain order

@@ -1365,6 +1365,21 @@ __device__ __forceinline__ double bperm_f64(int src_lane, double v)
 // (r02, same box: C3 2.48 -> 2.69e11, C4 2.24 -> 2.36e11 chain-s/s).
 constexpr uint32_t WALK_AUTO_SMALL = 8192;
 constexpr int WALK_REG = 64;   // sigma entries held in VGPRs per chain (entries past them: the chain's global row)
+// TP: the 8-lane walk of a throughput-bound batch (rows >= the engine's walk_tp_rows, 65,536 by
+// default: C3's 1 M chains, 131,072 waves): 32 register entries and at least 4 waves per SIMD (128
+// VGPRs, 27 spilled) instead of 64 entries at 180 VGPRs (2 waves).  Round 6, same box: C3 3.06
+// against 2.96e11; a latency-bound batch (C4's 16,384 chains, 2 waves per SIMD) keeps the
+// unspilled walk (the TP walk: C4 3.01 against 3.09e11).
+template <int G, bool TP>
+constexpr int walk_reg()
+{
+    return TP ? 32 : WALK_REG;
+}
+template <int G, bool TP>
+constexpr int walk_waves()
+{
+    return TP ? 4 : 1;
+}
 constexpr int WALK_FIX = 16;   // entries scanned unconditionally (one chunk at G = 16); the rest only when some chain of the wave needs them
 static_assert(WALK_FIX >= 12, "reset_sigma writes up to 11 entries into the unconditional chunks");
 constexpr int WALK_CAND = 32;   // try-0 candidates per LDS refill of a chain (one exposed load per 32 calls)
@@ -1400,8 +1415,8 @@ __device__ unsigned long long g_walk_prof[WPROF_WAVES][WPROF_N + 2];
     } while (0)
 #endif
 
-template <bool QUEUE, int G>
-__global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
+template <bool QUEUE, int G, bool TP = false>
+__global__ __launch_bounds__(256, (walk_waves<G, TP>())) void segments_kernel(DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
                                                           int64_t W0, uint32_t nsteps, tmh_clock ck,
                                                           const int2* __restrict__ events,
                                                           const uint32_t* __restrict__ n_events, SegView sg,
@@ -1411,9 +1426,9 @@ __global__ __launch_bounds__(256, 1) void segments_kernel(DrawParams dp, StateVi
 #ifdef TMH_WALK_SETPRIO
     __builtin_amdgcn_s_setprio(TMH_WALK_SETPRIO);   // A/B builds: the walk's waves issue first on their SIMD
 #endif
-    constexpr int NCH = WALK_REG / G;                              // register chunks
+    constexpr int NCH = walk_reg<G, TP>() / G;                     // register chunks
     constexpr int NFIX = (WALK_FIX + G - 1) / G < NCH ? (WALK_FIX + G - 1) / G : NCH;
-    static_assert(NCH * G == WALK_REG, "WALK_REG: a multiple of 16");
+    static_assert(NCH * G == walk_reg<G, TP>() && NCH >= 1, "register entries: a multiple of G");
     constexpr int GSH = G == 4 ? 2 : G == 8 ? 3 : 4;
     constexpr int CARRY = 0x100 | (G - 1);                        // row_shl:G-1: group lane 0 <- group lane G-1
     extern __shared__ double walk_lds[];                           // [groups of the workgroup][WALK_CAND]
@@ -2975,6 +2990,7 @@ struct tmh_engine {
     // pipeline, round 6: 1.55 against 1.42-1.45 ms per step, same box -- launch order mixes the
     // store-bound night tiles with the VALU-bound day tiles over the launch)
     bool cost_order = false;
+    uint32_t walk_tp_rows = 65536;   // 8-lane walks of this many rows or more: segments_kernel's TP variant
     // kernel timing (tmh_profile_*): event pairs per kernel, read and recycled
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[TMH_K_COUNT];
@@ -3195,6 +3211,8 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
     tmh_engine* e = new (std::nothrow) tmh_engine;
     if (!e) return fail(TMH_E_NOMEM, "out of host memory");
     if (const char* co = std::getenv("TMH_EXP_COST_ORDER")) e->cost_order = std::atoi(co) != 0;
+    // the 8-lane walk's throughput variant from this many walk rows (tests force it on small batches)
+    if (const char* tp = std::getenv("TMH_WALK_TP_ROWS")) e->walk_tp_rows = (uint32_t)std::strtoul(tp, nullptr, 10);
     KParams& k = e->kp;
     memset(&k, 0, sizeof k);
     k.cc_mode = p->cc_mode;
@@ -3649,12 +3667,12 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
     const uint32_t gpw = 16;   // groups (chains) per workgroup
     const dim3 wg((rows + gpw - 1) / gpw), wt(gpw * G);
     const size_t wlds = gpw * WALK_CAND * sizeof(double);
-#define WALK(Q, GG)                                                                                           \
-    hipLaunchKernelGGL((segments_kernel<Q, GG>), wg, wt, wlds, s, eng->dp, v, chain0, n_chains, step0, n_steps, \
-                       eng->gp.clock, pv.events, pv.n_events, sg, prev)
+#define WALK(Q, GG, ...)                                                                                          \
+    hipLaunchKernelGGL((segments_kernel<Q, GG, ##__VA_ARGS__>), wg, wt, wlds, s, eng->dp, v, chain0, n_chains, step0, \
+                       n_steps, eng->gp.clock, pv.events, pv.n_events, sg, prev)
     const bool q = rows < n_chains;   // groups take queued chains
     if (G == 4) { if (q) WALK(true, 4); else WALK(false, 4); }
-    else if (G == 8) { if (q) WALK(true, 8); else WALK(false, 8); }
+    else if (G == 8) { if (q) WALK(true, 8); else if (rows >= eng->walk_tp_rows) WALK(false, 8, true); else WALK(false, 8); }
     else { if (q) WALK(true, 16); else WALK(false, 16); }
 #undef WALK
     hipLaunchKernelGGL(overflow_settle_kernel, dim3(cb), dim3(256), 0, s, n_chains, sg);
