@@ -1370,6 +1370,7 @@ constexpr int WALK_REG = 64;   // sigma entries held in VGPRs per chain (entries
 // VGPRs, 27 spilled) instead of 64 entries at 180 VGPRs (2 waves).  Round 6, same box: C3 3.06
 // against 2.96e11; a latency-bound batch (C4's 16,384 chains, 2 waves per SIMD) keeps the
 // unspilled walk (the TP walk: C4 3.01 against 3.09e11).
+// (a 4-lane TP walk, 16 entries at 3 or 4 waves per SIMD: C3 2.90 / 2.72e11, round 6)
 template <int G, bool TP>
 constexpr int walk_reg()
 {
@@ -1428,7 +1429,7 @@ __global__ __launch_bounds__(256, (walk_waves<G, TP>())) void segments_kernel(Dr
 #endif
     constexpr int NCH = walk_reg<G, TP>() / G;                     // register chunks
     constexpr int NFIX = (WALK_FIX + G - 1) / G < NCH ? (WALK_FIX + G - 1) / G : NCH;
-    static_assert(NCH * G == walk_reg<G, TP>() && NCH >= 1, "register entries: a multiple of G");
+    static_assert(NCH * G == walk_reg<G, TP>() && NCH * G >= 12, "register entries: a multiple of G, >= 12 (reset_sigma)");
     constexpr int GSH = G == 4 ? 2 : G == 8 ? 3 : 4;
     constexpr int CARRY = 0x100 | (G - 1);                        // row_shl:G-1: group lane 0 <- group lane G-1
     extern __shared__ double walk_lds[];                           // [groups of the workgroup][WALK_CAND]
