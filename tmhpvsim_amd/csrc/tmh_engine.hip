@@ -1371,15 +1371,23 @@ constexpr int WALK_REG = 64;   // sigma entries held in VGPRs per chain (entries
 // against 2.96e11; a latency-bound batch (C4's 16,384 chains, 2 waves per SIMD) keeps the
 // unspilled walk (the TP walk: C4 3.01 against 3.09e11).
 // (a 4-lane TP walk, 16 entries at 3 or 4 waves per SIMD: C3 2.90 / 2.72e11, round 6)
+// the 16-lane walk (latency-bound batches: C2, C5) -- A/B builds: its register entries and minimum
+// waves per SIMD (its VGPRs decide how many expansion waves fit beside two walk waves)
+#ifndef TMH_WALK16_REG
+#define TMH_WALK16_REG WALK_REG
+#endif
+#ifndef TMH_WALK16_WAVES
+#define TMH_WALK16_WAVES 1
+#endif
 template <int G, bool TP>
 constexpr int walk_reg()
 {
-    return TP ? 32 : WALK_REG;
+    return TP ? 32 : (G == 16 ? TMH_WALK16_REG : WALK_REG);
 }
 template <int G, bool TP>
 constexpr int walk_waves()
 {
-    return TP ? 4 : 1;
+    return TP ? 4 : (G == 16 ? TMH_WALK16_WAVES : 1);
 }
 constexpr int WALK_FIX = 16;   // entries scanned unconditionally (one chunk at G = 16); the rest only when some chain of the wave needs them
 static_assert(WALK_FIX >= 12, "reset_sigma writes up to 11 entries into the unconditional chunks");
