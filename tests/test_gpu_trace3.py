@@ -338,3 +338,35 @@ def test_pipelines_closed_in_turn_release_their_streams():
         with pytest.raises(RuntimeError, match="closed"):
             pipe.run(0, 1)
     assert peak == per, (peak, per)
+
+
+def test_compacted_pipeline_closed_exits_cleanly(tmp_path):
+    """Lifecycle: a compacted (C5-shape) pipeline copies each window's live count to pinned
+    host memory on its context's stream; PyTorch's host allocator records an event on that
+    stream when the buffer is freed.  close() frees those buffers before it releases the
+    streams, so a process that closes its pipeline and exits ends with status 0 (round 6:
+    bench.py --workload c5 printed its line, then aborted at exit with 'invalid resource
+    handle').  Run in a child process: the failure is an abort at interpreter exit."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "c5_close.py"
+    script.write_text(
+        "import sys, torch\n"
+        f"sys.path.insert(0, {root!r})\n"
+        "from tmhpvsim_amd.engine import BatchedSim\n"
+        "from tmhpvsim_amd.params import CC_MARKOV, ModelParams, site_grid, site_shape_tables\n"
+        "from tmhpvsim_amd.pipeline import BatchPipeline, pipeline_defaults\n"
+        "n, secs = 256, 2 * 86400\n"
+        "kw = dict(shape_tables=site_shape_tables(n), sites=site_grid(16, 16))\n"
+        "sim = BatchedSim(n, '2019-09-05 00:00:00', tz='Europe/Berlin', params=ModelParams(cc_mode=CC_MARKOV),\n"
+        "                 device='cuda:0', horizon=secs, **kw)\n"
+        "cfg = pipeline_defaults('c5', seconds=secs)\n"
+        "pipe = BatchPipeline(sim, n, secs, cfg, lambda k: 9_000_000 + k * n, torch.device('cuda:0'))\n"
+        "pipe.run(0, len(pipe.ctxs))\n"
+        "pipe.sync()\n"
+        "pipe.close()\n"
+        "print('closed', flush=True)\n")
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "closed" in r.stdout, (r.returncode, r.stderr[-2000:])

@@ -1973,14 +1973,18 @@ constexpr int PVF_VGPR = TMH_PVF_VGPR;   // leading PVF fields pinned in VGPRs i
 //    8 KB, + 12 KB staging: 8 workgroups per CU; +6 % over 5 waves);
 //  fp64 single-site: 4 = at most 128 VGPRs (the trace kernel takes 110, no VGPR spills since the
 //    round-4 PV-constant and table changes; 5 waves = 96 VGPRs spill 14 and run 6 % slower, round 5);
-//  per-chain sites (C5): 2 (a few spills) is 35 % faster than 1
+//  per-chain sites (C5): 3 = at most 168 VGPRs (12-18 spilled): C5 5.36 against 4.47e10 at 2 (206 VGPRs,
+//    round 6, same box) and 4.37e10 at 4 (79 spilled); 2 was 35 % faster than 1 (round 2)
 template <typename R, int OUT, bool SITES>
 constexpr int exp_waves()
 {
 #ifndef TMH_EXP_WAVES_F64
 #define TMH_EXP_WAVES_F64 4
 #endif
-    return SITES ? 2 : (sizeof(R) == 8 ? TMH_EXP_WAVES_F64 : (out_base(OUT) == OUT_TRACE3 ? (TMH_ROW_LDS ? TMH_ROW_LDS_WAVES : TMH_EXP_WAVES_TRACE) : 6));
+#ifndef TMH_EXP_WAVES_SITES
+#define TMH_EXP_WAVES_SITES 3
+#endif
+    return SITES ? TMH_EXP_WAVES_SITES : (sizeof(R) == 8 ? TMH_EXP_WAVES_F64 : (out_base(OUT) == OUT_TRACE3 ? (TMH_ROW_LDS ? TMH_ROW_LDS_WAVES : TMH_EXP_WAVES_TRACE) : 6));
 }
 // One (128-second block b, chain block cblk) tile of the expansion: one work-item per
 // chain of the block (the expansion's unit of work, below).  The LDS staging areas are

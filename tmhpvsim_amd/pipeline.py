@@ -253,6 +253,12 @@ class BatchPipeline:
         if self._closed:
             return
         self.torch.cuda.synchronize(self.dev)
+        # a pinned host tensor copied to on a stream (the compacted windows' live counts) records
+        # an event on that stream when it is freed: free them while the streams exist (freed after
+        # release_stream, the event record fails and aborts the process, e.g. at interpreter exit)
+        for cx in self.ctxs:
+            if getattr(cx, "nlive_host", None) is not None:
+                cx.nlive_host = None
         for st in self._owned:
             st.synchronize()
             _lib.release_stream(st)
