@@ -2371,7 +2371,10 @@ __device__ __forceinline__ void expand_tile(uint32_t b, uint32_t cblk, const KPa
     };
     // (fp32 single-site only: in the fp64 and per-site kernels, which sit at their
     // register bounds, the second copy adds spills)
-    if (sizeof(R) == 4 && !SITES && wave_ok) loops(std::true_type{});
+#ifndef TMH_EXP_FF_F64
+#define TMH_EXP_FF_F64 0   // the fault-free loop copy for the fp64 single-site kernels too (A/B builds)
+#endif
+    if ((sizeof(R) == 4 || (TMH_EXP_FF_F64 && out_base(OUT) == OUT_TRACE3)) && !SITES && wave_ok) loops(std::true_type{});
     else loops(std::false_type{});
     if constexpr (sizeof(R) == 4) {
         const uint4 hm = held_lds[threadIdx.x];
