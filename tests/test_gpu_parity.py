@@ -565,19 +565,24 @@ def test_walk_lanes_invariance(window, markov, start):
     tab = site_shape_tables(n) if markov else None
     outs = []
     # tp: the 8-lane walk's throughput variant (32 register entries, 4 waves per SIMD: C3's
-    # batches), forced on this small batch through the engine's row threshold
-    for lanes, cpr, order, tp in ((16, 1, 1, 0), (16, 1, 0, 0), (8, 1, 1, 0), (4, 1, 1, 0), (4, 3, 1, 0), (4, 3, 0, 0),
-                                  (8, 2, 1, 0), (8, 1, 1, 1), (8, 1, 0, 1)):
-        old = os.environ.get("TMH_WALK_TP_ROWS")
-        os.environ["TMH_WALK_TP_ROWS"] = "1" if tp else "4294967295"
+    # batches), forced on this small batch through the engine's row threshold; mk: markov mode's
+    # hour quantiles precomputed by event_draws_kernel (the default at this size) or drawn in
+    # markov_cc_kernel's walk (0: a full C5 batch's path)
+    for lanes, cpr, order, tp, mk in ((16, 1, 1, 0, 1), (16, 1, 0, 0, 1), (8, 1, 1, 0, 1), (4, 1, 1, 0, 1),
+                                      (4, 3, 1, 0, 1), (4, 3, 0, 0, 1), (8, 2, 1, 0, 1), (8, 1, 1, 1, 1),
+                                      (8, 1, 0, 1, 1), (16, 1, 1, 0, 0)):
+        env = {"TMH_WALK_TP_ROWS": "1" if tp else "4294967295", "TMH_MK_PRE_MAX": "4294967295" if mk else "0"}
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
         try:
             s = _sim(n, start, tz="Europe/Berlin", mp=mp, prec="fp32", kernel_path="time_parallel", horizon=steps,
                      tables=tab)
         finally:
-            if old is None:
-                del os.environ["TMH_WALK_TP_ROWS"]
-            else:
-                os.environ["TMH_WALK_TP_ROWS"] = old
+            for k, v in old.items():
+                if v is None:
+                    del os.environ[k]
+                else:
+                    os.environ[k] = v
         _lib.check(L.tmh_set_walk_lanes(s._eng, lanes))
         _lib.check(L.tmh_set_walk_chains_per_row(s._eng, cpr))
         _lib.check(L.tmh_set_walk_order(s._eng, order))   # rows windiest chain first, or in chain order

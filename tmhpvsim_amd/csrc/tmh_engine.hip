@@ -584,9 +584,34 @@ __global__ __launch_bounds__(256) void desc_kernel(int64_t step0, uint32_t n, in
 }
 
 // ------------------------------------------------------------ boundary draws
-// _next_day / _next_hour draws of every (event, chain): clearskyindexmodel.py:101-107
-__global__ __launch_bounds__(256) void event_draws_kernel(DrawParams dp, uint64_t chain0, uint32_t n, uint32_t nsteps,
-                                                          const int2* __restrict__ events,
+// markov mode: the first Student-t bin of chain slot c's shape table (the reference's table has
+// one, bin 2: cloud_cover_hourly.py:282-288,314) and its degrees of freedom; -1 when none
+__device__ __forceinline__ int first_t_bin(const KParams& kp, uint32_t c, double& df)
+{
+    const uint32_t r = gid(kp.ids, c);   // the table row of the slot's chain
+    for (int b = 0; b < 6; ++b) {
+        const int t = kp.tab && kp.tab_t ? kp.tab_t[(size_t)r * 6 + b] : kp.is_t[b];
+        if (t) {
+            df = kp.tab ? kp.tab[(size_t)r * 24 + 4 * b + 3] : kp.shapes[b][3];
+            return b;
+        }
+    }
+    df = 0.0;
+    return -1;
+}
+
+// _next_day / _next_hour draws of every (event, chain): clearskyindexmodel.py:101-107.
+// Markov mode (round 6): the hour's Student-t quantile of the chain's first t bin,
+// stdtrit(df, u) of the hour's uniform, into the cc slot (evd[e][0]): it does not depend on the
+// hour-to-hour state, so it is drawn here for every (hour, chain) at full occupancy, and
+// markov_cc_kernel's one-lane-per-chain walk takes it when the state's bin is that bin (the same
+// function of the same values, so bit for bit what it computed in line).  Only for batches of at
+// most the engine's mk_pre_max chains (the walk is latency-bound there: C5's N = 8 shard, 8,192
+// chains, 3.13 -> 4.14e10 live chain-s/s); a full C5 batch (65,536) computes the quantile in the
+// walk, only for the hours whose state sits in the t bin (precomputed: 5.36 -> 4.96e10).  mk_pre:
+// this launch precomputes (markov_cc_kernel's tb = -1 otherwise).
+__global__ __launch_bounds__(256) void event_draws_kernel(DrawParams dp, KParams kp, bool mk_pre, uint64_t chain0,
+                                                          uint32_t n, uint32_t nsteps, const int2* __restrict__ events,
                                                           const uint32_t* __restrict__ n_events, double* evd,
                                                           uint32_t* identity_order, uint32_t* identity_rank)
 {
@@ -607,7 +632,13 @@ __global__ __launch_bounds__(256) void event_draws_kernel(DrawParams dp, uint64_
     }
     if (fl & FL_HOUR) {
         const U4 u = keyed_block(dp.seed, chain, step, TAG_BOUNDARY, 1);
-        if (!dp.markov) o[0] = cc_faithful(dp, gid(dp.ids, c), u52(u.x, u.y));
+        if (!dp.markov) {
+            o[0] = cc_faithful(dp, gid(dp.ids, c), u52(u.x, u.y));
+        } else if (mk_pre) {
+            double df;
+            const int tb = first_t_bin(kp, c, df);
+            o[0] = tb >= 0 ? stdtrit(df, u52(u.x, u.y)) : 0.0;
+        }
         o[3 * (size_t)n] = normal(u52(u.z, u.w), 0.99, 0.08);
     }
 }
@@ -629,7 +660,7 @@ __global__ __launch_bounds__(256) void event_draws_kernel(DrawParams dp, uint64_
 // Student-t flags (bin 2 of the reference's table, cloud_cover_hourly.py:314),
 // so a wave whose lanes all sit in AL bins never enters stdtrit.
 constexpr int MK_BLOCK = 256;
-__global__ __launch_bounds__(MK_BLOCK) void markov_cc_kernel(KParams kp, StateView st, uint64_t chain0, uint32_t n,
+__global__ __launch_bounds__(MK_BLOCK) void markov_cc_kernel(KParams kp, bool mk_pre, StateView st, uint64_t chain0, uint32_t n,
                                                         uint32_t nsteps, const int2* __restrict__ events,
                                                         const uint32_t* __restrict__ n_events, double* evd,
                                                         PrevView prev)
@@ -659,9 +690,15 @@ __global__ __launch_bounds__(MK_BLOCK) void markov_cc_kernel(KParams kp, StateVi
     const double* row = kp.tab ? reinterpret_cast<const double*>(tab_s) + threadIdx.x * 24 : nullptr;
     const int32_t* rowt = tabt_s + threadIdx.x * 6;
     double state = prev.status ? prev.end_p1[(size_t)n + c] : st.mstate[c];   // the last hourly draw
+    // the first Student-t bin, whose quantile event_draws_kernel left in the hour's cc slot
+    int tb = -1;
+    if (mk_pre)
+        for (int b = 5; b >= 0; --b)
+            if (row ? rowt[b] : kp.is_t[b]) tb = b;
     for (uint32_t e = 0; e < ne; ++e) {
         const int2 ev = events[e];
         if (!(ev.y & FL_HOUR)) continue;
+        const double qt = mk_pre ? evd[(size_t)e * 4 * n + c] : 0.0;   // stdtrit(df of bin tb, u): event_draws_kernel
         const U4 u4 = keyed_block(kp.seed, chain, (uint64_t)ev.x, TAG_BOUNDARY, 1);
         const double u = u52(u4.x, u4.y);
         int bin = 5;   // np.searchsorted(bins, state): the first bin whose right edge is >= state
@@ -683,10 +720,12 @@ __global__ __launch_bounds__(MK_BLOCK) void markov_cc_kernel(KParams kp, StateVi
             df = kp.shapes[bin][3];
             is_t = kp.is_t[bin];
         }
-        const uint64_t tl = __builtin_amdgcn_ballot_w64(is_t != 0);
+        // a t bin other than tb (none in the reference's table) draws its quantile here
+        const bool t_here = is_t && bin != tb;
+        const uint64_t tl = __builtin_amdgcn_ballot_w64(t_here);
         const uint64_t al = __builtin_amdgcn_ballot_w64(is_t == 0);
-        double v = 0.0;
-        if (tl && is_t) v = stdtrit(df, u);
+        double v = is_t ? qt : 0.0;
+        if (tl && t_here) v = stdtrit(df, u);
         if (al && !is_t) v = al_ppf(u, kappa);
         v = v * scale + loc;                              // scipy rvs: vals * scale + loc
         const double x = state + v;
@@ -3007,6 +3046,7 @@ struct tmh_engine {
     // store-bound night tiles with the VALU-bound day tiles over the launch)
     bool cost_order = false;
     uint32_t walk_tp_rows = 65536;   // 8-lane walks of this many rows or more: segments_kernel's TP variant
+    uint32_t mk_pre_max = 16384;     // markov batches of at most this many chains: hour quantiles precomputed
     // kernel timing (tmh_profile_*): event pairs per kernel, read and recycled
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof[TMH_K_COUNT];
@@ -3229,6 +3269,8 @@ int tmh_engine_create(const tmh_params* p, const tmh_clock* clock, int device, s
     if (const char* co = std::getenv("TMH_EXP_COST_ORDER")) e->cost_order = std::atoi(co) != 0;
     // the 8-lane walk's throughput variant from this many walk rows (tests force it on small batches)
     if (const char* tp = std::getenv("TMH_WALK_TP_ROWS")) e->walk_tp_rows = (uint32_t)std::strtoul(tp, nullptr, 10);
+    // the markov walk's precomputed Student-t quantiles up to this batch size (tests force either path)
+    if (const char* mp = std::getenv("TMH_MK_PRE_MAX")) e->mk_pre_max = (uint32_t)std::strtoul(mp, nullptr, 10);
     KParams& k = e->kp;
     memset(&k, 0, sizeof k);
     k.cc_mode = p->cc_mode;
@@ -3649,11 +3691,12 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
         // the walk rows' order, read by the candidate table's layout and by the walk: computed
         // here (tmh_set_walk_order before a window's draws), so the walk uses the order its
         // window's draws were made with whatever the engine's flag says when it runs
-        hipLaunchKernelGGL(event_draws_kernel, dim3(sg.evcap, cb), dim3(256), 0, s, eng->dp, chain0, n_chains, n_steps,
+        const bool mk_pre = eng->dp.markov && n_chains <= eng->mk_pre_max;
+        hipLaunchKernelGGL(event_draws_kernel, dim3(sg.evcap, cb), dim3(256), 0, s, eng->dp, eng->kp, mk_pre, chain0, n_chains, n_steps,
                            pv.events, pv.n_events, sg.evd, eng->walk_order ? nullptr : sg.order,
                            eng->walk_order ? nullptr : sg.rank);
         if (eng->dp.markov)
-            hipLaunchKernelGGL(markov_cc_kernel, dim3(cb), dim3(256), 0, s, eng->kp, v, chain0, n_chains, n_steps,
+            hipLaunchKernelGGL(markov_cc_kernel, dim3(cb), dim3(256), 0, s, eng->kp, mk_pre, v, chain0, n_chains, n_steps,
                                pv.events, pv.n_events, sg.evd, prev);
         if (eng->walk_order)
             hipLaunchKernelGGL(walk_order_kernel, dim3((n_chains + ORDER_TILE - 1) / ORDER_TILE), dim3(1024), 0, s, v,
