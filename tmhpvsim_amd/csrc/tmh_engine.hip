@@ -1279,12 +1279,15 @@ __device__ __forceinline__ void fractions_at(const WinClock& w, int32_t j, const
 // chain-days), and a walk wavefront runs as many iterations as the busiest of its 4
 // (16) chains: grouping chains of similar wind cuts the wavefronts' iterations by 11 %
 // (17 % at 16 chains per wavefront), and the busiest wavefronts are dispatched first.
-// Faulted chains last.  Bitonic sort of (key, chain) per tile of ORDER_TILE rows in LDS.
+// Faulted chains last.  Bitonic sort of (key, chain) per tile of ORDER_TILE rows in LDS
+// (walk_order_kernel), or for small batches a rank sort (walk_rank_kernel, the same permutation).
 // The walk's results do not depend on the order (each group walks its own chain).  The
 // try-0 candidate table is stored by walk row (draws_tail_kernel writes row rank[c]), so
 // a wavefront's candidate loads stay on shared cache lines as in chain order (read by
 // chain, the scattered rows made the 16-chain C3 walk 3.7x slower).
 constexpr uint32_t ORDER_TILE = 4096;
+constexpr uint32_t ORDER_EPB = 64;   // walk_rank_kernel: tile entries ranked per workgroup (4 waves: a quarter of the tile each)
+constexpr uint32_t WALK_RANK_TILES = 4;   // up to this many tiles the rank sort (O(tile^2) compares per tile, 64 workgroups)
 __global__ __launch_bounds__(1024) void walk_order_kernel(StateView st, uint32_t n, SegView sg, PrevView prev)
 {
     __shared__ unsigned long long v[ORDER_TILE];
@@ -1321,6 +1324,48 @@ __global__ __launch_bounds__(1024) void walk_order_kernel(StateView st, uint32_t
         const uint32_t c = 0xFFFFFFFFu - (uint32_t)~v[i];
         sg.order[t0 + i] = c;
         sg.rank[c] = t0 + i;
+    }
+}
+
+// Batches of at most WALK_RANK_TILES tiles (C2, C4): the same permutation by a rank sort.
+__global__ __launch_bounds__(256) void walk_rank_kernel(StateView st, uint32_t n, SegView sg, PrevView prev)
+{
+    // round 6: a rank sort.  Every workgroup loads its tile's keys into LDS and ranks 64 of them
+    // (each wave counts the smaller keys in a quarter of the tile, broadcast LDS reads); the
+    // rank of a key among the tile's is its place in the ascending order, so the permutation is
+    // the bitonic sort's of round 2 bit for bit (keys are unique: the chain id is in the low word),
+    // in 64 workgroups per tile instead of one workgroup's 78 barrier stages (79 us per C2 batch).
+    __shared__ unsigned long long v[ORDER_TILE];
+    __shared__ uint32_t part[4][ORDER_EPB];
+    constexpr uint32_t SUBS = ORDER_TILE / ORDER_EPB;
+    const uint32_t t0 = (blockIdx.x / SUBS) * ORDER_TILE;
+    const uint32_t m = min(ORDER_TILE, n - t0);   // the tile's chains (a partial last tile has no padding keys)
+    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+        const uint32_t c = t0 + i;
+        const bool ok = (prev.status ? prev.status[c] : st.status[c]) == 0;
+        const double w = prev.status ? prev.end_p1[2 * (size_t)n + c] + prev.end_p1[3 * (size_t)n + c]
+                                     : st.sb[S_WS][c] + st.sa[S_WS][c];
+        const uint32_t kb = ok && w > 0.0 ? __float_as_uint((float)w) : 0u;   // positive floats order as their bits
+        // ascending order of the complement: larger key first, then the lower chain
+        v[i] = ~(((unsigned long long)kb << 32) | (0xFFFFFFFFu - c));
+    }
+    __syncthreads();
+    const uint32_t e = (blockIdx.x % SUBS) * ORDER_EPB + (threadIdx.x & (ORDER_EPB - 1));   // entry in the tile
+    const uint32_t q = threadIdx.x / ORDER_EPB;                                               // quarter (wave)
+    uint32_t cnt = 0;
+    if (e < m) {
+        const unsigned long long me = v[e];
+        const uint32_t j1 = min((q + 1) * (ORDER_TILE / 4), m);
+#pragma unroll 8
+        for (uint32_t j = q * (ORDER_TILE / 4); j < j1; ++j) cnt += v[j] < me ? 1u : 0u;
+    }
+    part[q][threadIdx.x & (ORDER_EPB - 1)] = cnt;
+    __syncthreads();
+    if (q == 0 && e < m) {
+        const uint32_t r = part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] + part[3][threadIdx.x];
+        const uint32_t c = t0 + e;
+        sg.order[t0 + r] = c;
+        sg.rank[c] = t0 + r;
     }
 }
 
@@ -2643,8 +2688,11 @@ __global__ __launch_bounds__(256) void state_move_kernel(StateView src, StateVie
 // (record, second) a work-item: ~1 flagged second in 20 per wave, 95 us per C2 batch.)
 // Grid-stride over the record groups.
 constexpr uint32_t FIX_RPW = 16;
+#ifndef TMH_FIX_WAVES_SITES
+#define TMH_FIX_WAVES_SITES 1   // min waves per SIMD of the per-site fixup (its fp64 redo recomputes the site's geometry)
+#endif
 template <bool SITES>
-__global__ __launch_bounds__(64) void fixup_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
+__global__ __launch_bounds__(64, (SITES ? TMH_FIX_WAVES_SITES : 1)) void fixup_kernel(KParams kp, DrawParams dp, StateView st, uint64_t chain0, uint32_t n,
                                                     int64_t W0, uint32_t nsteps, int64_t utc0,
                                                     const double* __restrict__ tab64, const float* __restrict__ tab32,
                                                     const double* __restrict__ sun,
@@ -3699,8 +3747,14 @@ static int step_phases(struct tmh_engine* eng, void* state, uint64_t chain0, uin
             hipLaunchKernelGGL(markov_cc_kernel, dim3(cb), dim3(256), 0, s, eng->kp, mk_pre, v, chain0, n_chains, n_steps,
                                pv.events, pv.n_events, sg.evd, prev);
         if (eng->walk_order)
-            hipLaunchKernelGGL(walk_order_kernel, dim3((n_chains + ORDER_TILE - 1) / ORDER_TILE), dim3(1024), 0, s, v,
-                               n_chains, sg, prev);
+        {
+            const uint32_t tiles = (n_chains + ORDER_TILE - 1) / ORDER_TILE;
+            if (tiles <= WALK_RANK_TILES)   // small batches (latency-bound on the construction stream): the rank sort
+                hipLaunchKernelGGL(walk_rank_kernel, dim3(tiles * (ORDER_TILE / ORDER_EPB)), dim3(256), 0, s, v, n_chains,
+                                   sg, prev);
+            else
+                hipLaunchKernelGGL(walk_order_kernel, dim3(tiles), dim3(1024), 0, s, v, n_chains, sg, prev);
+        }
         hipEvent_t t_cand = eng->mark(s);
         {   // candidates + the window's minute draws (+ counter resets), one launch
             const int64_t fmh = first_minute_host(utc0, step0);
