@@ -31,6 +31,8 @@ class PipelineConfig:
     pipeline: int = 5            # contexts (batches in flight)
     walks: int = 2               # gated schedule: segment walks in flight
     build_ahead: int = 4         # gated: construction of batch k + A released when walk k ends
+    plan_stream: bool = False    # gated: each construction's plan on a stream of its own, beside its
+                                 # chains' init (the draws wait for both)
     build_streams: int = 1       # gated: constructions on this many streams in turn (2: consecutive
                                  # batches' constructions may overlap; their kernels are latency-bound)
     stagger: bool = True         # one-window batches software-pipelined (else one tmh_step each, in turn)
@@ -211,13 +213,14 @@ class BatchPipeline:
         # order across the streams sharing it, so streams nobody uses are not created (bench.py
         # raises the queues to 32 for these workloads' 3 streams per context).
         W = self.W = max(1, cfg.walks)
-        self.estream = self.bst = self._cst = None
+        self.estream = self.bst = self._cst = self.psts = None
         self.wsts = []
         if nwin == 1:
             self.estream = mk(cfg.expand_priority)
             self.wsts = [mk(cfg.walk_priority) for _ in range(W)]
             self.bst = mk(cfg.build_priority)
             self.bsts = [self.bst] + [mk(cfg.build_priority) for _ in range(max(1, cfg.build_streams) - 1)]
+            self.psts = mk(cfg.build_priority) if cfg.plan_stream else None
             if cfg.walk_cus:   # the walks on a share of every XCD's CUs (CU-masked streams)
                 ncu = torch.cuda.get_device_properties(device).multi_processor_count
                 self.wsts = [own(_lib.cu_stream(0, cfg.walk_cus, device)) for _ in range(W)]
@@ -451,8 +454,21 @@ class BatchPipeline:
             bst.wait_event(gate)
         if cx.expanded is not None:                        # the context's previous batch is committed
             bst.wait_event(cx.expanded)
-        _lib.check(L.tmh_init(sim._eng, self._p(cx.state), cx.chain0, self.n, None, bp))
-        _lib.check(L.tmh_plan(sim._eng, 0, self.secs, self._p(cx.plan), bp))
+        if self.psts is not None:   # the plan beside the chains' init, on its own stream
+            pst = self.psts
+            if gate is not None:
+                pst.wait_event(gate)
+            if cx.expanded is not None:   # the previous batch of this context read the plan
+                pst.wait_event(cx.expanded)
+            _lib.check(L.tmh_plan(sim._eng, 0, self.secs, self._p(cx.plan), C.c_void_p(pst.cuda_stream)))
+            if getattr(cx, "planned", None) is None:
+                cx.planned = self.torch.cuda.Event()
+            cx.planned.record(pst)
+            _lib.check(L.tmh_init(sim._eng, self._p(cx.state), cx.chain0, self.n, None, bp))
+            bst.wait_event(cx.planned)
+        else:
+            _lib.check(L.tmh_init(sim._eng, self._p(cx.state), cx.chain0, self.n, None, bp))
+            _lib.check(L.tmh_plan(sim._eng, 0, self.secs, self._p(cx.plan), bp))
         _lib.check(L.tmh_walk_part(sim._eng, self._p(cx.state), cx.chain0, self.n, 0, self.secs, self._p(cx.plan),
                                    self._p(cx.scratch), cx.scratch.numel(), None, 0, _lib.WALK_DRAWS, bp))
         cx.done.record(bst)
