@@ -1224,6 +1224,9 @@ __device__ __forceinline__ PP lds_fence(PP p)
 // keep the multiply-add form: fused as well, the trace kernel took 122 VGPRs instead of 110,
 // i.e. two waves per SIMD beside a 146-VGPR walk wave instead of three (measured: alone
 // 2.74 against 2.89 ms, in the pipeline 3.05 against 2.94 ms).
+#ifndef TMH_DISC64_HORNER
+#define TMH_DISC64_HORNER 0   // A/B builds: 9 fmas, but 33 VGPRs spilled in the fp64 trace loop (2.99-3.07 against 2.55-2.70 ms alone, round 6)
+#endif
 template <typename PP, typename LT>
 __device__ __forceinline__ double pv_power_d(PP p, const double* g, double csi, LT lt)
 {
@@ -1232,8 +1235,22 @@ __device__ __forceinline__ double pv_power_d(PP p, const double* g, double csi, 
     double kt = c * g[G_KTC];
     kt = kt > 0.0 ? kt : 0.0;
     kt = kt < 1.0 ? kt : 1.0;
-    const double am = g[G_AM], kt2 = kt * kt, kt3 = kt2 * kt;
+    const double am = g[G_AM];
     double a, b, cc;
+#if TMH_DISC64_HORNER
+    // Horner with fmas (round 6): within ~1e-16 relative of pvmodel.py's power form (the fp64
+    // bar is 1e-12), 9 fmas instead of 14 multiplies and adds
+    if (kt <= 0.6) {
+        a = fma(fma(fma(-2.222, kt, 2.286), kt, -1.56), kt, 0.512);
+        b = fma(0.962, kt, 0.37);
+        cc = fma(fma(-2.048, kt, 0.932), kt, -0.28);
+    } else {
+        a = fma(fma(fma(11.56, kt, -27.49), kt, 21.77), kt, -5.743);
+        b = fma(fma(fma(31.9, kt, 66.05), kt, -118.5), kt, 41.4);
+        cc = fma(fma(fma(73.81, kt, -222.0), kt, 184.2), kt, -47.01);
+    }
+#else
+    const double kt2 = kt * kt, kt3 = kt2 * kt;
     if (kt <= 0.6) {
         a = 0.512 - 1.56 * kt + 2.286 * kt2 - 2.222 * kt3;
         b = 0.37 + 0.962 * kt;
@@ -1243,6 +1260,7 @@ __device__ __forceinline__ double pv_power_d(PP p, const double* g, double csi, 
         b = 41.4 - 118.5 * kt + 66.05 * kt2 + 31.9 * kt3;
         cc = -47.01 + 184.2 * kt - 222.0 * kt2 + 73.81 * kt3;
     }
+#endif
     double ex;
     if constexpr (__is_same(LT, decltype(nullptr))) ex = exp_tab(cc * am, (const double*)g_pv_tab);
     else ex = exp_tab(cc * am, lt);
