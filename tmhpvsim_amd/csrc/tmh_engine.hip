@@ -2065,10 +2065,13 @@ constexpr int exp_waves()
 #ifndef TMH_EXP_WAVES_F64
 #define TMH_EXP_WAVES_F64 4
 #endif
+#ifndef TMH_EXP_WAVES_STATS
+#define TMH_EXP_WAVES_STATS 6
+#endif
 #ifndef TMH_EXP_WAVES_SITES
 #define TMH_EXP_WAVES_SITES 3
 #endif
-    return SITES ? TMH_EXP_WAVES_SITES : (sizeof(R) == 8 ? TMH_EXP_WAVES_F64 : (out_base(OUT) == OUT_TRACE3 ? (TMH_ROW_LDS ? TMH_ROW_LDS_WAVES : TMH_EXP_WAVES_TRACE) : 6));
+    return SITES ? TMH_EXP_WAVES_SITES : (sizeof(R) == 8 ? TMH_EXP_WAVES_F64 : (out_base(OUT) == OUT_TRACE3 ? (TMH_ROW_LDS ? TMH_ROW_LDS_WAVES : TMH_EXP_WAVES_TRACE) : TMH_EXP_WAVES_STATS));
 }
 // One (128-second block b, chain block cblk) tile of the expansion: one work-item per
 // chain of the block (the expansion's unit of work, below).  The LDS staging areas are
