@@ -35,6 +35,13 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+
+// min waves per SIMD of the construction kernels (init, variates, geometry, boundary draws), i.e.
+// their VGPR bound: beside the expansion (72-VGPR waves) a wave that needs more registers than
+// one expansion wave frees waits for several to retire (A/B builds)
+#ifndef TMH_BUILD_WAVES
+#define TMH_BUILD_WAVES 4   // geom_kernel 146 -> 128 VGPRs (38 spilled): C2 +0.9 % over three pairs, round 6
+#endif
 #include <cstring>
 #include <string>
 #include <type_traits>
@@ -205,7 +212,7 @@ __device__ __forceinline__ void init_cc_pair(const KParams& kp, uint32_t c, cons
     a = draw_cc(kp, gid(kp.ids, c), ch, u[1]);
 }
 
-__global__ __launch_bounds__(256) void init_variates_kernel(KParams kp, StateView st, uint64_t chain0, uint32_t n,
+__global__ __launch_bounds__(256, TMH_BUILD_WAVES) void init_variates_kernel(KParams kp, StateView st, uint64_t chain0, uint32_t n,
                                                             double hf)
 {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -236,7 +243,7 @@ __global__ __launch_bounds__(256) void init_variates_kernel(KParams kp, StateVie
 
 // ClearskyindexModel.__init__ (clearskyindexmodel.py:57-99)
 template <int RNG>
-__global__ __launch_bounds__(256) void init_kernel(KParams kp, StateView st, uint64_t chain0, uint32_t n,
+__global__ __launch_bounds__(256, TMH_BUILD_WAVES) void init_kernel(KParams kp, StateView st, uint64_t chain0, uint32_t n,
                                                    double hf, InjView inj)
 {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -328,7 +335,7 @@ __global__ __launch_bounds__(256) void init_kernel(KParams kp, StateView st, uin
 }
 
 // ------------------------------------------------------------ plan kernels
-__global__ __launch_bounds__(256) void geom_kernel(GParams gp, int64_t step0, uint32_t n, double* tab64,
+__global__ __launch_bounds__(256, TMH_BUILD_WAVES) void geom_kernel(GParams gp, int64_t step0, uint32_t n, double* tab64,
                                                    float* tab32, double* sun)
 {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -610,7 +617,7 @@ __device__ __forceinline__ int first_t_bin(const KParams& kp, uint32_t c, double
 // chains, 3.13 -> 4.14e10 live chain-s/s); a full C5 batch (65,536) computes the quantile in the
 // walk, only for the hours whose state sits in the t bin (precomputed: 5.36 -> 4.96e10).  mk_pre:
 // this launch precomputes (markov_cc_kernel's tb = -1 otherwise).
-__global__ __launch_bounds__(256) void event_draws_kernel(DrawParams dp, KParams kp, bool mk_pre, uint64_t chain0,
+__global__ __launch_bounds__(256, TMH_BUILD_WAVES) void event_draws_kernel(DrawParams dp, KParams kp, bool mk_pre, uint64_t chain0,
                                                           uint32_t n, uint32_t nsteps, const int2* __restrict__ events,
                                                           const uint32_t* __restrict__ n_events, double* evd,
                                                           uint32_t* identity_order, uint32_t* identity_rank)
