@@ -43,6 +43,7 @@ class PipelineConfig:
     build_priority: str = "normal"
     commit_stream: bool = False  # gated: fixup + commit on a stream of their own
     walk_order: bool = True      # walk rows windiest chain first (the run's first walk in chain order)
+    drain_order: bool = True     # gated: the run's last walk in chain order too (it drains the pipeline)
     walk_cus: int = 0            # gated: segment walks on CU-mask bits 0 .. K-1 (0 = all CUs)
     other_cus: str = "all"       # with walk_cus: the other streams on all CUs or the rest
     compact: bool = False        # multi-window stats batches: later windows on the live chains only
@@ -586,7 +587,7 @@ class BatchPipeline:
             # nothing else to do): chain order, whose windiest wavefront is shorter than the wind
             # order's (four windy chains); the wind order for the rest, which run beside expansions
             if cfg.walk_order:
-                _lib.check(L.tmh_set_walk_order(sim._eng, 0 if (j == k0 and W > 1) else 1))
+                _lib.check(L.tmh_set_walk_order(sim._eng, 0 if (j == k0 and W > 1) or self._drains(j, end) else 1))
             if j == k0 and self.split:
                 self.s_build(j)
             else:
@@ -599,6 +600,8 @@ class BatchPipeline:
         for k in range(k0, end):
             gate = self.ctx_of(k).walked
             if k + A < end:
+                if cfg.walk_order:   # the order is read by the construction's draws
+                    _lib.check(L.tmh_set_walk_order(sim._eng, 0 if self._drains(k + A, end) else 1))
                 self.g_build(k + A, gate)
             if k + W < end:
                 self.g_walk(k + W)
@@ -606,6 +609,11 @@ class BatchPipeline:
                 self.s_expand(k)
             else:
                 self.g_expand(k)
+
+    def _drains(self, j, end):
+        """Batch j is the run's last: nothing is left to overlap its walk, so (drain_order) it
+        walks in chain order, whose windiest wavefront is shorter than the wind order's."""
+        return self.cfg.drain_order and self.W > 1 and j == end - 1
 
     def gated(self):
         """Whether `run` takes the gated schedule (one-window, staggered batches)."""
