@@ -223,7 +223,7 @@ def parse():
                     help="gated schedule: when the walk of batch k ends, the construction of batch k + A is "
                          "released (default A = walks + 2 with two or more walks, else walks + 1; needs --pipeline >= A + 1)")
     ap.add_argument("--drain-order", type=int, default=None,
-                    help="gated schedule: the run's last walk in chain order (1, default) or wind order (0)")
+                    help="gated schedule: the run's last N walks in chain order (default 1; 0: wind order)")
     ap.add_argument("--plan-stream", type=int, default=None,
                     help="gated schedule: each construction's plan on a stream of its own beside its chains' init (1)")
     ap.add_argument("--build-streams", type=int, default=None,
@@ -273,7 +273,7 @@ def parse():
                               timeline=a.timeline, queues=a.queues, first_split=a.first_split,
                               build_streams=a.build_streams,
                               plan_stream=None if a.plan_stream is None else bool(a.plan_stream),
-                              drain_order=None if a.drain_order is None else bool(a.drain_order))
+                              drain_order=a.drain_order)
     for k in ("mode", "window", "pipeline", "walks", "build_ahead", "build_streams", "build_on", "walk_priority",
               "compact", "commit_stream"):
         setattr(a, k, getattr(a.cfg, k))

@@ -43,7 +43,7 @@ class PipelineConfig:
     build_priority: str = "normal"
     commit_stream: bool = False  # gated: fixup + commit on a stream of their own
     walk_order: bool = True      # walk rows windiest chain first (the run's first walk in chain order)
-    drain_order: bool = True     # gated: the run's last walk in chain order too (it drains the pipeline)
+    drain_order: int = 1         # gated: the run's last walks in chain order too (they drain the pipeline)
     walk_cus: int = 0            # gated: segment walks on CU-mask bits 0 .. K-1 (0 = all CUs)
     other_cus: str = "all"       # with walk_cus: the other streams on all CUs or the rest
     compact: bool = False        # multi-window stats batches: later windows on the live chains only
@@ -611,9 +611,9 @@ class BatchPipeline:
                 self.g_expand(k)
 
     def _drains(self, j, end):
-        """Batch j is the run's last: nothing is left to overlap its walk, so (drain_order) it
+        """Batch j is among the run's last drain_order: little is left to overlap its walk, so it
         walks in chain order, whose windiest wavefront is shorter than the wind order's."""
-        return self.cfg.drain_order and self.W > 1 and j == end - 1
+        return self.W > 1 and j >= end - int(self.cfg.drain_order)
 
     def gated(self):
         """Whether `run` takes the gated schedule (one-window, staggered batches)."""
